@@ -1,0 +1,782 @@
+// mrgpu_api.hip — the C ABI (include/mrgpu.h): contexts, map/reduce
+// orchestration, intermediate export/import and the RCCL shuffle.
+//
+// Call flow of mrg_map (replaces mr/worker.go:58-92 for a known app):
+//   [H2D copy of the split if host-resident] -> clear HBM tables ->
+//   wc_map_kernel (tokenize + LDS combine + HBM table) -> wc_long_kernel ->
+//   collect (distinct keys -> records, partition = ihash % nReduce).
+// If a table or list overflowed (the status word says which), the capacity is
+// multiplied by 4 and the map is re-run, so results never depend on the
+// initial sizing.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mrgpu.h"
+#include "letter_table.inc"
+#include "mrgpu_internal.h"
+
+using namespace mrg;
+
+namespace {
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = n < 4096 ? 4096 : n;
+        hipError_t e = hipMalloc(&p, c);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    DevBuf() = default;
+    DevBuf(const DevBuf&) = delete;
+    DevBuf& operator=(const DevBuf&) = delete;
+    ~DevBuf() { release(); }
+};
+
+constexpr uint64_t kHostMagic = 0x4D524748424F5354ull;  // "MRGHBOST"
+
+}  // namespace
+
+struct mrg_ctx {
+    int device = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[8] = {};
+    std::string err;
+    uint8_t* d_l1 = nullptr;
+    uint32_t* d_l2 = nullptr;
+    DevBuf sh, lo, list, ctr, staging, pat;
+    int sh_log2 = 22, lo_log2 = 14;
+    uint64_t list_cap = 1u << 20;
+    int grid = 256;
+    ReduceWs* rws = nullptr;
+    mrg_stats stats{};
+    Counters* h_ctr = nullptr;     // pinned
+    uint8_t* h_out = nullptr;      // pinned result buffer for mrg_run_job
+    size_t h_out_cap = 0;
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+};
+
+struct mrg_parts {
+    int app = 0;
+    uint32_t nreduce = 1;
+    int device = 0;
+    Recs r{};
+    void* block = nullptr;  // record arrays
+    uint8_t* arena = nullptr;
+};
+
+static int fail(mrg_ctx* c, int code, const char* fmt, ...) {
+    char b[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(b, sizeof b, fmt, ap);
+    va_end(ap);
+    if (c) c->err = b;
+    return code;
+}
+
+#define HCHK(c, x)                                                                                       \
+    do {                                                                                                 \
+        hipError_t _e = (x);                                                                             \
+        if (_e != hipSuccess)                                                                            \
+            return fail((c), _e == hipErrorOutOfMemory ? MRG_ENOMEM : MRG_EDEVICE, "%s failed: %s (%s:%d)", #x, \
+                        hipGetErrorString(_e), __FILE__, __LINE__);                                      \
+    } while (0)
+
+#define NCHK(c, x)                                                                                  \
+    do {                                                                                            \
+        ncclResult_t _r = (x);                                                                      \
+        if (_r != ncclSuccess) return fail((c), MRG_ECOMM, "%s failed: %s", #x, ncclGetErrorString(_r)); \
+    } while (0)
+
+static int bind(mrg_ctx* c) {
+    HCHK(c, hipSetDevice(c->device));
+    return MRG_OK;
+}
+
+static Tables make_tables(mrg_ctx* c) {
+    Tables t;
+    t.sh = (ShortSlot*)c->sh.p;
+    t.sh_mask = (1ull << c->sh_log2) - 1;
+    t.lo = (LongSlot*)c->lo.p;
+    t.lo_mask = (1ull << c->lo_log2) - 1;
+    t.list = (uint64_t*)c->list.p;
+    t.list_cap = c->list_cap;
+    t.ctr = (Counters*)c->ctr.p;
+    return t;
+}
+
+static int ensure_tables(mrg_ctx* c) {
+    HCHK(c, c->sh.ensure(sizeof(ShortSlot) << c->sh_log2));
+    HCHK(c, c->lo.ensure(sizeof(LongSlot) << c->lo_log2));
+    HCHK(c, c->list.ensure(c->list_cap * sizeof(uint64_t)));
+    HCHK(c, c->ctr.ensure(sizeof(Counters)));
+    return MRG_OK;
+}
+
+static int read_counters(mrg_ctx* c) {
+    HCHK(c, hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->s));
+    HCHK(c, hipStreamSynchronize(c->s));
+    return MRG_OK;
+}
+
+static float ev_ms(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    if (hipEventElapsedTime(&ms, a, b) != hipSuccess) return 0.f;
+    return ms;
+}
+
+// ---------------------------------------------------------------- parts
+static int parts_alloc(mrg_ctx* c, uint64_t n, uint64_t arena_n, int app, uint32_t nreduce, mrg_parts** out) {
+    mrg_parts* p = new mrg_parts();
+    p->app = app;
+    p->nreduce = nreduce;
+    p->device = c->device;
+    uint64_t cap = n ? n : 1;
+    size_t bytes = cap * (8 + 8 + 4 + 8 + 4 + 8) + 256;
+    hipError_t e = hipMalloc(&p->block, bytes);
+    if (e != hipSuccess) { delete p; return fail(c, MRG_ENOMEM, "hipMalloc(%zu) for parts failed", bytes); }
+    e = hipMalloc((void**)&p->arena, arena_n ? arena_n : 16);
+    if (e != hipSuccess) { hipFree(p->block); delete p; return fail(c, MRG_ENOMEM, "hipMalloc arena failed"); }
+    char* b = (char*)p->block;
+    p->r.k0 = (uint64_t*)b; b += cap * 8;
+    p->r.k1 = (uint64_t*)b; b += cap * 8;
+    p->r.cnt = (uint64_t*)b; b += cap * 8;
+    p->r.koff = (uint64_t*)b; b += cap * 8;
+    p->r.len = (uint32_t*)b; b += cap * 4;
+    p->r.part = (uint32_t*)b;
+    p->r.arena = p->arena;
+    p->r.n = n;
+    p->r.arena_n = arena_n;
+    *out = p;
+    return MRG_OK;
+}
+
+// Collect the current HBM tables into a fresh parts object.
+static int collect_parts(mrg_ctx* c, int app, uint32_t nreduce, mrg_parts** out) {
+    int rc = read_counters(c);
+    if (rc) return rc;
+    Counters& h = *c->h_ctr;
+    uint64_t n = h.short_used + h.long_used;
+    uint64_t arena = h.long_bytes;
+    mrg_parts* p = nullptr;
+    if ((rc = parts_alloc(c, n, arena, app, nreduce, &p))) return rc;
+    Tables t = make_tables(c);
+    HCHK(c, hipMemsetAsync(&t.ctr->nrec, 0, 3 * sizeof(unsigned long long), c->s));
+    launch_collect(t, p->r, nreduce, c->s);
+    HCHK(c, hipGetLastError());
+    rc = read_counters(c);
+    if (rc) { mrg_parts_free(p); return rc; }
+    if (h.nrec != n || h.arena != arena) {
+        mrg_parts_free(p);
+        return fail(c, MRG_EDEVICE, "collect mismatch: %llu/%llu records, %llu/%llu arena bytes", h.nrec,
+                    (unsigned long long)n, h.arena, (unsigned long long)arena);
+    }
+    c->stats.distinct_keys = n;
+    c->stats.long_keys = h.nlong_rec;
+    *out = p;
+    return MRG_OK;
+}
+
+// Grow whatever overflowed; returns 1 if a re-run is needed.
+static int grow_on_overflow(mrg_ctx* c, uint32_t st) {
+    int again = 0;
+    if (st & kStShortFull) { c->sh_log2 += 2; again = 1; }
+    if (st & kStLongFull) { c->lo_log2 += 2; again = 1; }
+    if (st & kStListFull) { c->list_cap = std::max<uint64_t>(c->list_cap * 4, c->h_ctr->nlist + 1024); again = 1; }
+    return again;
+}
+
+// ---------------------------------------------------------------- C ABI
+extern "C" {
+
+int mrg_device_count(int* n) {
+    int k = 0;
+    if (hipGetDeviceCount(&k) != hipSuccess) k = 0;
+    *n = k;
+    return MRG_OK;
+}
+
+int mrg_open(int device, mrg_ctx** out) {
+    if (!out) return MRG_EINVAL;
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return MRG_EDEVICE;
+    if (device < 0 || device >= ndev) return MRG_EINVAL;
+    mrg_ctx* c = new mrg_ctx();
+    c->device = device;
+    int rc;
+    if ((rc = bind(c))) { delete c; return rc; }
+    if (hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking) != hipSuccess) { delete c; return MRG_EDEVICE; }
+    for (auto& e : c->ev) hipEventCreate(&e);
+    if (hipMalloc((void**)&c->d_l1, sizeof(mrg_letter_l1_init)) != hipSuccess ||
+        hipMalloc((void**)&c->d_l2, sizeof(mrg_letter_l2_init)) != hipSuccess) {
+        mrg_close(c);
+        return MRG_ENOMEM;
+    }
+    hipMemcpy(c->d_l1, mrg_letter_l1_init, sizeof(mrg_letter_l1_init), hipMemcpyHostToDevice);
+    hipMemcpy(c->d_l2, mrg_letter_l2_init, sizeof(mrg_letter_l2_init), hipMemcpyHostToDevice);
+    if (hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+        mrg_close(c);
+        return MRG_ENOMEM;
+    }
+    c->grid = map_grid_size(device);
+    c->rws = reduce_ws_new();
+    *out = c;
+    return MRG_OK;
+}
+
+void mrg_close(mrg_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    if (c->s) hipStreamSynchronize(c->s);
+    if (c->comm) ncclCommDestroy(c->comm);
+    DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat};
+    for (DevBuf* b : bs) b->release();
+    if (c->d_l1) hipFree(c->d_l1);
+    if (c->d_l2) hipFree(c->d_l2);
+    if (c->h_ctr) hipHostFree(c->h_ctr);
+    if (c->h_out) hipHostFree(c->h_out);
+    reduce_ws_free(c->rws);
+    for (auto& e : c->ev)
+        if (e) hipEventDestroy(e);
+    if (c->s) hipStreamDestroy(c->s);
+    delete c;
+}
+
+const char* mrg_last_error(const mrg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
+    if (!c || !name) return MRG_EINVAL;
+    if (!strcmp(name, "short_table_log2")) c->sh_log2 = v > 0 ? (int)v : 22;
+    else if (!strcmp(name, "long_table_log2")) c->lo_log2 = v > 0 ? (int)v : 14;
+    else if (!strcmp(name, "list_cap")) c->list_cap = v > 0 ? (uint64_t)v : (1u << 20);
+    else if (!strcmp(name, "map_grid")) c->grid = v > 0 ? (int)v : map_grid_size(c->device);
+    else return fail(c, MRG_EINVAL, "unknown option %s", name);
+    return MRG_OK;
+}
+
+uint32_t mrg_ihash(const uint8_t* key, size_t n) {
+    uint32_t h = 2166136261u;
+    for (size_t i = 0; i < n; i++) h = fnv1a32_step(h, key[i]);
+    return h & 0x7fffffffu;
+}
+
+void mrg_free(void* p) {
+    if (!p) return;
+    uint64_t* hdr = (uint64_t*)p - 2;
+    if (hdr[0] == kHostMagic) {
+        hdr[0] = 0;
+        free(hdr);
+    }
+}
+
+static void* host_result(size_t n) {
+    uint64_t* hdr = (uint64_t*)malloc(n + 16);
+    if (!hdr) return nullptr;
+    hdr[0] = kHostMagic;
+    hdr[1] = n;
+    return hdr + 2;
+}
+
+int mrg_device_alloc(mrg_ctx* c, size_t n, void** d) {
+    if (!c || !d) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    HCHK(c, hipMalloc(d, n ? n : 16));
+    return MRG_OK;
+}
+int mrg_device_free(mrg_ctx* c, void* d) {
+    if (!c) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    HCHK(c, hipFree(d));
+    return MRG_OK;
+}
+int mrg_memcpy_h2d(mrg_ctx* c, void* dst, const void* src, size_t n) {
+    int rc;
+    if ((rc = bind(c))) return rc;
+    HCHK(c, hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
+    return MRG_OK;
+}
+int mrg_memcpy_d2h(mrg_ctx* c, void* dst, const void* src, size_t n) {
+    int rc;
+    if ((rc = bind(c))) return rc;
+    HCHK(c, hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
+    return MRG_OK;
+}
+int mrg_sync(mrg_ctx* c) {
+    int rc;
+    if ((rc = bind(c))) return rc;
+    HCHK(c, hipStreamSynchronize(c->s));
+    HCHK(c, hipDeviceSynchronize());
+    return MRG_OK;
+}
+int mrg_get_stats(const mrg_ctx* c, mrg_stats* out) {
+    if (!c || !out) return MRG_EINVAL;
+    *out = c->stats;
+    return MRG_OK;
+}
+
+int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const uint8_t* pat, size_t plen,
+            uint32_t nreduce, mrg_parts** out) {
+    if (!c || !out || (len && !buf) || nreduce == 0 || (app != MRG_APP_WC && app != MRG_APP_GREP))
+        return c ? fail(c, MRG_EINVAL, "mrg_map: bad arguments") : MRG_EINVAL;
+    if (app == MRG_APP_GREP && plen && !pat) return fail(c, MRG_EINVAL, "mrg_map: null pattern");
+    *out = nullptr;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    c->stats = mrg_stats{};
+    c->stats.input_bytes = len;
+    const uint8_t* in = (const uint8_t*)buf;
+    if (kind == MRG_INPUT_HOST || (((uintptr_t)buf) & 15)) {
+        HCHK(c, c->staging.ensure(len + 64));
+        HCHK(c, hipMemcpyAsync(c->staging.p, buf, len, kind == MRG_INPUT_HOST ? hipMemcpyHostToDevice
+                                                                           : hipMemcpyDeviceToDevice, c->s));
+        in = (const uint8_t*)c->staging.p;
+    }
+    bool grep_nl = false;
+    if (app == MRG_APP_GREP) {
+        HCHK(c, c->pat.ensure(plen + 16));
+        if (plen) HCHK(c, hipMemcpyAsync(c->pat.p, pat, plen, hipMemcpyHostToDevice, c->s));
+        grep_nl = plen && memchr(pat, '\n', plen) != nullptr;  // no line can contain '\n'
+    }
+    LetterTables lt{c->d_l1, c->d_l2};
+    for (int attempt = 0; attempt < 8; attempt++) {
+        if ((rc = ensure_tables(c))) return rc;
+        Tables t = make_tables(c);
+        clear_tables(t, c->s);
+        HCHK(c, hipEventRecord(c->ev[0], c->s));
+        if (app == MRG_APP_WC) {
+            launch_wc_map(in, len, t, lt, c->grid, 0, c->s);
+        } else if (!grep_nl) {
+            if (plen) launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);
+            else launch_grep_all_lines(in, len, t, c->grid, c->s);
+        }
+        HCHK(c, hipGetLastError());
+        HCHK(c, hipEventRecord(c->ev[1], c->s));
+        if ((rc = read_counters(c))) return rc;
+        if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
+        uint64_t nlist = c->h_ctr->nlist;
+        if (app == MRG_APP_WC) launch_wc_long(in, len, t, lt, nlist, c->s);
+        else launch_grep_lines(in, len, (uint32_t)plen, t, nlist, c->s);
+        HCHK(c, hipGetLastError());
+        HCHK(c, hipEventRecord(c->ev[2], c->s));
+        if ((rc = read_counters(c))) return rc;
+        uint32_t st = c->h_ctr->status;
+        if (st & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", st);
+        if (grow_on_overflow(c, st)) continue;
+        c->stats.map_kernel_ms = ev_ms(c->ev[0], c->ev[1]);
+        c->stats.lds_overflow = c->h_ctr->lds_miss;
+        mrg_parts* p = nullptr;
+        if ((rc = collect_parts(c, app, nreduce, &p))) return rc;
+        HCHK(c, hipEventRecord(c->ev[3], c->s));
+        HCHK(c, hipEventSynchronize(c->ev[3]));
+        c->stats.map_total_ms = ev_ms(c->ev[0], c->ev[3]);
+        *out = p;
+        return MRG_OK;
+    }
+    return fail(c, MRG_ENOMEM, "mrg_map: tables kept overflowing");
+}
+
+void mrg_parts_free(mrg_parts* p) {
+    if (!p) return;
+    hipSetDevice(p->device);
+    if (p->block) hipFree(p->block);
+    if (p->arena) hipFree(p->arena);
+    delete p;
+}
+
+int mrg_parts_info(const mrg_parts* p, uint64_t* nkeys, uint32_t* nreduce, int* app) {
+    if (!p) return MRG_EINVAL;
+    if (nkeys) *nkeys = p->r.n;
+    if (nreduce) *nreduce = p->nreduce;
+    if (app) *app = p->app;
+    return MRG_OK;
+}
+
+// Aggregate several record sets into one parts object (exact, by key).
+static int aggregate(mrg_ctx* c, const std::vector<Recs>& srcs, int app, uint32_t nreduce, mrg_parts** out) {
+    int rc;
+    uint64_t tot = 0, longs = 0;
+    for (const Recs& r : srcs) { tot += r.n; longs += r.n; }
+    while ((1ull << c->sh_log2) < tot * 2) c->sh_log2++;
+    while ((1ull << c->lo_log2) < longs / 4 + 1024 && c->lo_log2 < 20) c->lo_log2++;
+    for (int attempt = 0; attempt < 8; attempt++) {
+        if ((rc = ensure_tables(c))) return rc;
+        Tables t = make_tables(c);
+        clear_tables(t, c->s);
+        for (const Recs& r : srcs) launch_insert_recs(r, t, c->s);
+        HCHK(c, hipGetLastError());
+        if ((rc = read_counters(c))) return rc;
+        uint32_t st = c->h_ctr->status;
+        if (st & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out");
+        if (grow_on_overflow(c, st)) continue;
+        return collect_parts(c, app, nreduce, out);
+    }
+    return fail(c, MRG_ENOMEM, "aggregate: tables kept overflowing");
+}
+
+int mrg_parts_merge(mrg_ctx* c, mrg_parts* into, const mrg_parts* from) {
+    if (!c || !into || !from) return MRG_EINVAL;
+    if (into->app != from->app || into->nreduce != from->nreduce) return fail(c, MRG_EINVAL, "merge: app/nreduce mismatch");
+    int rc;
+    if ((rc = bind(c))) return rc;
+    mrg_parts* m = nullptr;
+    if ((rc = aggregate(c, {into->r, from->r}, into->app, into->nreduce, &m))) return rc;
+    hipFree(into->block);
+    hipFree(into->arena);
+    into->block = m->block;
+    into->arena = m->arena;
+    into->r = m->r;
+    m->block = nullptr;
+    m->arena = nullptr;
+    delete m;
+    return MRG_OK;
+}
+
+// Intermediate format "MRGI": header {magic, app, nreduce, part, n, arena_n} then
+// SoA k0[n] k1[n] cnt[n] koff[n] len[n] part[n], then arena bytes.
+struct IHdr {
+    uint32_t magic, app, nreduce, part;
+    uint64_t n, arena_n;
+};
+constexpr uint32_t kIMagic = 0x4947524Du;  // "MRGI"
+
+static int parts_to_host(mrg_ctx* c, const Recs& r, int app, uint32_t nreduce, uint32_t part, void** bytes, size_t* nb) {
+    const uint64_t n = r.n;
+    size_t sz = sizeof(IHdr) + n * (8 * 4 + 4 * 2) + r.arena_n;
+    uint8_t* h = (uint8_t*)host_result(sz);
+    if (!h) return fail(c, MRG_ENOMEM, "host alloc %zu", sz);
+    IHdr hd{kIMagic, (uint32_t)app, nreduce, part, n, r.arena_n};
+    memcpy(h, &hd, sizeof hd);
+    uint8_t* o = h + sizeof hd;
+    auto cp = [&](const void* d, size_t b) -> hipError_t {
+        hipError_t e = b ? hipMemcpyAsync(o, d, b, hipMemcpyDeviceToHost, c->s) : hipSuccess;
+        o += b;
+        return e;
+    };
+    hipError_t e = hipSuccess;
+    if (e == hipSuccess) e = cp(r.k0, n * 8);
+    if (e == hipSuccess) e = cp(r.k1, n * 8);
+    if (e == hipSuccess) e = cp(r.cnt, n * 8);
+    if (e == hipSuccess) e = cp(r.koff, n * 8);
+    if (e == hipSuccess) e = cp(r.len, n * 4);
+    if (e == hipSuccess) e = cp(r.part, n * 4);
+    if (e == hipSuccess) e = cp(r.arena, r.arena_n);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->s);
+    if (e != hipSuccess) { mrg_free(h); return fail(c, MRG_EDEVICE, "export copy: %s", hipGetErrorString(e)); }
+    *bytes = h;
+    *nb = sz;
+    return MRG_OK;
+}
+
+int mrg_parts_export(mrg_ctx* c, const mrg_parts* p, uint32_t r, void** bytes, size_t* nb) {
+    if (!c || !p || !bytes || !nb) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    if (r == 0xFFFFFFFFu) return parts_to_host(c, p->r, p->app, p->nreduce, r, bytes, nb);
+    if (r >= p->nreduce) return fail(c, MRG_EINVAL, "export: partition %u >= nreduce %u", r, p->nreduce);
+    mrg_parts* sel = nullptr;
+    if ((rc = parts_alloc(c, p->r.n, 0, p->app, p->nreduce, &sel))) return rc;
+    Recs d = sel->r;
+    if ((rc = select_recs(c->rws, p->r, p->nreduce, r, &d, c->s))) { mrg_parts_free(sel); return fail(c, MRG_EDEVICE, "select failed"); }
+    rc = parts_to_host(c, d, p->app, p->nreduce, r, bytes, nb);  // arena shared with p (whole arena exported)
+    mrg_parts_free(sel);
+    return rc;
+}
+
+int mrg_parts_import(mrg_ctx* c, const void* bytes, size_t nb, mrg_parts** out) {
+    if (!c || !bytes || !out || nb < sizeof(IHdr)) return c ? fail(c, MRG_EFORMAT, "import: short buffer") : MRG_EINVAL;
+    IHdr hd;
+    memcpy(&hd, bytes, sizeof hd);
+    if (hd.magic != kIMagic || (hd.app != MRG_APP_WC && hd.app != MRG_APP_GREP) || hd.nreduce == 0)
+        return fail(c, MRG_EFORMAT, "import: bad header");
+    const uint64_t n = hd.n;
+    if (sizeof(IHdr) + n * 40 + hd.arena_n != nb) return fail(c, MRG_EFORMAT, "import: size mismatch");
+    int rc;
+    if ((rc = bind(c))) return rc;
+    mrg_parts* p = nullptr;
+    if ((rc = parts_alloc(c, n, hd.arena_n, (int)hd.app, hd.nreduce, &p))) return rc;
+    const uint8_t* s = (const uint8_t*)bytes + sizeof hd;
+    auto cp = [&](void* d, size_t b) -> hipError_t {
+        hipError_t e = b ? hipMemcpyAsync(d, s, b, hipMemcpyHostToDevice, c->s) : hipSuccess;
+        s += b;
+        return e;
+    };
+    hipError_t e = cp(p->r.k0, n * 8);
+    if (e == hipSuccess) e = cp(p->r.k1, n * 8);
+    if (e == hipSuccess) e = cp(p->r.cnt, n * 8);
+    if (e == hipSuccess) e = cp(p->r.koff, n * 8);
+    if (e == hipSuccess) e = cp(p->r.len, n * 4);
+    if (e == hipSuccess) e = cp(p->r.part, n * 4);
+    if (e == hipSuccess) e = cp(p->r.arena, hd.arena_n);
+    if (e == hipSuccess) e = hipStreamSynchronize(c->s);
+    if (e != hipSuccess) { mrg_parts_free(p); return fail(c, MRG_EDEVICE, "import copy: %s", hipGetErrorString(e)); }
+    *out = p;
+    return MRG_OK;
+}
+
+static int reduce_common(mrg_ctx* c, const mrg_parts* p, uint32_t only, uint8_t** d_out, uint64_t* n_out, uint64_t* offsets) {
+    int rc;
+    if ((rc = bind(c))) return rc;
+    HCHK(c, hipEventRecord(c->ev[4], c->s));
+    if (only == 0xFFFFFFFFu) {
+        rc = reduce_format(c->rws, p->r, p->app, p->nreduce, only, d_out, n_out, offsets, c->s);
+        if (rc) return fail(c, MRG_EDEVICE, "reduce_format: %s", hipGetErrorString((hipError_t)rc));
+    } else {
+        mrg_parts* sel = nullptr;
+        if ((rc = parts_alloc(c, p->r.n, 0, p->app, p->nreduce, &sel))) return rc;
+        Recs d = sel->r;
+        if (select_recs(c->rws, p->r, p->nreduce, only, &d, c->s)) { mrg_parts_free(sel); return fail(c, MRG_EDEVICE, "select"); }
+        rc = reduce_format(c->rws, d, p->app, p->nreduce, only, d_out, n_out, offsets, c->s);
+        HCHK(c, hipStreamSynchronize(c->s));
+        mrg_parts_free(sel);
+        if (rc) return fail(c, MRG_EDEVICE, "reduce_format: %s", hipGetErrorString((hipError_t)rc));
+    }
+    HCHK(c, hipEventRecord(c->ev[5], c->s));
+    return MRG_OK;
+}
+
+int mrg_reduce(mrg_ctx* c, const mrg_parts* p, uint32_t r, void** bytes, size_t* nb) {
+    if (!c || !p || !bytes || !nb) return MRG_EINVAL;
+    if (r >= p->nreduce) return fail(c, MRG_EINVAL, "reduce: partition %u >= nreduce %u", r, p->nreduce);
+    uint8_t* d = nullptr;
+    uint64_t n = 0, offs[2];
+    int rc = reduce_common(c, p, r, &d, &n, offs);
+    if (rc) return rc;
+    void* h = host_result(n);
+    if (!h) return fail(c, MRG_ENOMEM, "host alloc");
+    if (n) HCHK(c, hipMemcpy(h, d, n, hipMemcpyDeviceToHost));
+    *bytes = h;
+    *nb = n;
+    c->stats.output_bytes = n;
+    return MRG_OK;
+}
+
+int mrg_reduce_all(mrg_ctx* c, const mrg_parts* p, void** bytes, size_t* nb, uint64_t* offsets) {
+    if (!c || !p || !bytes || !nb || !offsets) return MRG_EINVAL;
+    uint8_t* d = nullptr;
+    uint64_t n = 0;
+    int rc = reduce_common(c, p, 0xFFFFFFFFu, &d, &n, offsets);
+    if (rc) return rc;
+    void* h = host_result(n);
+    if (!h) return fail(c, MRG_ENOMEM, "host alloc");
+    if (n) HCHK(c, hipMemcpy(h, d, n, hipMemcpyDeviceToHost));
+    *bytes = h;
+    *nb = n;
+    c->stats.output_bytes = n;
+    c->stats.reduce_ms = ev_ms(c->ev[4], c->ev[5]);
+    return MRG_OK;
+}
+
+// ---------------------------------------------------------------- RCCL shuffle
+int mrg_comm_unique_id(uint8_t id[128]) {
+    static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+    ncclUniqueId u;
+    if (ncclGetUniqueId(&u) != ncclSuccess) return MRG_ECOMM;
+    memcpy(id, &u, 128);
+    return MRG_OK;
+}
+
+int mrg_comm_init(mrg_ctx* c, const uint8_t id[128], int nranks, int rank) {
+    if (!c || !id || nranks < 1 || rank < 0 || rank >= nranks) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
+    ncclUniqueId u;
+    memcpy(&u, id, 128);
+    NCHK(c, ncclCommInitRank(&c->comm, nranks, u, rank));
+    c->nranks = nranks;
+    c->rank = rank;
+    return MRG_OK;
+}
+
+// Wire record: the parts SoA of one destination, then its arena bytes.
+__global__ void owner_count_kernel(Recs r, uint32_t nranks, unsigned long long* cnt /*[2*nranks]*/) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += stride) {
+        uint32_t o = r.part[i] % nranks;
+        atomicAdd(&cnt[2 * o], 1ull);
+        if (r.koff[i] != ~0ull) atomicAdd(&cnt[2 * o + 1], (unsigned long long)r.len[i]);
+    }
+}
+
+// Pack into per-destination segments: records at rec_base[o] (AoS 40 B), arena at ar_base[o].
+struct WireRec {
+    uint64_t k0, k1, cnt, koff;
+    uint32_t len, part;
+};
+
+__global__ void pack_kernel(Recs r, uint32_t nranks, const uint64_t* rec_base, const uint64_t* ar_base,
+                            unsigned long long* cur /*[2*nranks]*/, WireRec* wrec, uint8_t* war) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += stride) {
+        uint32_t o = r.part[i] % nranks;
+        unsigned long long slot = atomicAdd(&cur[2 * o], 1ull);
+        WireRec w{r.k0[i], r.k1[i], r.cnt[i], ~0ull, r.len[i], r.part[i]};
+        if (r.koff[i] != ~0ull) {
+            unsigned long long a = atomicAdd(&cur[2 * o + 1], (unsigned long long)r.len[i]);
+            for (uint32_t k = 0; k < r.len[i]; k++) war[ar_base[o] + a + k] = r.arena[r.koff[i] + k];
+            w.koff = a;  // relative to the destination's segment from this source
+        }
+        wrec[rec_base[o] + slot] = w;
+    }
+}
+
+// Unpack received wire records; koff rebased by the source's arena displacement.
+__global__ void unpack_kernel(const WireRec* wrec, uint64_t n, const uint64_t* src_rec_begin, const uint64_t* src_ar_begin,
+                              uint32_t nsrc, Recs r) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t s = 0;
+        while (s + 1 < nsrc && src_rec_begin[s + 1] <= i) s++;
+        WireRec w = wrec[i];
+        r.k0[i] = w.k0;
+        r.k1[i] = w.k1;
+        r.cnt[i] = w.cnt;
+        r.len[i] = w.len;
+        r.part[i] = w.part;
+        r.koff[i] = w.koff == ~0ull ? ~0ull : src_ar_begin[s] + w.koff;
+    }
+}
+
+int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
+    if (!c || !local || !owned) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    const int P = c->nranks;
+    if (!c->comm || P == 1) {  // single rank: everything is owned; copy through aggregate for a fresh object
+        return aggregate(c, {local->r}, local->app, local->nreduce, owned);
+    }
+    HCHK(c, hipEventRecord(c->ev[6], c->s));
+    const Recs& r = local->r;
+    DevBuf scratch;
+    std::vector<uint64_t> h(4 * P + 8, 0);
+    // counts per owner
+    size_t meta = sizeof(unsigned long long) * (8 * P + 8);
+    HCHK(c, scratch.ensure(meta));
+    unsigned long long* d_cnt = (unsigned long long*)scratch.p;          // [2P] send counts (rec, arena)
+    unsigned long long* d_rcv = d_cnt + 2 * P;                           // [2P] recv counts
+    unsigned long long* d_cur = d_cnt + 4 * P;                           // [2P] pack cursors
+    uint64_t* d_base = (uint64_t*)(d_cnt + 6 * P);                       // [2P] rec base, arena base
+    HCHK(c, hipMemsetAsync(scratch.p, 0, meta, c->s));
+    if (r.n) owner_count_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, d_cnt);
+    NCHK(c, ncclAllToAll(d_cnt, d_rcv, 2, ncclUint64, c->comm, c->s));
+    std::vector<unsigned long long> snd(2 * P), rcv(2 * P);
+    HCHK(c, hipMemcpyAsync(snd.data(), d_cnt, 16 * P, hipMemcpyDeviceToHost, c->s));
+    HCHK(c, hipMemcpyAsync(rcv.data(), d_rcv, 16 * P, hipMemcpyDeviceToHost, c->s));
+    HCHK(c, hipStreamSynchronize(c->s));
+    std::vector<size_t> sc(P), sd(P), rc_(P), rd(P), asc(P), asd(P), arc(P), ard(P);
+    std::vector<uint64_t> hbase(2 * P);
+    size_t srec = 0, sar = 0, rrec = 0, rar = 0;
+    for (int o = 0; o < P; o++) {
+        hbase[o] = srec;
+        hbase[P + o] = sar;
+        sc[o] = snd[2 * o] * sizeof(WireRec); sd[o] = srec * sizeof(WireRec); srec += snd[2 * o];
+        asc[o] = snd[2 * o + 1]; asd[o] = sar; sar += snd[2 * o + 1];
+        rc_[o] = rcv[2 * o] * sizeof(WireRec); rd[o] = rrec * sizeof(WireRec); rrec += rcv[2 * o];
+        arc[o] = rcv[2 * o + 1]; ard[o] = rar; rar += rcv[2 * o + 1];
+    }
+    DevBuf sbuf, rbuf, sar_b, rar_b, rmeta;
+    HCHK(c, sbuf.ensure(srec * sizeof(WireRec) + 64));
+    HCHK(c, rbuf.ensure(rrec * sizeof(WireRec) + 64));
+    HCHK(c, sar_b.ensure(sar + 64));
+    HCHK(c, rar_b.ensure(rar + 64));
+    HCHK(c, hipMemcpyAsync(d_base, hbase.data(), 16 * P, hipMemcpyHostToDevice, c->s));
+    if (r.n)
+        pack_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, d_base, d_base + P, d_cur, (WireRec*)sbuf.p, (uint8_t*)sar_b.p);
+    HCHK(c, hipGetLastError());
+    NCHK(c, ncclAllToAllv(sbuf.p, sc.data(), sd.data(), rbuf.p, rc_.data(), rd.data(), ncclUint8, c->comm, c->s));
+    NCHK(c, ncclAllToAllv(sar_b.p, asc.data(), asd.data(), rar_b.p, arc.data(), ard.data(), ncclUint8, c->comm, c->s));
+    HCHK(c, hipEventRecord(c->ev[7], c->s));
+    // unpack received records into a Recs view, then aggregate exactly
+    std::vector<uint64_t> hsrc(2 * P);
+    for (int o = 0; o < P; o++) { hsrc[o] = rd[o] / sizeof(WireRec); hsrc[P + o] = ard[o]; }
+    HCHK(c, rmeta.ensure(16 * P));
+    HCHK(c, hipMemcpyAsync(rmeta.p, hsrc.data(), 16 * P, hipMemcpyHostToDevice, c->s));
+    mrg_parts* tmp = nullptr;
+    if ((rc = parts_alloc(c, rrec, 0, local->app, local->nreduce, &tmp))) return rc;
+    hipFree(tmp->arena);
+    tmp->arena = (uint8_t*)rar_b.p;  // adopt the received arena
+    rar_b.p = nullptr;
+    rar_b.cap = 0;
+    tmp->r.arena = tmp->arena;
+    tmp->r.arena_n = rar;
+    if (rrec)
+        unpack_kernel<<<1024, 256, 0, c->s>>>((const WireRec*)rbuf.p, rrec, (const uint64_t*)rmeta.p,
+                                              (const uint64_t*)rmeta.p + P, (uint32_t)P, tmp->r);
+    HCHK(c, hipGetLastError());
+    rc = aggregate(c, {tmp->r}, local->app, local->nreduce, owned);
+    HCHK(c, hipStreamSynchronize(c->s));
+    c->stats.exchange_ms = ev_ms(c->ev[6], c->ev[7]);
+    mrg_parts_free(tmp);
+    sbuf.release(); rbuf.release(); sar_b.release(); rmeta.release(); scratch.release();
+    return rc;
+}
+
+int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const uint8_t* pat, size_t plen,
+                uint32_t nreduce, void** bytes, size_t* nb, uint64_t* offsets) {
+    if (!c || !bytes || !nb || !offsets) return MRG_EINVAL;
+    mrg_parts* p = nullptr;
+    int rc = mrg_map(c, app, buf, len, kind, pat, plen, nreduce, &p);
+    if (rc) return rc;
+    mrg_stats keep = c->stats;
+    mrg_parts* use = p;
+    if (c->comm && c->nranks > 1) {
+        mrg_parts* o = nullptr;
+        rc = mrg_exchange(c, p, &o);
+        keep.exchange_ms = c->stats.exchange_ms;
+        mrg_parts_free(p);
+        if (rc) return rc;
+        use = o;
+    }
+    uint8_t* d = nullptr;
+    uint64_t n = 0;
+    rc = reduce_common(c, use, 0xFFFFFFFFu, &d, &n, offsets);
+    if (rc) { mrg_parts_free(use); return rc; }
+    if (n + 1 > c->h_out_cap) {
+        if (c->h_out) hipHostFree(c->h_out);
+        c->h_out = nullptr;
+        c->h_out_cap = 0;
+        size_t cap = n + n / 4 + 4096;
+        if (hipHostMalloc((void**)&c->h_out, cap, hipHostMallocDefault) != hipSuccess) {
+            mrg_parts_free(use);
+            return fail(c, MRG_ENOMEM, "pinned output alloc");
+        }
+        c->h_out_cap = cap;
+    }
+    HCHK(c, hipEventRecord(c->ev[6], c->s));
+    if (n) HCHK(c, hipMemcpyAsync(c->h_out, d, n, hipMemcpyDeviceToHost, c->s));
+    HCHK(c, hipEventRecord(c->ev[7], c->s));
+    HCHK(c, hipEventSynchronize(c->ev[7]));
+    keep.reduce_ms = ev_ms(c->ev[4], c->ev[5]);
+    keep.d2h_ms = ev_ms(c->ev[6], c->ev[7]);
+    keep.output_bytes = n;
+    keep.distinct_keys = use->r.n;
+    c->stats = keep;
+    mrg_parts_free(use);
+    *bytes = c->h_out;  // context-owned; valid until the next call on this context (do not mrg_free)
+    *nb = n;
+    return MRG_OK;
+}
+
+}  // extern "C"

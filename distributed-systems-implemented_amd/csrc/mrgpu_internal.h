@@ -1,0 +1,111 @@
+// mrgpu_internal.h — device data layout and internal launch interfaces.
+//
+// HBM layout (one context = one GPU):
+//   input      raw split bytes (caller's device buffer, or the context's staging copy)
+//   ShortTable open-addressing table of distinct keys <= 16 bytes, 32 B slots
+//              {k0, k1, count, 0}: k0/k1 = key bytes 0-7 / 8-15 little-endian,
+//              zero padded (letters are never 0x00, so padding is unambiguous).
+//              Empty slot: k0 == 0; claimed but not yet published: k1 == kUnwritten
+//              (0xFF bytes never occur in UTF-8, so no key has that k1).
+//   LongTable  distinct keys > 16 bytes (wc) and every grep line: 32 B slots
+//              {hash64|1, rep pointer, count, len}; bytes compared against rep.
+//   Recs       compacted distinct keys: SoA k0,k1,len,cnt,part,koff + byte arena
+//              for long keys (the "parts" handed between map, exchange, reduce).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mrg {
+
+constexpr uint64_t kUnwritten = ~0ull;
+constexpr int kWave = 64;
+
+// status word bits (device -> host)
+enum : uint32_t {
+    kStShortFull = 1u << 0,
+    kStLongFull = 1u << 1,
+    kStListFull = 1u << 2,
+    kStSpin = 1u << 3,
+};
+
+struct ShortSlot {
+    uint64_t k0, k1, count, pad;
+};
+struct LongSlot {
+    uint64_t hash;        // fnv1a64 | 1; 0 = empty
+    const uint8_t* rep;   // representative bytes; nullptr = not yet published
+    uint64_t count;
+    uint64_t len;
+};
+
+struct Counters {
+    uint32_t status;
+    uint32_t pad0;
+    unsigned long long nlist;      // long-word starts / grep matches appended
+    unsigned long long short_used; // distinct keys claimed in ShortTable
+    unsigned long long long_used;  // distinct keys claimed in LongTable
+    unsigned long long lds_miss;   // occurrences that went to HBM tables
+    unsigned long long nrec;       // collect: records written
+    unsigned long long arena;      // collect: arena bytes used
+    unsigned long long nlong_rec;  // collect: long records
+    unsigned long long chunks_utf8;// chunks that took the UTF-8 decode path
+    unsigned long long long_bytes; // total bytes of distinct long keys (arena size)
+    unsigned long long pad[6];
+};
+
+struct Tables {
+    ShortSlot* sh;
+    uint64_t sh_mask;
+    LongSlot* lo;
+    uint64_t lo_mask;
+    uint64_t* list;      // u64 offsets (long-word starts / grep match positions)
+    uint64_t list_cap;
+    Counters* ctr;
+};
+
+struct Recs {
+    uint64_t* k0;
+    uint64_t* k1;
+    uint32_t* len;
+    uint64_t* cnt;
+    uint32_t* part;
+    uint64_t* koff;      // arena offset (len > 16), else ~0
+    uint8_t* arena;
+    uint64_t n;
+    uint64_t arena_n;
+};
+
+struct LetterTables {
+    const uint8_t* l1;
+    const uint32_t* l2;
+};
+
+// ---- launchers (mrgpu_map.hip) ----
+void clear_tables(const Tables& t, hipStream_t s);
+void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int lds_slots,
+                   hipStream_t s);
+void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
+void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
+                     hipStream_t s);
+void launch_grep_lines(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nlist, hipStream_t s);
+void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int grid, hipStream_t s);
+void launch_collect(const Tables& t, Recs r, uint32_t nreduce, hipStream_t s);
+void launch_insert_recs(const Recs& src, const Tables& t, hipStream_t s);
+int map_grid_size(int device);
+
+// ---- reduce (mrgpu_reduce.hip) ----
+struct ReduceWs;  // opaque workspace
+ReduceWs* reduce_ws_new();
+void reduce_ws_free(ReduceWs*);
+// Sort recs (optionally only partition `only_part`), format "key value\n" lines.
+// Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
+int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,
+                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s);
+// Compact recs with part == p (or owner rank) into dst (device), returns count on host.
+int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst_host_desc, hipStream_t s);
+
+__host__ __device__ inline uint32_t fnv1a32_step(uint32_t h, uint32_t byte) {
+    return (h ^ byte) * 16777619u;
+}
+
+}  // namespace mrg

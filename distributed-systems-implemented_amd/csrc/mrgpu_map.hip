@@ -1,0 +1,689 @@
+// mrgpu_map.hip — Map side of the MI355X MapReduce hot path (gfx950).
+//
+// wc (MapReduce/mrapps/wc.go:21-34 + mr/worker.go:72-78):
+//   One wave owns a 2 KiB chunk of input at a time (plus a 16 B look-back and a
+//   64 B look-ahead halo).  Lanes load 16 B each (two coalesced 1 KiB wave loads),
+//   stage the bytes in the wave's LDS slice and classify them:
+//     * ASCII chunks (wave-uniform test): SWAR letter test, 4 bytes per op;
+//     * otherwise a Go-exact UTF-8 decode (utf8.DecodeRune acceptance ranges,
+//       invalid byte = U+FFFD width 1) + unicode.IsLetter via a two-level bitmap.
+//   A word is a maximal run of letter bytes (strings.FieldsFunc with
+//   !unicode.IsLetter).  Word starts are compacted with ballot/mbcnt prefix sums
+//   into an LDS list, then each lane takes one word: its length comes from the
+//   letter bitmaps (ctz), its <= 16 key bytes are packed into two u64 with
+//   v_alignbyte, and the word is counted in the workgroup's LDS hash table (the
+//   combiner: every wc value is "1", so Reduce(len(values)) == sum of counts).
+//   Misses (table full) and the final LDS flush go to the HBM ShortTable; words
+//   longer than 16 bytes go to a list handled by wc_long_kernel.
+//   ihash (FNV-1a) is computed once per *distinct* key in collect_kernel — the
+//   partition is a pure function of the key, so this equals the per-KV
+//   ihash(kv.Key) % NReduce of worker.go:76 with W/U times fewer hashes.
+//
+// grep (MapReduce/mrapps/dgrep.go:18-36): streaming literal search (first-byte
+//   SWAR filter, LDS verify); each hit's line (strings.Split on "\n") is
+//   resolved and inserted, deduplicated by content, into the LongTable.
+#include "mrgpu_internal.h"
+
+namespace mrg {
+
+constexpr int kChunk = 2048;
+constexpr int kBack = 16;
+constexpr int kAhead = 64;
+constexpr int kBuf = kBack + kChunk + kAhead;  // 2128, multiple of 16
+constexpr int kWavesPerWG = 8;
+constexpr int kThreads = kWavesPerWG * kWave;
+constexpr int kListCap = kChunk / 2;              // max word starts in a chunk
+constexpr int kNMask = 136;                       // [0]=look-back piece, [1..128]=chunk, [129..131]=look-ahead
+constexpr int kLdsSlots = 4096;
+constexpr int kLdsLimit = kLdsSlots * 7 / 8;
+constexpr int kLdsProbes = 24;
+constexpr int kGlobalProbes = 4096;
+constexpr uint32_t kSpinLimit = 1u << 22;
+
+struct alignas(16) WaveLds {
+    uint8_t buf[kBuf];
+    uint16_t mask[kNMask];
+    uint16_t list[kListCap];
+};
+
+struct alignas(16) MapLds {
+    WaveLds w[kWavesPerWG];
+    unsigned long long k0[kLdsSlots];
+    unsigned long long k1[kLdsSlots];
+    uint32_t cnt[kLdsSlots];
+    uint32_t occ;
+};
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ const uint8_t* ld_agent_ptr(const uint8_t* const* p) {
+    return __hip_atomic_load(const_cast<const uint8_t**>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void set_status(Counters* c, uint32_t bits) { atomicOr(&c->status, bits); }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Exclusive prefix sum over the wave of c (0 <= c < 32) by ballot bit-planes.
+__device__ __forceinline__ uint32_t wave_excl_scan5(uint32_t c, uint32_t* total) {
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < 5; k++) {
+        uint64_t b = __ballot((c >> k) & 1u);
+        base += mbcnt64(b) << k;
+        tot += (uint32_t)__popcll(b) << k;
+    }
+    *total = tot;
+    return base;
+}
+
+// 4 ASCII bytes -> 4-bit letter mask ([A-Za-z]); requires every byte < 0x80.
+__device__ __forceinline__ uint32_t ascii_letters4(uint32_t x) {
+    uint32_t y = x | 0x20202020u;
+    uint32_t t = (y + 0x1F1F1F1Fu) & ~(y + 0x05050505u) & 0x80808080u;
+    return ((t >> 7) * 0x10204080u) >> 28;
+}
+__device__ __forceinline__ uint32_t ascii_mask16(uint4 v) {
+    return ascii_letters4(v.x) | (ascii_letters4(v.y) << 4) | (ascii_letters4(v.z) << 8) | (ascii_letters4(v.w) << 12);
+}
+
+__device__ __forceinline__ bool is_letter_cp(uint32_t cp, LetterTables lt) {
+    if (cp < 0x80) return ((cp | 0x20u) - 0x61u) < 26u;
+    uint32_t idx = lt.l1[cp >> 8];
+    return (lt.l2[idx * 8 + ((cp >> 5) & 7)] >> (cp & 31)) & 1u;
+}
+
+// Go utf8 acceptance: length of the valid sequence starting with bytes c0..c3, or 0.
+__device__ __forceinline__ int utf8_valid_len(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    if (c0 < 0x80) return 1;
+    if (c0 < 0xC2 || c0 > 0xF4) return 0;
+    uint32_t lo = 0x80, hi = 0xBF;
+    if (c0 == 0xE0) lo = 0xA0;
+    else if (c0 == 0xED) hi = 0x9F;
+    else if (c0 == 0xF0) lo = 0x90;
+    else if (c0 == 0xF4) hi = 0x8F;
+    if (c1 < lo || c1 > hi) return 0;
+    if (c0 < 0xE0) return 2;
+    if ((c2 & 0xC0) != 0x80) return 0;
+    if (c0 < 0xF0) return 3;
+    if ((c3 & 0xC0) != 0x80) return 0;
+    return 4;
+}
+
+__device__ __forceinline__ uint32_t utf8_decode(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, int n) {
+    if (n == 1) return c0;
+    if (n == 2) return ((c0 & 0x1F) << 6) | (c1 & 0x3F);
+    if (n == 3) return ((c0 & 0x0F) << 12) | ((c1 & 0x3F) << 6) | (c2 & 0x3F);
+    return ((c0 & 0x07) << 18) | ((c1 & 0x3F) << 12) | ((c2 & 0x3F) << 6) | (c3 & 0x3F);
+}
+
+// Letter mask of the W bytes at b[q0 .. q0+W) with Go decoding semantics.
+// Needs b[q0-6 .. q0+W+3) addressable (zeros outside the input act as
+// non-continuation terminators, matching Go's truncated-sequence rule).
+// Rune starts use the local rule: byte q starts a rune unless a valid sequence
+// of length > k starts at q-k, k in {1,2,3}.
+template <int W>
+__device__ uint32_t utf8_letter_mask(const uint8_t* b, int q0, LetterTables lt) {
+    uint32_t mask = 0;
+    int vl1 = 0, vl2 = 0, vl3 = 0;  // valid lengths at q-1, q-2, q-3
+    for (int q = q0 - 6; q < q0 + W; q++) {
+        uint32_t c0 = b[q], c1 = b[q + 1], c2 = b[q + 2], c3 = b[q + 3];
+        int vl = utf8_valid_len(c0, c1, c2, c3);
+        if (q >= q0 - 3) {
+            bool start = !(vl1 >= 2 || vl2 >= 3 || vl3 >= 4);
+            if (start) {
+                bool let = vl > 0 && is_letter_cp(utf8_decode(c0, c1, c2, c3, vl), lt);
+                if (let) {
+                    for (int k = 0; k < vl; k++) {
+                        int pos = q + k - q0;
+                        if (pos >= 0 && pos < W) mask |= 1u << pos;
+                    }
+                }
+            }
+        }
+        vl3 = vl2; vl2 = vl1; vl1 = vl;
+    }
+    return mask;
+}
+
+__device__ __forceinline__ uint32_t fold32(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    uint32_t x = w0 ^ __builtin_rotateleft32(w1, 7) ^ __builtin_rotateleft32(w2, 13) ^ __builtin_rotateleft32(w3, 21);
+    return x * 0x9E3779B1u;
+}
+
+__device__ __forceinline__ uint64_t short_hash64(uint64_t k0, uint64_t k1) {
+    uint64_t h = (k0 ^ (k1 * 0x9E3779B97F4A7C15ull)) * 0xD6E8FEB86659FD93ull;
+    return h ^ (h >> 32);
+}
+
+__device__ __forceinline__ uint64_t fnv1a64_step(uint64_t h, uint32_t b) { return (h ^ b) * 1099511628211ull; }
+constexpr uint64_t kFnv64Off = 14695981039346656037ull;
+
+// ------------------------------------------------------- HBM table inserts
+// Lock-free insert of a short key.  Claim = CAS on k0 (0 -> key); publish k1
+// afterwards; a reader that matches k0 waits (re-executes the loop, never a
+// nested spin, so a claimer in the same wave always makes progress) until k1 is
+// visible.  All shared words use agent-scope atomics (sc1: coherent across the
+// 8 XCD L2s).
+__device__ void short_insert(const Tables& t, uint64_t k0, uint64_t k1, uint64_t cnt) {
+    uint64_t i = short_hash64(k0, k1) & t.sh_mask;
+    uint32_t probes = 0, spins = 0;
+    while (true) {
+        ShortSlot* s = &t.sh[i];
+        uint64_t cur = ld_agent(&s->k0);
+        if (cur == 0) {
+            uint64_t prev = atomicCAS((unsigned long long*)&s->k0, 0ull, (unsigned long long)k0);
+            if (prev == 0) {
+                st_agent(&s->k1, k1);
+                atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                unsigned long long used = atomicAdd(&t.ctr->short_used, 1ull);
+                if (used * 10 > (t.sh_mask + 1) * 7) set_status(t.ctr, kStShortFull);
+                return;
+            }
+            cur = prev;
+        }
+        if (cur == k0) {
+            uint64_t v = ld_agent(&s->k1);
+            if (v == kUnwritten) {
+                if (++spins > kSpinLimit) { set_status(t.ctr, kStSpin); return; }
+                continue;
+            }
+            if (v == k1) {
+                atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                return;
+            }
+        }
+        if (++probes > kGlobalProbes) { set_status(t.ctr, kStShortFull); return; }
+        i = (i + 1) & t.sh_mask;
+    }
+}
+
+// Long keys: claim = CAS on hash; publish len+1 and rep separately; readers wait
+// until both are visible, then compare bytes.
+__device__ void long_insert(const Tables& t, uint64_t h, const uint8_t* rep, uint64_t len, uint64_t cnt) {
+    h |= 1ull;
+    uint64_t i = (h * 0x9E3779B97F4A7C15ull >> 17) & t.lo_mask;
+    uint32_t probes = 0, spins = 0;
+    while (true) {
+        LongSlot* s = &t.lo[i];
+        uint64_t cur = ld_agent(&s->hash);
+        if (cur == 0) {
+            uint64_t prev = atomicCAS((unsigned long long*)&s->hash, 0ull, (unsigned long long)h);
+            if (prev == 0) {
+                st_agent(&s->len, len + 1);
+                __hip_atomic_store(const_cast<const uint8_t**>(&s->rep), rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                atomicAdd(&t.ctr->long_bytes, (unsigned long long)len);
+                unsigned long long used = atomicAdd(&t.ctr->long_used, 1ull);
+                if (used * 10 > (t.lo_mask + 1) * 7) set_status(t.ctr, kStLongFull);
+                return;
+            }
+            cur = prev;
+        }
+        if (cur == h) {
+            const uint8_t* r = ld_agent_ptr(&s->rep);
+            uint64_t lp1 = ld_agent(&s->len);
+            if (r == nullptr || lp1 == 0) {
+                if (++spins > kSpinLimit) { set_status(t.ctr, kStSpin); return; }
+                continue;
+            }
+            if (lp1 == len + 1) {
+                bool eq = true;
+                for (uint64_t k = 0; k < len; k++)
+                    if (r[k] != rep[k]) { eq = false; break; }
+                if (eq) {
+                    atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                    return;
+                }
+            }
+        }
+        if (++probes > kGlobalProbes) { set_status(t.ctr, kStLongFull); return; }
+        i = (i + 1) & t.lo_mask;
+    }
+}
+
+__device__ __forceinline__ void list_append(const Tables& t, uint64_t v) {
+    unsigned long long idx = atomicAdd(&t.ctr->nlist, 1ull);
+    if (idx < t.list_cap) t.list[idx] = v;
+    else set_status(t.ctr, kStListFull);
+}
+
+// ------------------------------------------------------------ LDS table
+// Same claim/publish protocol inside the workgroup's LDS (the combiner).
+__device__ __forceinline__ bool lds_insert(MapLds& L, uint64_t k0, uint64_t k1, uint32_t h) {
+    uint32_t i = h >> (32 - 12);
+    uint32_t probes = 0, spins = 0;
+    while (true) {
+        uint64_t cur = __hip_atomic_load(&L.k0[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (cur == 0) {
+            if (__hip_atomic_load(&L.occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (uint32_t)kLdsLimit)
+                return false;
+            uint64_t prev = atomicCAS(&L.k0[i], 0ull, (unsigned long long)k0);
+            if (prev == 0) {
+                __hip_atomic_store(&L.k1[i], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                atomicAdd(&L.cnt[i], 1u);
+                atomicAdd(&L.occ, 1u);
+                return true;
+            }
+            cur = prev;
+        }
+        if (cur == k0) {
+            uint64_t v = __hip_atomic_load(&L.k1[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (v == kUnwritten) {
+                if (++spins > kSpinLimit) return false;
+                continue;
+            }
+            if (v == k1) {
+                atomicAdd(&L.cnt[i], 1u);
+                return true;
+            }
+        }
+        if (++probes >= (uint32_t)kLdsProbes) return false;
+        i = (i + 1) & (kLdsSlots - 1);
+    }
+}
+
+// ------------------------------------------------------------ chunk loading
+struct ChunkRegs {
+    uint4 a, b, h;  // a: bytes [16l,16l+16), b: [1024+16l, ...), h: halo piece (lanes 0-4)
+};
+
+__device__ __forceinline__ uint4 load16_bounded(const uint8_t* in, uint64_t n, int64_t off) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 16; k++) {
+        int64_t o = off + k;
+        if (o >= 0 && (uint64_t)o < n) w[k >> 2] |= (uint32_t)in[o] << (8 * (k & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ in, uint64_t n, uint64_t cs, uint32_t lane,
+                                           ChunkRegs& r) {
+    if (cs + kChunk + kAhead <= n && cs >= (uint64_t)kBack) {
+        const uint4* p = reinterpret_cast<const uint4*>(in + cs);
+        r.a = p[lane];
+        r.b = p[64 + lane];
+        if (lane < 4) r.h = p[128 + lane];
+        else if (lane == 4) r.h = p[-1];
+        else r.h = make_uint4(0, 0, 0, 0);
+    } else {
+        r.a = load16_bounded(in, n, (int64_t)cs + 16 * lane);
+        r.b = load16_bounded(in, n, (int64_t)cs + 1024 + 16 * lane);
+        if (lane < 4) r.h = load16_bounded(in, n, (int64_t)cs + 2048 + 16 * lane);
+        else if (lane == 4) r.h = load16_bounded(in, n, (int64_t)cs - 16);
+        else r.h = make_uint4(0, 0, 0, 0);
+    }
+}
+
+__device__ __forceinline__ void stage_chunk(WaveLds& W, const ChunkRegs& r, uint32_t lane) {
+    uint4* b4 = reinterpret_cast<uint4*>(W.buf);
+    b4[1 + lane] = r.a;
+    b4[65 + lane] = r.b;
+    if (lane < 4) b4[129 + lane] = r.h;
+    else if (lane == 4) b4[0] = r.h;
+}
+
+// ------------------------------------------------------------ wc map kernel
+__global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
+                                                          Tables t, LetterTables lt) {
+    __shared__ MapLds L;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const uint32_t wv = tid >> 6;
+    WaveLds& W = L.w[wv];
+
+    for (uint32_t i = tid; i < kLdsSlots; i += kThreads) {
+        L.k0[i] = 0;
+        L.k1[i] = kUnwritten;
+        L.cnt[i] = 0;
+    }
+    if (tid == 0) L.occ = 0;
+    __syncthreads();
+
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
+    uint64_t c = (uint64_t)blockIdx.x * kWavesPerWG + wv;
+    uint64_t miss = 0, utf8_chunks = 0;
+    ChunkRegs cur, nxt;
+    if (c < nchunks) load_chunk(in, n, c * kChunk, lane, cur);
+
+    for (; c < nchunks; c += stride) {
+        const uint64_t cs = c * kChunk;
+        if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);  // prefetch
+
+        stage_chunk(W, cur, lane);
+        uint32_t hi = (cur.a.x | cur.a.y | cur.a.z | cur.a.w | cur.b.x | cur.b.y | cur.b.z | cur.b.w | cur.h.x |
+                       cur.h.y | cur.h.z | cur.h.w) & 0x80808080u;
+        const bool ascii = __ballot(hi != 0) == 0;
+        uint32_t mA, mB, mH = 0;
+        if (ascii) {
+            mA = ascii_mask16(cur.a);
+            mB = ascii_mask16(cur.b);
+            if (lane < 5) mH = ascii_mask16(cur.h);
+        } else {
+            utf8_chunks++;
+            wave_sync();
+            mA = utf8_letter_mask<16>(W.buf, kBack + 16 * lane, lt);
+            mB = utf8_letter_mask<16>(W.buf, kBack + 1024 + 16 * lane, lt);
+            if (lane < 3) mH = utf8_letter_mask<16>(W.buf, kBack + 2048 + 16 * lane, lt);
+            else if (lane == 4) mH = utf8_letter_mask<8>(W.buf, 8, lt) << 8;  // look-back bits 8..15
+        }
+        W.mask[1 + lane] = (uint16_t)mA;
+        W.mask[65 + lane] = (uint16_t)mB;
+        if (lane < 4) W.mask[129 + lane] = (uint16_t)mH;
+        else if (lane == 4) W.mask[0] = (uint16_t)mH;
+
+        // word starts: letter byte whose predecessor byte is not a letter byte
+        const uint32_t prevA_m = __shfl(mA, (int)((lane + 63) & 63));
+        const uint32_t prevB_m = __shfl(mB, (int)((lane + 63) & 63));
+        const uint32_t lastA = __shfl(mA, 63);
+        const uint32_t back = __shfl(mH, 4);
+        const uint32_t pa = (lane == 0 ? back : prevA_m) >> 15 & 1u;
+        const uint32_t pb = (lane == 0 ? lastA : prevB_m) >> 15 & 1u;
+        uint32_t SA = mA & ~((mA << 1) | pa) & 0xFFFFu;
+        uint32_t SB = mB & ~((mB << 1) | pb) & 0xFFFFu;
+        uint32_t total;
+        uint32_t j = wave_excl_scan5(__popc(SA) + __popc(SB), &total);
+        while (SA) {
+            uint32_t bit = __builtin_ctz(SA);
+            W.list[j++] = (uint16_t)(16 * lane + bit);
+            SA &= SA - 1;
+        }
+        while (SB) {
+            uint32_t bit = __builtin_ctz(SB);
+            W.list[j++] = (uint16_t)(1024 + 16 * lane + bit);
+            SB &= SB - 1;
+        }
+        wave_sync();
+
+        for (uint32_t w = lane; w < total; w += 64) {
+            const uint32_t s = W.list[w];
+            const uint32_t p = s >> 4, bsh = s & 15;
+            const uint64_t win = (uint64_t)W.mask[p + 1] | ((uint64_t)W.mask[p + 2] << 16) | ((uint64_t)W.mask[p + 3] << 32);
+            const uint32_t len = (uint32_t)__builtin_ctzll(~(win >> bsh));
+            if (len > 16) {
+                list_append(t, cs + s);
+                continue;
+            }
+            const uint32_t q = kBack + s;
+            const uint32_t* d = reinterpret_cast<const uint32_t*>(W.buf + (q & ~3u));
+            const uint32_t sh = q & 3u;
+            const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+            uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+            uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+            uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+            uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+            uint64_t k0 = ((uint64_t)w1 << 32) | w0;
+            uint64_t k1 = ((uint64_t)w3 << 32) | w2;
+            k0 &= len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1);
+            k1 &= len >= 16 ? ~0ull : (len <= 8 ? 0ull : ((1ull << (8 * (len - 8))) - 1));
+            const uint32_t h = fold32((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+            if (!lds_insert(L, k0, k1, h)) {
+                short_insert(t, k0, k1, 1);
+                miss++;
+            }
+        }
+        cur = nxt;
+    }
+
+    __syncthreads();
+    for (uint32_t i = tid; i < kLdsSlots; i += kThreads) {
+        uint64_t k0 = L.k0[i];
+        if (k0 != 0) short_insert(t, k0, L.k1[i], L.cnt[i]);
+    }
+    if (miss) atomicAdd(&t.ctr->lds_miss, (unsigned long long)miss);
+    if (utf8_chunks && lane == 0) atomicAdd(&t.ctr->chunks_utf8, (unsigned long long)utf8_chunks);
+}
+
+// Words longer than 16 bytes: decode forward from the start (one lane per word).
+__global__ void wc_long_kernel(const uint8_t* __restrict__ in, uint64_t n, Tables t, LetterTables lt, uint64_t nlist) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlist) return;
+    const uint64_t s = t.list[i];
+    uint64_t q = s, h = kFnv64Off;
+    while (q < n) {
+        uint32_t c0 = in[q];
+        uint32_t c1 = q + 1 < n ? in[q + 1] : 0, c2 = q + 2 < n ? in[q + 2] : 0, c3 = q + 3 < n ? in[q + 3] : 0;
+        int vl = utf8_valid_len(c0, c1, c2, c3);
+        if (vl == 0 || !is_letter_cp(utf8_decode(c0, c1, c2, c3, vl), lt)) break;
+        for (int k = 0; k < vl; k++) h = fnv1a64_step(h, in[q + k]);
+        q += vl;
+    }
+    long_insert(t, h, in + s, q - s, 1);
+}
+
+// ------------------------------------------------------------ grep kernels
+// Pattern occurrence search.  Every occurrence start p (with p + plen <= n) is
+// appended to the list; grep_lines_kernel resolves its line.
+__device__ __forceinline__ uint32_t eq_mask16(uint4 v, uint32_t rep) {
+    // exact per-byte equality with the broadcast byte (no borrow false positives)
+    uint32_t m = 0;
+    uint32_t ws[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        uint32_t x = ws[k] ^ rep;
+        uint32_t z = ~(((x & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | x) & 0x80808080u;  // 0x80 where byte == 0
+        m |= (((z >> 7) * 0x10204080u) >> 28) << (4 * k);
+    }
+    return m;
+}
+
+__global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
+                                                            const uint8_t* __restrict__ pat, uint32_t plen, Tables t) {
+    __shared__ WaveLds Wl[kWavesPerWG];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    WaveLds& W = Wl[tid >> 6];
+    const uint32_t p0 = pat[0];
+    const uint32_t rep = p0 * 0x01010101u;
+    const bool in_lds = plen <= (uint32_t)kAhead;
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
+    uint64_t c = (uint64_t)blockIdx.x * kWavesPerWG + (tid >> 6);
+    ChunkRegs cur, nxt;
+    if (c < nchunks) load_chunk(in, n, c * kChunk, lane, cur);
+    for (; c < nchunks; c += stride) {
+        const uint64_t cs = c * kChunk;
+        if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);
+        stage_chunk(W, cur, lane);
+        wave_sync();
+        uint32_t cand[2] = {eq_mask16(cur.a, rep), eq_mask16(cur.b, rep)};
+#pragma unroll
+        for (int piece = 0; piece < 2; piece++) {
+            uint32_t m = cand[piece];
+            const uint32_t base = piece * 1024 + 16 * lane;
+            while (m) {
+                const uint32_t bit = __builtin_ctz(m);
+                m &= m - 1;
+                const uint64_t pos = cs + base + bit;
+                if (pos + plen > n) continue;
+                bool ok = true;
+                if (in_lds) {
+                    const uint8_t* q = W.buf + kBack + base + bit;
+                    for (uint32_t k = 1; k < plen; k++)
+                        if (q[k] != pat[k]) { ok = false; break; }
+                } else {
+                    for (uint32_t k = 1; k < plen; k++)
+                        if (in[pos + k] != pat[k]) { ok = false; break; }
+                }
+                if (ok) list_append(t, pos);
+            }
+        }
+        wave_sync();
+        cur = nxt;
+    }
+}
+
+// Empty pattern: every line (strings.Split yields len(sep-count)+1 lines).
+__global__ void grep_all_lines_kernel(const uint8_t* __restrict__ in, uint64_t n, Tables t) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += stride) {
+        if (i == 0) list_append(t, 0);
+        else if (in[i - 1] == '\n') list_append(t, i);
+    }
+}
+
+// Resolve the line of each hit: [last '\n' before p]+1 .. next '\n' at/after p.
+// plen == 0 means the list already holds line starts.
+__global__ void grep_lines_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen, Tables t, uint64_t nlist) {
+    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nlist) return;
+    const uint64_t p = t.list[i];
+    uint64_t s = p;
+    if (plen > 0)
+        while (s > 0 && in[s - 1] != '\n') s--;
+    uint64_t e = p;
+    while (e < n && in[e] != '\n') e++;
+    uint64_t h = kFnv64Off;
+    for (uint64_t k = s; k < e; k++) h = fnv1a64_step(h, in[k]);
+    long_insert(t, h, in + s, e - s, 1);
+}
+
+// ------------------------------------------------------------ collect
+__device__ __forceinline__ uint32_t key_len_short(uint64_t k0, uint64_t k1) {
+    if (k1) return 8 + (uint32_t)((71 - __builtin_clzll(k1)) >> 3);
+    return (uint32_t)((71 - __builtin_clzll(k0)) >> 3);
+}
+
+__global__ void collect_short_kernel(Tables t, Recs r, uint32_t nreduce) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= t.sh_mask; i += stride) {
+        const ShortSlot s = t.sh[i];
+        if (s.k0 == 0) continue;
+        const uint32_t len = key_len_short(s.k0, s.k1);
+        uint32_t h = 2166136261u;
+        for (uint32_t k = 0; k < len; k++) {
+            const uint64_t w = k < 8 ? s.k0 : s.k1;
+            h = fnv1a32_step(h, (uint32_t)(w >> (8 * (k & 7))) & 0xFFu);
+        }
+        const unsigned long long o = atomicAdd(&t.ctr->nrec, 1ull);
+        r.k0[o] = s.k0;
+        r.k1[o] = s.k1;
+        r.len[o] = len;
+        r.cnt[o] = s.count;
+        r.part[o] = (h & 0x7fffffffu) % nreduce;
+        r.koff[o] = ~0ull;
+    }
+}
+
+__global__ void collect_long_kernel(Tables t, Recs r, uint32_t nreduce) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= t.lo_mask; i += stride) {
+        const LongSlot s = t.lo[i];
+        if (s.hash == 0 || s.rep == nullptr || s.len == 0) continue;
+        const uint64_t len = s.len - 1;
+        const unsigned long long off = atomicAdd(&t.ctr->arena, (unsigned long long)len);
+        uint32_t h = 2166136261u;
+        uint64_t k0 = 0, k1 = 0;
+        for (uint64_t k = 0; k < len; k++) {
+            const uint32_t b = s.rep[k];
+            r.arena[off + k] = (uint8_t)b;
+            h = fnv1a32_step(h, b);
+            if (k < 8) k0 |= (uint64_t)b << (8 * k);
+            else if (k < 16) k1 |= (uint64_t)b << (8 * (k - 8));
+        }
+        const unsigned long long o = atomicAdd(&t.ctr->nrec, 1ull);
+        atomicAdd(&t.ctr->nlong_rec, 1ull);
+        r.k0[o] = k0;
+        r.k1[o] = k1;
+        r.len[o] = (uint32_t)len;
+        r.cnt[o] = s.count;
+        r.part[o] = (h & 0x7fffffffu) % nreduce;
+        r.koff[o] = off;
+    }
+}
+
+// Re-aggregate records (merge / import / exchange receive).
+__global__ void insert_recs_kernel(Recs src, Tables t) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < src.n; i += stride) {
+        const uint64_t ko = src.koff[i];
+        if (ko == ~0ull) {
+            short_insert(t, src.k0[i], src.k1[i], src.cnt[i]);
+        } else {
+            const uint8_t* p = src.arena + ko;
+            const uint32_t len = src.len[i];
+            uint64_t h = kFnv64Off;
+            for (uint32_t k = 0; k < len; k++) h = fnv1a64_step(h, p[k]);
+            long_insert(t, h, p, len, src.cnt[i]);
+        }
+    }
+}
+
+__global__ void clear_tables_kernel(Tables t) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= t.sh_mask; i += stride)
+        t.sh[i] = ShortSlot{0, kUnwritten, 0, 0};
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= t.lo_mask; i += stride)
+        t.lo[i] = LongSlot{0, nullptr, 0, 0};
+}
+
+// ------------------------------------------------------------ launchers
+int map_grid_size(int device) {
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || ncu <= 0) ncu = 256;
+    return ncu;  // one 512-thread workgroup per CU (LDS-bound), persistent over chunks
+}
+
+void clear_tables(const Tables& t, hipStream_t s) {
+    hipMemsetAsync(t.ctr, 0, sizeof(Counters), s);
+    clear_tables_kernel<<<2048, 256, 0, s>>>(t);
+}
+
+void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int, hipStream_t s) {
+    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    if (nchunks == 0) return;
+    uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
+    if (g > (uint64_t)grid) g = (uint64_t)grid;
+    wc_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt);
+}
+
+void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s) {
+    if (nlist == 0) return;
+    wc_long_kernel<<<(unsigned)((nlist + 255) / 256), 256, 0, s>>>(in, n, t, lt, nlist);
+}
+
+void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
+                     hipStream_t s) {
+    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    if (nchunks == 0 || plen == 0) return;
+    uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
+    uint64_t gmax = (uint64_t)grid * 4;
+    if (g > gmax) g = gmax;
+    grep_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, d_pat, plen, t);
+}
+
+void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int grid, hipStream_t s) {
+    grep_all_lines_kernel<<<grid * 4, 256, 0, s>>>(in, n, t);
+}
+
+void launch_grep_lines(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nlist, hipStream_t s) {
+    if (nlist == 0) return;
+    grep_lines_kernel<<<(unsigned)((nlist + 255) / 256), 256, 0, s>>>(in, n, plen, t, nlist);
+}
+
+void launch_collect(const Tables& t, Recs r, uint32_t nreduce, hipStream_t s) {
+    collect_short_kernel<<<1024, 256, 0, s>>>(t, r, nreduce);
+    collect_long_kernel<<<256, 256, 0, s>>>(t, r, nreduce);
+}
+
+void launch_insert_recs(const Recs& src, const Tables& t, hipStream_t s) {
+    if (src.n == 0) return;
+    uint64_t g = (src.n + 255) / 256;
+    if (g > 4096) g = 4096;
+    insert_recs_kernel<<<(unsigned)g, 256, 0, s>>>(src, t);
+}
+
+}  // namespace mrg

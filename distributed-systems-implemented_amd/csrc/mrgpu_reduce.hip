@@ -1,0 +1,334 @@
+// mrgpu_reduce.hip — Reduce side: sort.Sort(ByKey) + group + Reduce + Fprintf.
+//
+// Reference: MapReduce/mr/worker.go:123-146 (and main/mrsequential.go:59-84).
+// Input records are already grouped (one record per distinct key with its
+// count), so "group + reducef(len(values))" is the record itself; what remains
+// is the bytewise key order and the "%v %v\n" formatting.
+//
+// Order: Go string '<' is unsigned bytewise with a shorter prefix first.  Keys
+// are sorted by (partition, first 16 bytes big-endian, length) with stable LSD
+// radix passes; zero padding makes that order exact for keys <= 16 bytes and
+// for any two keys whose 16-byte prefixes differ.  Remaining ties (keys > 16
+// bytes sharing a 16-byte prefix and a length) are resolved by a full bytewise
+// comparison inside each tied run.
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/device/device_scan.hpp>
+
+#include "mrgpu_internal.h"
+
+namespace mrg {
+
+struct DBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t n) {
+        if (n <= cap) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t c = n < 4096 ? 4096 : n + n / 4;
+        hipError_t e = hipMalloc(&p, c);
+        if (e == hipSuccess) cap = c;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T>
+    T* as() const { return static_cast<T*>(p); }
+};
+
+struct ReduceWs {
+    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs;
+    uint64_t* h_pinned = nullptr;  // small pinned staging
+};
+
+ReduceWs* reduce_ws_new() {
+    ReduceWs* w = new ReduceWs();
+    if (hipHostMalloc((void**)&w->h_pinned, 4096 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) w->h_pinned = nullptr;
+    return w;
+}
+
+void reduce_ws_free(ReduceWs* w) {
+    if (!w) return;
+    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs};
+    for (DBuf* b : bs) b->release();
+    if (w->h_pinned) hipHostFree(w->h_pinned);
+    delete w;
+}
+
+// flags[0]: any long record, flags[1]: any k1 != 0, flags[2]: tied runs found
+__global__ void rec_flags_kernel(Recs r, unsigned long long* flags) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    bool lng = false, k1 = false;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += stride) {
+        lng |= r.len[i] > 16;
+        k1 |= r.k1[i] != 0;
+    }
+    if (__ballot(lng) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1ull);
+    if (__ballot(k1) && (threadIdx.x & 63) == 0) atomicOr(&flags[1], 1ull);
+}
+
+__global__ void iota_kernel(uint32_t* p, uint64_t n) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = (uint32_t)i;
+}
+
+// which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part
+__global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t j = perm[i];
+        if (which == 0) k32[i] = r.len[j];
+        else if (which == 1) k64[i] = __builtin_bswap64(r.k1[j]);
+        else if (which == 2) k64[i] = __builtin_bswap64(r.k0[j]);
+        else k32[i] = r.part[j];
+    }
+}
+
+__device__ __forceinline__ const uint8_t* rec_bytes(const Recs& r, uint32_t j, uint8_t* tmp16) {
+    if (r.koff[j] != ~0ull) return r.arena + r.koff[j];
+    uint64_t k0 = r.k0[j], k1 = r.k1[j];
+    for (int k = 0; k < 8; k++) {
+        tmp16[k] = (uint8_t)(k0 >> (8 * k));
+        tmp16[8 + k] = (uint8_t)(k1 >> (8 * k));
+    }
+    return tmp16;
+}
+
+__device__ int rec_cmp(const Recs& r, uint32_t a, uint32_t b) {
+    uint8_t ta[16], tb[16];
+    const uint8_t* pa = rec_bytes(r, a, ta);
+    const uint8_t* pb = rec_bytes(r, b, tb);
+    uint32_t la = r.len[a], lb = r.len[b];
+    uint32_t m = la < lb ? la : lb;
+    for (uint32_t k = 0; k < m; k++)
+        if (pa[k] != pb[k]) return pa[k] < pb[k] ? -1 : 1;
+    return (la > lb) - (la < lb);
+}
+
+__device__ __forceinline__ bool same_sort_key(const Recs& r, uint32_t a, uint32_t b) {
+    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && r.k1[a] == r.k1[b] && r.len[a] == r.len[b];
+}
+
+// tie[i] = 1 when sorted position i has the same (part, prefix, len) as i-1
+__global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8_t* tie, unsigned long long* flags) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint8_t t = 0;
+        if (i > 0 && r.len[perm[i]] > 16 && same_sort_key(r, perm[i - 1], perm[i])) t = 1;
+        tie[i] = t;
+        if (t) atomicOr(&flags[2], 1ull);
+    }
+}
+
+// Insertion sort of each tied run by full bytewise comparison (runs are tiny in practice).
+__global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_t* tie) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
+        if (tie[i] || !tie[i + 1]) continue;
+        uint64_t e = i + 1;
+        while (e < n && tie[e]) e++;
+        for (uint64_t a = i + 1; a < e; a++) {
+            uint32_t v = perm[a];
+            uint64_t b = a;
+            while (b > i && rec_cmp(r, perm[b - 1], v) > 0) {
+                perm[b] = perm[b - 1];
+                b--;
+            }
+            perm[b] = v;
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t ndigits(uint64_t v) {
+    uint32_t d = 1;
+    while (v >= 10) { v /= 10; d++; }
+    return d;
+}
+
+__global__ void line_len_kernel(Recs r, const uint32_t* perm, uint64_t n, int app, uint64_t* ll) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t j = perm[i];
+        uint64_t len = r.len[j];
+        ll[i] = len + 2 + (app == 1 ? ndigits(r.cnt[j]) : len);
+    }
+}
+
+__global__ void write_lines_kernel(Recs r, const uint32_t* perm, uint64_t n, int app, const uint64_t* off, uint8_t* out) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        uint32_t j = perm[i];
+        uint8_t tmp[16];
+        const uint8_t* kb = rec_bytes(r, j, tmp);
+        uint32_t len = r.len[j];
+        uint8_t* o = out + off[i];
+        for (uint32_t k = 0; k < len; k++) o[k] = kb[k];
+        o += len;
+        *o++ = ' ';
+        if (app == 1) {
+            uint64_t v = r.cnt[j];
+            uint32_t d = ndigits(v);
+            for (uint32_t k = d; k > 0; k--) { o[k - 1] = (uint8_t)('0' + v % 10); v /= 10; }
+            o += d;
+        } else {
+            for (uint32_t k = 0; k < len; k++) o[k] = kb[k];
+            o += len;
+        }
+        *o = '\n';
+    }
+}
+
+// offsets[p] = byte offset of the first line of partition p (lower bound on sorted part).
+__global__ void part_offsets_kernel(Recs r, const uint32_t* perm, uint64_t n, const uint64_t* off, uint64_t total,
+                                    uint32_t nparts, uint64_t* offsets) {
+    uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p > nparts) return;
+    if (p == nparts) { offsets[p] = total; return; }
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+        uint64_t mid = (lo + hi) >> 1;
+        if (r.part[perm[mid]] < p) lo = mid + 1; else hi = mid;
+    }
+    offsets[p] = lo < n ? off[lo] : total;
+}
+
+__global__ void select_kernel(Recs src, uint32_t mod, uint32_t want, Recs dst, unsigned long long* cnt) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < src.n; i += stride) {
+        if (src.part[i] % mod != want) continue;
+        unsigned long long o = atomicAdd(cnt, 1ull);
+        dst.k0[o] = src.k0[i];
+        dst.k1[o] = src.k1[i];
+        dst.len[o] = src.len[i];
+        dst.cnt[o] = src.cnt[i];
+        dst.part[o] = src.part[i];
+        dst.koff[o] = src.koff[i];
+    }
+}
+
+static inline unsigned grid_for(uint64_t n) {
+    uint64_t g = (n + 255) / 256;
+    if (g < 1) g = 1;
+    if (g > 4096) g = 4096;
+    return (unsigned)g;
+}
+
+#define RCHK(x)                                   \
+    do {                                          \
+        hipError_t _e = (x);                      \
+        if (_e != hipSuccess) return (int)_e;     \
+    } while (0)
+
+template <class K>
+static int sort_pass(ReduceWs* ws, K* keys_in, K* keys_out, uint32_t* v_in, uint32_t* v_out, uint64_t n, unsigned bits,
+                     hipStream_t s) {
+    size_t tb = 0;
+    RCHK(rocprim::radix_sort_pairs(nullptr, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
+    RCHK(ws->tmp.ensure(tb));
+    RCHK(rocprim::radix_sort_pairs(ws->tmp.p, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
+    return 0;
+}
+
+int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst, hipStream_t s) {
+    // dst arrays must be preallocated by the caller with src.n capacity; arena shared with src.
+    unsigned long long* cnt = nullptr;
+    RCHK(ws->flags.ensure(64));
+    cnt = ws->flags.as<unsigned long long>();
+    RCHK(hipMemsetAsync(cnt, 0, 8, s));
+    if (src.n) select_kernel<<<grid_for(src.n), 256, 0, s>>>(src, mod, want, *dst, cnt);
+    RCHK(hipMemcpyAsync(ws->h_pinned, cnt, 8, hipMemcpyDeviceToHost, s));
+    RCHK(hipStreamSynchronize(s));
+    dst->n = ws->h_pinned[0];
+    dst->arena = src.arena;
+    dst->arena_n = src.arena_n;
+    return 0;
+}
+
+int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,
+                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s) {
+    const uint64_t n = r.n;
+    const bool all = only_part == 0xFFFFFFFFu;
+    const uint32_t nparts = all ? nreduce : 1;
+    if (n == 0) {
+        for (uint32_t p = 0; p <= nparts; p++) h_offsets[p] = 0;
+        *out_n = 0;
+        RCHK(ws->out.ensure(16));
+        *d_out = ws->out.as<uint8_t>();
+        return 0;
+    }
+    RCHK(ws->flags.ensure(64));
+    unsigned long long* flags = ws->flags.as<unsigned long long>();
+    RCHK(hipMemsetAsync(flags, 0, 64, s));
+    rec_flags_kernel<<<grid_for(n), 256, 0, s>>>(r, flags);
+    RCHK(hipMemcpyAsync(ws->h_pinned, flags, 24, hipMemcpyDeviceToHost, s));
+    RCHK(ws->perm_a.ensure(n * 4));
+    RCHK(ws->perm_b.ensure(n * 4));
+    RCHK(ws->key_a.ensure(n * 8));
+    RCHK(ws->key_b.ensure(n * 8));
+    RCHK(ws->lineoff.ensure(n * 8 + 8));
+    RCHK(hipStreamSynchronize(s));
+    const bool has_long = ws->h_pinned[0] != 0, has_k1 = ws->h_pinned[1] != 0;
+
+    uint32_t* pa = ws->perm_a.as<uint32_t>();
+    uint32_t* pb = ws->perm_b.as<uint32_t>();
+    iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
+    auto pass32 = [&](int which, unsigned bits) -> int {
+        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, nullptr, ws->key_a.as<uint32_t>());
+        int e = sort_pass<uint32_t>(ws, ws->key_a.as<uint32_t>(), ws->key_b.as<uint32_t>(), pa, pb, n, bits, s);
+        std::swap(pa, pb);
+        return e;
+    };
+    auto pass64 = [&](int which) -> int {
+        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, ws->key_a.as<uint64_t>(), nullptr);
+        int e = sort_pass<uint64_t>(ws, ws->key_a.as<uint64_t>(), ws->key_b.as<uint64_t>(), pa, pb, n, 64, s);
+        std::swap(pa, pb);
+        return e;
+    };
+    int e;
+    if (has_long && (e = pass32(0, 32))) return e;
+    if (has_k1 && (e = pass64(1))) return e;
+    if ((e = pass64(2))) return e;
+    if (all && nreduce > 1) {
+        unsigned bits = 1;
+        while ((1ull << bits) < nreduce) bits++;
+        if ((e = pass32(3, bits))) return e;
+    }
+    if (has_long) {
+        uint8_t* tie = ws->key_a.as<uint8_t>();
+        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags);
+        fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie);
+    }
+    uint64_t* ll = ws->key_b.as<uint64_t>();
+    uint64_t* off = ws->lineoff.as<uint64_t>();
+    line_len_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, app, ll);
+    size_t tb = 0;
+    RCHK(rocprim::exclusive_scan(nullptr, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+    RCHK(ws->tmp.ensure(tb));
+    RCHK(rocprim::exclusive_scan(ws->tmp.p, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+    RCHK(hipMemcpyAsync(ws->h_pinned, off + (n - 1), 8, hipMemcpyDeviceToHost, s));
+    RCHK(hipMemcpyAsync(ws->h_pinned + 1, ll + (n - 1), 8, hipMemcpyDeviceToHost, s));
+    RCHK(hipStreamSynchronize(s));
+    const uint64_t total = ws->h_pinned[0] + ws->h_pinned[1];
+    RCHK(ws->out.ensure(total + 16));
+    uint8_t* out = ws->out.as<uint8_t>();
+    write_lines_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, app, off, out);
+    if (all) {
+        RCHK(ws->offs.ensure((size_t)(nparts + 1) * 8));
+        part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, total, nparts, ws->offs.as<uint64_t>());
+        RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
+        RCHK(hipStreamSynchronize(s));
+    } else {
+        h_offsets[0] = 0;
+        h_offsets[1] = total;
+    }
+    *d_out = out;
+    *out_n = total;
+    return 0;
+}
+
+}  // namespace mrg

@@ -1,0 +1,312 @@
+"""ctypes binding of the C ABI in include/mrgpu.h (build/libmrgpu.so).
+
+The HIP library is the product: there is no CPU fallback.  If the library is
+missing or no GPU is visible, the calls raise — never silently compute on the
+host.
+
+Load order matters on this image: torch ships its own ROCm runtime
+(libamdhip64.so.7 / librccl.so.1 under torch/lib).  If torch is imported first,
+our library's DT_NEEDED entries resolve by SONAME to those already-loaded
+copies, so one HIP runtime serves both; so this module imports torch (when it
+is installed) before dlopen-ing libmrgpu.so.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, byref, c_char_p, c_int, c_int64, c_size_t, c_uint8, c_uint32, c_uint64, c_void_p
+
+try:  # share torch's HIP runtime when torch is present (see module docstring)
+    import torch  # noqa: F401
+except Exception:  # pragma: no cover - torch is optional for the C ABI itself
+    torch = None
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BUILD_DIR = os.path.join(PKG_DIR, "build")
+LIB_PATH = os.path.join(BUILD_DIR, "libmrgpu.so")
+
+MRG_OK = 0
+MRG_APP_WC = 1
+MRG_APP_GREP = 2
+MRG_INPUT_HOST = 0
+MRG_INPUT_DEVICE = 1
+ALL_PARTS = 0xFFFFFFFF
+
+# every symbol declared in include/mrgpu.h (checked by tests/test_abi.py)
+EXPORTED = [
+    "mrg_open", "mrg_close", "mrg_last_error", "mrg_device_count", "mrg_map", "mrg_parts_merge",
+    "mrg_parts_info", "mrg_parts_export", "mrg_parts_import", "mrg_parts_free", "mrg_reduce",
+    "mrg_reduce_all", "mrg_run_job", "mrg_comm_unique_id", "mrg_comm_init", "mrg_exchange",
+    "mrg_device_alloc", "mrg_device_free", "mrg_memcpy_h2d", "mrg_memcpy_d2h", "mrg_sync",
+    "mrg_get_stats", "mrg_set_option", "mrg_ihash", "mrg_free",
+]
+
+
+class MrgError(RuntimeError):
+    pass
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("map_kernel_ms", ctypes.c_double),
+        ("map_total_ms", ctypes.c_double),
+        ("exchange_ms", ctypes.c_double),
+        ("reduce_ms", ctypes.c_double),
+        ("d2h_ms", ctypes.c_double),
+        ("input_bytes", c_uint64),
+        ("distinct_keys", c_uint64),
+        ("output_bytes", c_uint64),
+        ("long_keys", c_uint64),
+        ("lds_overflow", c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def load_library(path: str | None = None):
+    """dlopen libmrgpu.so and declare prototypes.  Raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise MrgError(f"{p} not built: run `make -C distributed-systems-implemented_amd lib` "
+                       "or __graft_entry__.build()")
+    L = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    vp = c_void_p
+    L.mrg_open.argtypes = [c_int, POINTER(vp)]
+    L.mrg_close.argtypes = [vp]
+    L.mrg_close.restype = None
+    L.mrg_last_error.argtypes = [vp]
+    L.mrg_last_error.restype = c_char_p
+    L.mrg_device_count.argtypes = [POINTER(c_int)]
+    L.mrg_map.argtypes = [vp, c_int, vp, c_size_t, c_int, vp, c_size_t, c_uint32, POINTER(vp)]
+    L.mrg_parts_merge.argtypes = [vp, vp, vp]
+    L.mrg_parts_info.argtypes = [vp, POINTER(c_uint64), POINTER(c_uint32), POINTER(c_int)]
+    L.mrg_parts_export.argtypes = [vp, vp, c_uint32, POINTER(vp), POINTER(c_size_t)]
+    L.mrg_parts_import.argtypes = [vp, vp, c_size_t, POINTER(vp)]
+    L.mrg_parts_free.argtypes = [vp]
+    L.mrg_parts_free.restype = None
+    L.mrg_reduce.argtypes = [vp, vp, c_uint32, POINTER(vp), POINTER(c_size_t)]
+    L.mrg_reduce_all.argtypes = [vp, vp, POINTER(vp), POINTER(c_size_t), POINTER(c_uint64)]
+    L.mrg_run_job.argtypes = [vp, c_int, vp, c_size_t, c_int, vp, c_size_t, c_uint32, POINTER(vp),
+                              POINTER(c_size_t), POINTER(c_uint64)]
+    L.mrg_comm_unique_id.argtypes = [POINTER(c_uint8)]
+    L.mrg_comm_init.argtypes = [vp, POINTER(c_uint8), c_int, c_int]
+    L.mrg_exchange.argtypes = [vp, vp, POINTER(vp)]
+    L.mrg_device_alloc.argtypes = [vp, c_size_t, POINTER(vp)]
+    L.mrg_device_free.argtypes = [vp, vp]
+    L.mrg_memcpy_h2d.argtypes = [vp, vp, vp, c_size_t]
+    L.mrg_memcpy_d2h.argtypes = [vp, vp, vp, c_size_t]
+    L.mrg_sync.argtypes = [vp]
+    L.mrg_get_stats.argtypes = [vp, POINTER(Stats)]
+    L.mrg_set_option.argtypes = [vp, c_char_p, c_int64]
+    L.mrg_ihash.argtypes = [vp, c_size_t]
+    L.mrg_ihash.restype = c_uint32
+    L.mrg_free.argtypes = [vp]
+    L.mrg_free.restype = None
+    _lib = L
+    return L
+
+
+def _buf(data):
+    """(pointer, keepalive) for bytes / bytearray / numpy arrays."""
+    if isinstance(data, bytes):
+        return ctypes.cast(ctypes.c_char_p(data), c_void_p), data
+    try:
+        import numpy as np
+        if isinstance(data, np.ndarray):
+            a = np.ascontiguousarray(data)
+            return c_void_p(a.ctypes.data), a
+    except ImportError:  # pragma: no cover
+        pass
+    if isinstance(data, (bytearray, memoryview)):
+        b = (ctypes.c_char * len(data)).from_buffer(data)
+        return ctypes.cast(b, c_void_p), b
+    raise TypeError(type(data))
+
+
+def device_count() -> int:
+    L = load_library()
+    n = c_int(0)
+    L.mrg_device_count(byref(n))
+    return n.value
+
+
+def ihash(key: bytes) -> int:
+    """mr/worker.go:33-37 through the library (host helper)."""
+    L = load_library()
+    return int(L.mrg_ihash(_buf(key)[0], len(key)))
+
+
+class Parts:
+    """Device-resident Map output (distinct keys with counts and partitions)."""
+
+    def __init__(self, ctx: "Context", handle: c_void_p):
+        self.ctx = ctx
+        self.h = handle
+
+    def info(self):
+        n, r, a = c_uint64(), c_uint32(), c_int()
+        self.ctx.L.mrg_parts_info(self.h, byref(n), byref(r), byref(a))
+        return n.value, r.value, a.value
+
+    def free(self):
+        if self.h:
+            self.ctx.L.mrg_parts_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Context:
+    """One GPU context (mrg_open).  Not thread-safe; one per device/thread."""
+
+    def __init__(self, device: int = 0):
+        self.L = load_library()
+        h = c_void_p()
+        rc = self.L.mrg_open(device, byref(h))
+        if rc != MRG_OK:
+            raise MrgError(f"mrg_open({device}) failed with {rc} (no GPU visible?)")
+        self.h = h
+        self.device = device
+
+    # -- errors
+    def _check(self, rc, what):
+        if rc != MRG_OK:
+            msg = self.L.mrg_last_error(self.h)
+            raise MrgError(f"{what} failed ({rc}): {msg.decode(errors='replace') if msg else ''}")
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.L.mrg_close(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    def set_option(self, name: str, value: int):
+        self._check(self.L.mrg_set_option(self.h, name.encode(), int(value)), f"set_option({name})")
+
+    def stats(self) -> dict:
+        s = Stats()
+        self._check(self.L.mrg_get_stats(self.h, byref(s)), "get_stats")
+        return s.as_dict()
+
+    # -- host result helper
+    def _take(self, p: c_void_p, n: int, free=True) -> bytes:
+        out = ctypes.string_at(p, n) if n else b""
+        if free:
+            self.L.mrg_free(p)
+        return out
+
+    # -- map / reduce
+    def map(self, app: int, data, pattern: bytes = b"", nreduce: int = 10, device_ptr: int | None = None,
+            nbytes: int | None = None) -> Parts:
+        out = c_void_p()
+        pat_p, _kp = _buf(pattern) if pattern else (None, None)
+        if device_ptr is not None:
+            rc = self.L.mrg_map(self.h, app, c_void_p(device_ptr), nbytes, MRG_INPUT_DEVICE, pat_p, len(pattern),
+                                nreduce, byref(out))
+        else:
+            p, _keep = _buf(data)
+            rc = self.L.mrg_map(self.h, app, p, len(data), MRG_INPUT_HOST, pat_p, len(pattern), nreduce, byref(out))
+        self._check(rc, "mrg_map")
+        return Parts(self, out)
+
+    def merge(self, into: Parts, frm: Parts):
+        self._check(self.L.mrg_parts_merge(self.h, into.h, frm.h), "mrg_parts_merge")
+
+    def export(self, parts: Parts, r: int = ALL_PARTS) -> bytes:
+        p, n = c_void_p(), c_size_t()
+        self._check(self.L.mrg_parts_export(self.h, parts.h, r, byref(p), byref(n)), "mrg_parts_export")
+        return self._take(p, n.value)
+
+    def import_(self, data: bytes) -> Parts:
+        out = c_void_p()
+        p, _keep = _buf(data)
+        self._check(self.L.mrg_parts_import(self.h, p, len(data), byref(out)), "mrg_parts_import")
+        return Parts(self, out)
+
+    def reduce(self, parts: Parts, r: int) -> bytes:
+        p, n = c_void_p(), c_size_t()
+        self._check(self.L.mrg_reduce(self.h, parts.h, r, byref(p), byref(n)), "mrg_reduce")
+        return self._take(p, n.value)
+
+    def reduce_all(self, parts: Parts) -> list[bytes]:
+        _, nreduce, _ = parts.info()
+        p, n = c_void_p(), c_size_t()
+        offs = (c_uint64 * (nreduce + 1))()
+        self._check(self.L.mrg_reduce_all(self.h, parts.h, byref(p), byref(n), offs), "mrg_reduce_all")
+        data = self._take(p, n.value)
+        return [data[offs[i]:offs[i + 1]] for i in range(nreduce)]
+
+    def run_job(self, app: int, data=None, pattern: bytes = b"", nreduce: int = 10, device_ptr: int | None = None,
+                nbytes: int | None = None, copy_out: bool = True):
+        """map + (exchange) + reduce_all.  Returns list of mr-out-r bytes (or (ptr, n, offsets) if not copy_out)."""
+        p, n = c_void_p(), c_size_t()
+        offs = (c_uint64 * (nreduce + 1))()
+        pat_p, _kp = _buf(pattern) if pattern else (None, None)
+        if device_ptr is not None:
+            rc = self.L.mrg_run_job(self.h, app, c_void_p(device_ptr), nbytes, MRG_INPUT_DEVICE, pat_p, len(pattern),
+                                    nreduce, byref(p), byref(n), offs)
+        else:
+            buf, _keep = _buf(data)
+            rc = self.L.mrg_run_job(self.h, app, buf, len(data), MRG_INPUT_HOST, pat_p, len(pattern), nreduce,
+                                    byref(p), byref(n), offs)
+        self._check(rc, "mrg_run_job")
+        if not copy_out:
+            return p.value, n.value, list(offs)
+        data = ctypes.string_at(p, n.value) if n.value else b""  # context-owned buffer: no mrg_free
+        return [data[offs[i]:offs[i + 1]] for i in range(nreduce)]
+
+    # -- multi-GPU
+    @staticmethod
+    def unique_id() -> bytes:
+        L = load_library()
+        a = (c_uint8 * 128)()
+        rc = L.mrg_comm_unique_id(a)
+        if rc != MRG_OK:
+            raise MrgError(f"mrg_comm_unique_id failed ({rc})")
+        return bytes(a)
+
+    def comm_init(self, uid: bytes, nranks: int, rank: int):
+        a = (c_uint8 * 128).from_buffer_copy(uid)
+        self._check(self.L.mrg_comm_init(self.h, a, nranks, rank), "mrg_comm_init")
+
+    def exchange(self, parts: Parts) -> Parts:
+        out = c_void_p()
+        self._check(self.L.mrg_exchange(self.h, parts.h, byref(out)), "mrg_exchange")
+        return Parts(self, out)
+
+    # -- device memory
+    def device_alloc(self, n: int) -> int:
+        d = c_void_p()
+        self._check(self.L.mrg_device_alloc(self.h, n, byref(d)), "mrg_device_alloc")
+        return d.value
+
+    def device_free(self, d: int):
+        self._check(self.L.mrg_device_free(self.h, c_void_p(d)), "mrg_device_free")
+
+    def h2d(self, dst: int, data, n: int | None = None):
+        p, _keep = _buf(data)
+        self._check(self.L.mrg_memcpy_h2d(self.h, c_void_p(dst), p, n if n is not None else len(data)), "h2d")
+
+    def d2h(self, src: int, n: int) -> bytes:
+        b = ctypes.create_string_buffer(n)
+        self._check(self.L.mrg_memcpy_d2h(self.h, b, c_void_p(src), n), "d2h")
+        return b.raw
+
+    def sync(self):
+        self._check(self.L.mrg_sync(self.h), "mrg_sync")

@@ -1,0 +1,138 @@
+/*
+ * mrgpu.h — C ABI of the MI355X-native MapReduce hot path (wc / grep).
+ *
+ * This is the drop-in boundary of BASELINE.json's north_star: mr/worker.go hands
+ * whole input splits to these entry points (through cgo)
+ * instead of running the plugin's Map + ihash partition loop and the
+ * sort/group/Reduce loop on the CPU.  Plain C types only; no torch types.
+ *
+ * Reference interfaces replaced (paths under MapReduce/ of the reference):
+ *   mrg_map            mrapps/wc.go:21-34 (Map) or mrapps/dgrep.go:18-36 (grepMap)
+ *                      + mr/worker.go:69-78 (mapf call, ihash(key) % NReduce bucketing)
+ *   mrg_parts_export   mr/worker.go:80-92  (write bucket r of map task X -> intermediate mr-X-r)
+ *   mrg_parts_import   mr/worker.go:100-122 (read mr-i-Y back for reduce task Y)
+ *   mrg_parts_merge    mr/worker.go:120 / mrsequential.go:50 (append intermediate KVs)
+ *   mrg_reduce         mr/worker.go:123-146 (sort.Sort(ByKey), group, reducef, Fprintf "%v %v\n")
+ *                      + mrapps/wc.go:41-44 (Reduce) or mrapps/dgrep.go:44-46 (grepReduce)
+ *   mrg_reduce_all     every partition at once; with nreduce = 1 it is
+ *                      main/mrsequential.go:59-84 (single mr-out-0)
+ *   mrg_exchange       the M x R intermediate-file shuffle (mr/worker.go:80-122) across GPUs,
+ *                      as an RCCL all-to-all over xGMI keyed by ihash(key) % nReduce
+ *   mrg_ihash          mr/worker.go:33-37 (host helper, same FNV-1a-32 & 0x7fffffff)
+ *
+ * Semantics are bit-exact with the reference: words are maximal runs of runes
+ * with unicode.IsLetter (Unicode 13.0.0), invalid UTF-8 bytes decode to U+FFFD
+ * (a separator); partition = (fnv1a32(key) & 0x7fffffff) % nreduce; output lines
+ * are sorted by unsigned bytewise key order; wc prints the decimal count, grep
+ * prints the line twice ("L L\n").  Every partition yields its (possibly empty)
+ * output, as worker.go:126-148 always writes mr-out-r.
+ *
+ * Errors: every int-returning call returns MRG_OK (0) or a negative MRG_E* code
+ * and leaves a message in mrg_last_error(ctx).  The library never aborts the
+ * process (the Go shim maps a nonzero code to log.Fatalf as worker.go:60-64 does).
+ *
+ * Threading: a context is bound to one device and is not re-entrant; every entry
+ * point re-binds its device (cgo calls may migrate OS threads).  Several contexts
+ * per process are allowed (one per GPU thread).
+ *
+ * Ownership: input buffers are borrowed for the duration of the call only (cgo
+ * pointer rules); outputs are library-owned and released with mrg_free /
+ * mrg_parts_free.
+ */
+#ifndef MRGPU_H
+#define MRGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MRG_OK 0
+#define MRG_EINVAL (-1)   /* bad argument */
+#define MRG_EDEVICE (-2)  /* HIP runtime / kernel error */
+#define MRG_ENOMEM (-3)   /* device or host allocation failed */
+#define MRG_ECOMM (-4)    /* RCCL error */
+#define MRG_EFORMAT (-5)  /* malformed intermediate bytes */
+
+#define MRG_APP_WC 1      /* mrapps/wc.go */
+#define MRG_APP_GREP 2    /* mrapps/dgrep.go, fixed literal pattern */
+
+#define MRG_INPUT_HOST 0  /* buf is a host pointer (copied to HBM by the call) */
+#define MRG_INPUT_DEVICE 1/* buf is a device pointer already resident in HBM */
+
+typedef struct mrg_ctx mrg_ctx;
+typedef struct mrg_parts mrg_parts;
+
+/* Per-call timing of the last mrg_map / mrg_reduce_all / mrg_run_job, from HIP
+ * events on the context's stream (milliseconds). */
+typedef struct {
+    double map_kernel_ms;     /* the tokenizer/aggregation kernel alone (dominant kernel) */
+    double map_total_ms;      /* map: every kernel from first launch to last */
+    double exchange_ms;       /* RCCL all-to-all (0 when single-GPU) */
+    double reduce_ms;         /* collect + sort + format */
+    double d2h_ms;            /* output bytes to host */
+    uint64_t input_bytes;     /* bytes mapped */
+    uint64_t distinct_keys;   /* distinct keys after aggregation */
+    uint64_t output_bytes;    /* total mr-out bytes */
+    uint64_t long_keys;       /* keys > 16 bytes (slow path) */
+    uint64_t lds_overflow;    /* occurrences that missed the LDS table and went to HBM */
+} mrg_stats;
+
+int mrg_open(int device, mrg_ctx** out);
+void mrg_close(mrg_ctx* ctx);
+const char* mrg_last_error(const mrg_ctx* ctx);
+int mrg_device_count(int* n);
+
+/* Map one input split (one file = one map task).  app = MRG_APP_WC or MRG_APP_GREP
+ * (pat/plen = the literal; ignored for wc).  Output: device-resident partial
+ * aggregates (distinct key, count, partition) for all nreduce partitions. */
+int mrg_map(mrg_ctx* ctx, int app, const void* buf, size_t len, int input_kind, const uint8_t* pat,
+            size_t plen, uint32_t nreduce, mrg_parts** out);
+/* Combine `from` into `into` (both on ctx's device, same app and nreduce). */
+int mrg_parts_merge(mrg_ctx* ctx, mrg_parts* into, const mrg_parts* from);
+/* Number of distinct keys held. */
+int mrg_parts_info(const mrg_parts* p, uint64_t* nkeys, uint32_t* nreduce, int* app);
+/* Serialize partition r (r = UINT32_MAX: all) to library-owned host bytes. */
+int mrg_parts_export(mrg_ctx* ctx, const mrg_parts* p, uint32_t r, void** bytes, size_t* n);
+int mrg_parts_import(mrg_ctx* ctx, const void* bytes, size_t n, mrg_parts** out);
+void mrg_parts_free(mrg_parts* p);
+
+/* Reduce partition r: exact mr-out-r bytes (library-owned host buffer). */
+int mrg_reduce(mrg_ctx* ctx, const mrg_parts* p, uint32_t r, void** bytes, size_t* n);
+/* Reduce every partition: bytes of mr-out-0..R-1 back to back; offsets[R+1]. */
+int mrg_reduce_all(mrg_ctx* ctx, const mrg_parts* p, void** bytes, size_t* n, uint64_t* offsets);
+
+/* Whole job on one device: map + (exchange) + reduce_all.  With a communicator
+ * attached (mrg_comm_init), every rank maps its own split and receives the
+ * partitions it owns (r % nranks == rank); offsets[] then index all R partitions
+ * and non-owned ones are empty. */
+int mrg_run_job(mrg_ctx* ctx, int app, const void* buf, size_t len, int input_kind, const uint8_t* pat,
+                size_t plen, uint32_t nreduce, void** bytes, size_t* n, uint64_t* offsets);
+
+/* Multi-GPU (one process or thread per GPU).  The 128-byte unique id is made by
+ * one rank and shared out of band (the coordinator RPC stays unchanged). */
+int mrg_comm_unique_id(uint8_t id[128]);
+int mrg_comm_init(mrg_ctx* ctx, const uint8_t id[128], int nranks, int rank);
+/* Send every key to the owner of its partition; returns the owned partials. */
+int mrg_exchange(mrg_ctx* ctx, const mrg_parts* local, mrg_parts** owned);
+
+/* Device memory helpers so callers can keep inputs resident in HBM. */
+int mrg_device_alloc(mrg_ctx* ctx, size_t n, void** dptr);
+int mrg_device_free(mrg_ctx* ctx, void* dptr);
+int mrg_memcpy_h2d(mrg_ctx* ctx, void* dst, const void* src, size_t n);
+int mrg_memcpy_d2h(mrg_ctx* ctx, void* dst, const void* src, size_t n);
+int mrg_sync(mrg_ctx* ctx);
+int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
+
+/* Tuning knobs (0 = default); for benchmarks and tests of the overflow paths. */
+int mrg_set_option(mrg_ctx* ctx, const char* name, int64_t value);
+
+uint32_t mrg_ihash(const uint8_t* key, size_t n);
+void mrg_free(void* p);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MRGPU_H */

@@ -1,0 +1,231 @@
+/*
+ * mroracle.c — C restatement of the reference MapReduce hot path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This is the oracle (the checker).  Only tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg may load or run it.
+ * The product library (distributed-systems-implemented_amd/csrc) never links it.
+ *
+ * Parity status: *parity unpinned* against reference-run outputs (the Go
+ * reference cannot be built here — no Go toolchain — and ships no fixtures).
+ * Pinned instead to: published FNV-1a-32 KATs, the Unicode 13.0.0 UCD via
+ * oracle/letter_ranges.h (generated from Python unicodedata), Go's UTF-8
+ * acceptance ranges, and the Python restatement oracle/mr_oracle.py (the
+ * golden fixtures in tests/golden/ are produced by that one and checked
+ * against this one).
+ *
+ * Restated reference functions (paths under /root/reference/MapReduce):
+ *   oracle_decode_rune   Go utf8.DecodeRuneInString (range loop in strings.FieldsFunc, mrapps/wc.go:26)
+ *   oracle_is_letter     unicode.IsLetter (mrapps/wc.go:23)
+ *   oracle_wc_words      wc.Map (mrapps/wc.go:21-34)
+ *   oracle_grep_lines    grepMap (mrapps/dgrep.go:18-36), literal pattern
+ *   oracle_ihash         ihash (mr/worker.go:33-37)
+ *   oracle_mrsequential  main/mrsequential.go:38-86 (map all, sort.Sort(ByKey), group, Reduce, Fprintf)
+ *   oracle_mr_partitioned mr/worker.go:72-78 (ihash % nReduce) + :123-146 (per-partition reduce)
+ */
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <stdio.h>
+
+#include "letter_ranges.h"
+
+#define ORACLE_APP_WC 1
+#define ORACLE_APP_GREP 2
+
+/* unicode.IsLetter: Latin-1 via the explicit list of SURVEY Appendix A.2, above
+ * that a binary search over the L* ranges (Go: isExcludingLatin(Letter, r)). */
+int oracle_is_letter(uint32_t cp) {
+    if (cp < 0x80) return (cp >= 'A' && cp <= 'Z') || (cp >= 'a' && cp <= 'z');
+    int lo = 0, hi = ORACLE_NLETTER_RANGES - 1;
+    while (lo <= hi) {
+        int mid = (lo + hi) >> 1;
+        if (cp < oracle_letter_ranges[mid][0]) hi = mid - 1;
+        else if (cp > oracle_letter_ranges[mid][1]) lo = mid + 1;
+        else return 1;
+    }
+    return 0;
+}
+
+/* Go utf8.DecodeRuneInString: returns width; *cp = rune or 0xFFFD (width 1). */
+size_t oracle_decode_rune(const uint8_t* s, size_t n, size_t i, uint32_t* cp) {
+    uint8_t c0 = s[i];
+    if (c0 < 0x80) { *cp = c0; return 1; }
+    *cp = 0xFFFD;
+    if (c0 < 0xC2 || c0 > 0xF4) return 1;
+    size_t need; uint8_t lo = 0x80, hi = 0xBF; uint32_t v;
+    if (c0 < 0xE0) { need = 1; v = c0 & 0x1F; }
+    else if (c0 < 0xF0) {
+        need = 2; v = c0 & 0x0F;
+        if (c0 == 0xE0) lo = 0xA0; else if (c0 == 0xED) hi = 0x9F;
+    } else {
+        need = 3; v = c0 & 0x07;
+        if (c0 == 0xF0) lo = 0x90; else if (c0 == 0xF4) hi = 0x8F;
+    }
+    if (i + need >= n) return 1;
+    uint8_t c1 = s[i + 1];
+    if (c1 < lo || c1 > hi) return 1;
+    v = (v << 6) | (c1 & 0x3F);
+    for (size_t k = 2; k <= need; k++) {
+        uint8_t ck = s[i + k];
+        if (ck < 0x80 || ck > 0xBF) return 1;
+        v = (v << 6) | (ck & 0x3F);
+    }
+    *cp = v;
+    return need + 1;
+}
+
+uint32_t oracle_fnv1a32(const uint8_t* p, size_t n) {
+    uint32_t h = 2166136261u;
+    for (size_t i = 0; i < n; i++) { h ^= p[i]; h *= 16777619u; }
+    return h;
+}
+
+/* worker.go:33-37 */
+uint32_t oracle_ihash(const uint8_t* p, size_t n) { return oracle_fnv1a32(p, n) & 0x7fffffffu; }
+
+typedef struct { const uint8_t* p; uint32_t n; } okey;
+
+typedef struct { okey* v; size_t n, cap; } okeyvec;
+
+static void okv_push(okeyvec* kv, const uint8_t* p, size_t n) {
+    if (kv->n == kv->cap) {
+        kv->cap = kv->cap ? kv->cap * 2 : 1024;
+        kv->v = (okey*)realloc(kv->v, kv->cap * sizeof(okey));
+    }
+    kv->v[kv->n].p = p; kv->v[kv->n].n = (uint32_t)n; kv->n++;
+}
+
+/* wc.Map (wc.go:21-34): strings.FieldsFunc(contents, !unicode.IsLetter). */
+static void wc_words(const uint8_t* s, size_t n, okeyvec* out) {
+    size_t i = 0; long start = -1;
+    while (i < n) {
+        uint32_t cp; size_t w;
+        if (s[i] < 0x80) { cp = s[i]; w = 1; } else w = oracle_decode_rune(s, n, i, &cp);
+        if (oracle_is_letter(cp)) { if (start < 0) start = (long)i; }
+        else if (start >= 0) { okv_push(out, s + start, i - (size_t)start); start = -1; }
+        i += w;
+    }
+    if (start >= 0) okv_push(out, s + start, n - (size_t)start);
+}
+
+/* grepMap (dgrep.go:18-36): strings.Split(contents, "\n"); literal match per line. */
+static int contains(const uint8_t* h, size_t hn, const uint8_t* pat, size_t pn) {
+    if (pn == 0) return 1;
+    if (pn > hn) return 0;
+    for (size_t i = 0; i + pn <= hn; i++)
+        if (h[i] == pat[0] && memcmp(h + i, pat, pn) == 0) return 1;
+    return 0;
+}
+
+static void grep_lines(const uint8_t* s, size_t n, const uint8_t* pat, size_t pn, okeyvec* out) {
+    size_t ls = 0;
+    for (size_t i = 0; i <= n; i++) {
+        if (i == n || s[i] == '\n') {
+            if (contains(s + ls, i - ls, pat, pn)) okv_push(out, s + ls, i - ls);
+            ls = i + 1;
+        }
+    }
+}
+
+/* Exported word / line listing for tests: returns count; fills up to cap (offset,len). */
+size_t oracle_wc_words(const uint8_t* s, size_t n, uint64_t* offs, uint32_t* lens, size_t cap) {
+    okeyvec kv = {0};
+    wc_words(s, n, &kv);
+    for (size_t i = 0; i < kv.n && i < cap; i++) { offs[i] = (uint64_t)(kv.v[i].p - s); lens[i] = kv.v[i].n; }
+    size_t r = kv.n; free(kv.v); return r;
+}
+
+size_t oracle_grep_lines(const uint8_t* s, size_t n, const uint8_t* pat, size_t pn,
+                         uint64_t* offs, uint32_t* lens, size_t cap) {
+    okeyvec kv = {0};
+    grep_lines(s, n, pat, pn, &kv);
+    for (size_t i = 0; i < kv.n && i < cap; i++) { offs[i] = (uint64_t)(kv.v[i].p - s); lens[i] = kv.v[i].n; }
+    size_t r = kv.n; free(kv.v); return r;
+}
+
+/* ByKey.Less (worker.go:27): Go string '<' = unsigned bytewise, shorter prefix first. */
+static int key_cmp(const void* a, const void* b) {
+    const okey* x = (const okey*)a; const okey* y = (const okey*)b;
+    uint32_t m = x->n < y->n ? x->n : y->n;
+    int c = memcmp(x->p, y->p, m);
+    if (c) return c;
+    return (x->n > y->n) - (x->n < y->n);
+}
+
+typedef struct { uint8_t* b; size_t n, cap; } obuf;
+
+static void ob_put(obuf* o, const void* p, size_t n) {
+    if (o->n + n > o->cap) {
+        size_t c = o->cap ? o->cap : 4096;
+        while (c < o->n + n) c *= 2;
+        o->b = (uint8_t*)realloc(o->b, c); o->cap = c;
+    }
+    memcpy(o->b + o->n, p, n); o->n += n;
+}
+
+/* sort + group + Reduce + Fprintf("%v %v\n") — worker.go:123-146, mrsequential.go:59-84. */
+static void group_reduce(int app, okey* v, size_t n, obuf* out) {
+    qsort(v, n, sizeof(okey), key_cmp);
+    size_t i = 0;
+    char num[32];
+    while (i < n) {
+        size_t j = i + 1;
+        while (j < n && v[j].n == v[i].n && memcmp(v[j].p, v[i].p, v[i].n) == 0) j++;
+        ob_put(out, v[i].p, v[i].n);
+        ob_put(out, " ", 1);
+        if (app == ORACLE_APP_WC) {               /* wc.Reduce: strconv.Itoa(len(values)) */
+            int k = snprintf(num, sizeof num, "%zu", j - i);
+            ob_put(out, num, (size_t)k);
+        } else {                                   /* grepReduce: returns key */
+            ob_put(out, v[i].p, v[i].n);
+        }
+        ob_put(out, "\n", 1);
+        i = j;
+    }
+}
+
+static void map_files(int app, const uint8_t* pat, size_t pn, const uint8_t* const* files,
+                      const size_t* sizes, size_t nfiles, okeyvec* kv) {
+    for (size_t f = 0; f < nfiles; f++) {
+        if (app == ORACLE_APP_WC) wc_words(files[f], sizes[f], kv);
+        else grep_lines(files[f], sizes[f], pat, pn, kv);
+    }
+}
+
+/* mrsequential.go:25-87: returns malloc'd mr-out-0 bytes (caller frees with oracle_free). */
+int oracle_mrsequential(int app, const uint8_t* pat, size_t pn, const uint8_t* const* files,
+                        const size_t* sizes, size_t nfiles, uint8_t** out, size_t* out_n) {
+    okeyvec kv = {0};
+    map_files(app, pat, pn, files, sizes, nfiles, &kv);
+    obuf o = {0};
+    group_reduce(app, kv.v, kv.n, &o);
+    free(kv.v);
+    *out = o.b ? o.b : (uint8_t*)malloc(1); *out_n = o.n;
+    return 0;
+}
+
+/* Partitioned job: mr-out-r for r < nreduce, concatenated; offsets[nreduce+1]. */
+int oracle_mr_partitioned(int app, const uint8_t* pat, size_t pn, const uint8_t* const* files,
+                          const size_t* sizes, size_t nfiles, uint32_t nreduce,
+                          uint8_t** out, size_t* out_n, uint64_t* offsets) {
+    okeyvec kv = {0};
+    map_files(app, pat, pn, files, sizes, nfiles, &kv);
+    okeyvec* buckets = (okeyvec*)calloc(nreduce, sizeof(okeyvec));
+    for (size_t i = 0; i < kv.n; i++) {         /* worker.go:74-78 */
+        uint32_t r = oracle_ihash(kv.v[i].p, kv.v[i].n) % nreduce;
+        okv_push(&buckets[r], kv.v[i].p, kv.v[i].n);
+    }
+    free(kv.v);
+    obuf o = {0};
+    for (uint32_t r = 0; r < nreduce; r++) {
+        offsets[r] = o.n;
+        group_reduce(app, buckets[r].v, buckets[r].n, &o);
+        free(buckets[r].v);
+    }
+    offsets[nreduce] = o.n;
+    free(buckets);
+    *out = o.b ? o.b : (uint8_t*)malloc(1); *out_n = o.n;
+    return 0;
+}
+
+void oracle_free(void* p) { free(p); }

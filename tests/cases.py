@@ -1,0 +1,64 @@
+"""Shared parity inputs: edge cases the reference's semantics hinge on
+ plus seeded synthetic corpora."""
+from __future__ import annotations
+
+import random
+
+from mrgpu import corpus as C
+
+W16 = b"abcdefghijklmnop"  # exactly 16 letters (the inline-key limit)
+
+
+def edge_cases() -> dict[str, list[bytes]]:
+    """name -> list of files (each file = one map split)."""
+    big_word = b"Z" * 5000
+    rnd = random.Random(11)
+    noisy = bytes(rnd.randrange(256) for _ in range(20000))
+    utf8_mix = ("Ωμέγα, Привет мир! 中文字符 𐐷𐐸 ĳ ǅ ʰ ª º µ ß ÿ  x—y、z 😀 é "
+                "٠١ Ⅻ ⅻ ⓐ 〆 ー ｱ").encode() * 30
+    chunk_cross = (b"x" * 2040 + b" " + b"abcdefghijklmnopqrstuvwxyz " * 3 + b"k" * 2100 + b" end") * 3
+    return {
+        "empty": [b""],
+        "one_word": [b"hello"],
+        "no_trailing_sep": [b"alpha beta gamma"],
+        "only_separators": [b" \n\t,.;:!?0123456789 " * 50],
+        "w16_w17": [W16 + b" " + W16 + b"q " + W16[:-1] + b"\n" + W16 + b"qr"],
+        "case_sensitive": [b"The the THE tHe the The\nthe"],
+        "big_word": [big_word + b" " + big_word + b"\n" + b"small"],
+        "all_letters": [b"q" * 70000],
+        "chunk_cross": [chunk_cross],
+        "random_bytes": [noisy],
+        "utf8_mix": [utf8_mix],
+        "invalid_utf8": [b"ab\xffcd\xc0\xafef\xe2\x82gh\xed\xa0\x80ij\xf4\x90\x80\x80kl\xc3mn\x80op\xce\xbb\xce"],
+        "truncated_at_eof": [b"word \xe2\x82", b"x\xf0\x9f\x98"],
+        "multi_file": [b"one two three\n", b"two three\n", b"three"],
+        "apostrophes": [b"don't can't won't it's O'Neil rock'n'roll"],
+    }
+
+
+def grep_edge_cases() -> dict[str, tuple[list[bytes], bytes]]:
+    return {
+        "basic": ([b"a distributed system\nnothing here\ndistributed\n\ndistributed distributed x\n"], b"distributed"),
+        "cr_kept": ([b"line distributed\r\nother\r\n"], b"distributed"),
+        "dup_lines": ([b"x distributed\nx distributed\ny\nx distributed"], b"distributed"),
+        "utf8_pattern": (["καλημέρα κόσμε\nγεια σου κόσμε\nhello\n".encode()], "κόσμε".encode()),
+        "no_trailing_nl": ([b"abc\ndistributedness"], b"distributed"),
+        "pattern_at_edges": ([b"distributed" * 300 + b"\n" + b"q" * 3000 + b"distributed"], b"distributed"),
+        "long_pattern": ([(b"x" * 100 + b"\n") * 10 + b"y" * 70 + b"\n" + b"zz" + b"y" * 70 + b"zz\n"], b"y" * 70),
+        "empty_pattern": ([b"a\nb\n\nc"], b""),
+        "newline_pattern": ([b"a\nb\n"], b"a\nb"),
+        "multi_file": ([b"distributed one\n", b"distributed two\ndistributed one\n"], b"distributed"),
+        "long_lines": ([(b"w" * 5000 + b" distributed " + b"v" * 3000 + b"\n") * 3], b"distributed"),
+    }
+
+
+def synthetic(kind: int, V: int, sizes: list[int], seed: int, invalid_rate: float = 0.0) -> list[bytes]:
+    voc = C.Vocab(kind, 1.07, V, seed)
+    files = voc.fill_files(sizes, [seed * 1000 + i for i in range(len(sizes))], C.wc_params(invalid_rate))
+    return [bytes(f) for f in files]
+
+
+def synthetic_grep(V: int, sizes: list[int], seed: int, match_rate: float = 0.02) -> list[bytes]:
+    voc = C.Vocab(C.KIND_UTF8, 1.07, V, seed)
+    files = voc.fill_files(sizes, [seed * 1000 + i for i in range(len(sizes))], C.grep_params(match_rate=match_rate))
+    return [bytes(f) for f in files]

@@ -1,0 +1,64 @@
+"""Generate tests/golden/*.json from the *Python* restatement (oracle/mr_oracle.py).
+
+The reference ships no fixtures and cannot run here (pure Go, no toolchain), so
+these vectors are produced by this repo's restatement of mrsequential.go /
+worker.go and pinned by the published FNV-1a KATs and the Unicode 13.0.0 UCD.
+The C oracle (oracle/mroracle.c) and the GPU path are both checked against
+them.  Re-run:  python tests/golden/make_golden.py
+"""
+from __future__ import annotations
+
+import base64
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+sys.path.insert(0, os.path.join(ROOT, "distributed-systems-implemented_amd"))
+
+import mr_oracle as M  # noqa: E402
+import cases  # noqa: E402
+from mrgpu import corpus as C  # noqa: E402
+
+NREDUCES = (1, 10, 64)
+
+
+def enc(b: bytes) -> str:
+    return base64.b64encode(b).decode()
+
+
+def main():
+    wc = {}
+    for name, files in sorted(cases.edge_cases().items()):
+        wc[name] = {"files": [enc(f) for f in files],
+                    "out": {str(R): [enc(x) for x in M.mr_partitioned("wc", files, R)] for R in NREDUCES}}
+    # small synthetic corpora (generator output is itself pinned by test_corpus)
+    for tag, kind, V, seed, inv in [("syn_ascii", C.KIND_ASCII, 3000, 21, 0.0),
+                                    ("syn_utf8", C.KIND_UTF8, 3000, 22, 0.002)]:
+        files = cases.synthetic(kind, V, [40_000, 25_001], seed, inv)
+        wc[tag] = {"files": [enc(f) for f in files],
+                   "out": {str(R): [enc(x) for x in M.mr_partitioned("wc", files, R)] for R in NREDUCES}}
+    grep = {}
+    for name, (files, pat) in sorted(cases.grep_edge_cases().items()):
+        app = "grep:" + pat.decode()
+        grep[name] = {"files": [enc(f) for f in files], "pattern": enc(pat),
+                      "out": {str(R): [enc(x) for x in M.mr_partitioned(app, files, R)] for R in (1, 10)}}
+    files = cases.synthetic_grep(3000, [60_000], 23, match_rate=0.05)
+    grep["syn_grep"] = {"files": [enc(f) for f in files], "pattern": enc(b"distributed"),
+                        "out": {str(R): [enc(x) for x in M.mr_partitioned("grep:distributed", files, R)]
+                                for R in (1, 10)}}
+    kat_keys = [b"", b"a", b"foobar", b"the", b"The", b"distributed", "κόσμε".encode(), b"\xff\x00\x80"]
+    kat = {"fnv1a32": {enc(k): M.fnv1a32(k) for k in kat_keys},
+           "ihash": {enc(k): M.ihash(k) for k in kat_keys},
+           "published": {"": 0x811C9DC5, "a": 0xE40C292C, "foobar": 0xBF9CF968}}
+    for fname, obj in (("wc_cases.json", wc), ("grep_cases.json", grep), ("fnv_kat.json", kat)):
+        with open(os.path.join(HERE, fname), "w") as f:
+            json.dump(obj, f, indent=0, sort_keys=True)
+        print("wrote", fname)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,142 @@
+"""GPU parity: the HIP path (through the C ABI) vs the oracle, bit-exact.
+
+Gate: for every r, mr-out-r from the GPU equals the oracle's
+partition-r output byte for byte (the stricter per-partition check); with
+nreduce = 1 that is mrsequential's mr-out-0.  Also the reference's own check
+(test-mr.sh:52-53): sorted concatenation of mr-out-* equals sorted mr-out-0.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import _oracle as O
+import cases
+from mrgpu import ALL_PARTS, MRG_APP_GREP, MRG_APP_WC
+from mrgpu import corpus as C
+
+pytestmark = pytest.mark.gpu
+
+
+def gpu_partitioned(ctx, app: str, files: list[bytes], nreduce: int) -> list[bytes]:
+    """Map each file as its own split (worker.go map task), merge, reduce all partitions."""
+    a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
+    pat = b"" if app == "wc" else app[5:].encode()
+    parts = None
+    for f in files:
+        p = ctx.map(a, f, pattern=pat, nreduce=nreduce)
+        if parts is None:
+            parts = p
+        else:
+            ctx.merge(parts, p)
+            p.free()
+    out = ctx.reduce_all(parts)
+    parts.free()
+    return out
+
+
+def check(ctx, app, files, nreduces=(1, 10, 64)):
+    for R in nreduces:
+        got = gpu_partitioned(ctx, app, files, R)
+        want = O.c_partitioned(app, files, R)
+        assert len(got) == R
+        for r in range(R):
+            if got[r] != want[r]:
+                gl, wl = got[r].split(b"\n"), want[r].split(b"\n")
+                diff = next((i for i in range(min(len(gl), len(wl))) if gl[i] != wl[i]), None)
+                raise AssertionError(f"app={app} R={R} r={r}: {len(got[r])} vs {len(want[r])} bytes; first diff "
+                                     f"line {diff}: got {gl[diff] if diff is not None else None!r} "
+                                     f"want {wl[diff] if diff is not None else None!r}")
+    # mrsequential gate (R = 1) and test-mr.sh's "sort | grep ." equivalence
+    seq = O.c_mrsequential(app, files)
+    allp = gpu_partitioned(ctx, app, files, 10)
+    lines = sorted(l for part in allp for l in part.split(b"\n") if l)
+    assert lines == sorted(l for l in seq.split(b"\n") if l)
+
+
+@pytest.mark.parametrize("name", sorted(cases.edge_cases()))
+def test_wc_edge_cases(ctx, name):
+    check(ctx, "wc", cases.edge_cases()[name])
+
+
+@pytest.mark.parametrize("name", sorted(cases.grep_edge_cases()))
+def test_grep_edge_cases(ctx, name):
+    files, pat = cases.grep_edge_cases()[name]
+    check(ctx, "grep:" + pat.decode(), files, nreduces=(1, 10))
+
+
+@pytest.mark.parametrize("kind,V,seed,inv", [(C.KIND_ASCII, 5000, 1, 0.0), (C.KIND_ASCII, 200000, 2, 0.0),
+                                             (C.KIND_UTF8, 20000, 3, 0.0), (C.KIND_UTF8, 20000, 4, 0.001)])
+def test_wc_synthetic(ctx, kind, V, seed, inv):
+    files = cases.synthetic(kind, V, [1_000_003, 2_500_000, 777_777], seed, inv)
+    check(ctx, "wc", files, nreduces=(1, 10, 64))
+
+
+def test_grep_synthetic(ctx):
+    files = cases.synthetic_grep(50000, [3_000_000, 1_000_001], 5)
+    check(ctx, "grep:distributed", files, nreduces=(1, 10))
+
+
+def test_wc_lds_overflow_and_table_growth(ctx):
+    """Force the HBM paths: tiny HBM table (growth + re-run) and a corpus whose
+    distinct keys overflow every workgroup's LDS table."""
+    files = cases.synthetic(C.KIND_ASCII, 2_000_000, [8_000_000], 9)
+    ctx.set_option("short_table_log2", 10)
+    try:
+        check(ctx, "wc", files, nreduces=(10,))
+        st = ctx.stats()
+        assert st["lds_overflow"] > 0
+    finally:
+        ctx.set_option("short_table_log2", 0)
+
+
+def test_wc_large_vs_oracle(ctx):
+    """64 MB C2-style corpus: full bytes vs the C oracle."""
+    voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
+    files = [bytes(f) for f in voc.fill_files([16_000_000] * 4, [2000 + i for i in range(4)], C.wc_params())]
+    check(ctx, "wc", files, nreduces=(10,))
+
+
+def test_run_job_device_resident(ctx):
+    """mrg_run_job over an HBM-resident buffer == per-file map + merge + reduce."""
+    files = cases.synthetic(C.KIND_ASCII, 100000, [3_000_000, 2_000_000], 12)
+    joined = b"\n".join(files)  # '\n' ends every file's last word/line: identical to per-file splits
+    d = ctx.device_alloc(len(joined))
+    try:
+        ctx.h2d(d, joined)
+        got = ctx.run_job(MRG_APP_WC, device_ptr=d, nbytes=len(joined), nreduce=10)
+    finally:
+        ctx.device_free(d)
+    assert got == O.c_partitioned("wc", files, 10)
+
+
+def test_export_import_reduce_task(ctx):
+    """worker.go flow: map task X -> intermediate mr-X-r (export) -> reduce task r (import, merge, reduce)."""
+    files = cases.synthetic(C.KIND_UTF8, 30000, [700_000, 900_000, 500_000], 13)
+    R = 5
+    inter = {}
+    for x, f in enumerate(files):
+        p = ctx.map(MRG_APP_WC, f, nreduce=R)
+        for r in range(R):
+            inter[(x, r)] = ctx.export(p, r)
+        p.free()
+    want = O.c_partitioned("wc", files, R)
+    for r in range(R):
+        acc = None
+        for x in range(len(files)):
+            q = ctx.import_(inter[(x, r)])
+            if acc is None:
+                acc = q
+            else:
+                ctx.merge(acc, q)
+                q.free()
+        assert ctx.reduce(acc, r) == want[r]
+        acc.free()
+
+
+def test_exchange_single_rank(ctx):
+    """mrg_exchange with one rank (no communicator) keeps every key."""
+    files = cases.synthetic(C.KIND_ASCII, 5000, [400_000], 14)
+    p = ctx.map(MRG_APP_WC, files[0], nreduce=4)
+    q = ctx.exchange(p)
+    assert ctx.reduce_all(q) == O.c_partitioned("wc", files, 4)

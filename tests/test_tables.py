@@ -1,0 +1,54 @@
+"""CPU tests: unicode.IsLetter tables (wc.go:23) against the Unicode 13.0.0 UCD.
+
+The product's two-level bitmap (csrc/letter_table.inc) and the oracle's range
+list (oracle/letter_ranges.h) are generated independently from unicodedata; both
+must equal category L* on every code point, and Latin-1 must equal the explicit
+list of SURVEY.md Appendix A.2 (Go's properties table).
+"""
+from __future__ import annotations
+
+import os
+import re
+import unicodedata
+
+import _oracle as O
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _parse_inc():
+    txt = open(os.path.join(ROOT, "distributed-systems-implemented_amd", "csrc", "letter_table.inc")).read()
+    l1 = [int(x) for x in re.search(r"mrg_letter_l1_init\[\d+\] = \{(.*?)\};", txt, re.S).group(1).split(",") if x.strip()]
+    l2 = [int(x.strip().rstrip("u"), 16) for x in
+          re.search(r"mrg_letter_l2_init\[\d+\] = \{(.*?)\};", txt, re.S).group(1).split(",") if x.strip()]
+    return l1, l2
+
+
+def _is_l(cp):
+    return not (0xD800 <= cp <= 0xDFFF) and unicodedata.category(chr(cp)).startswith("L")
+
+
+def test_ucd_version():
+    assert unicodedata.unidata_version == "13.0.0"
+
+
+def test_product_bitmap_equals_ucd():
+    l1, l2 = _parse_inc()
+    assert len(l1) == 0x1100
+    for cp in range(0x110000):
+        bit = (l2[l1[cp >> 8] * 8 + ((cp >> 5) & 7)] >> (cp & 31)) & 1
+        assert bool(bit) == _is_l(cp), hex(cp)
+
+
+def test_oracle_ranges_equal_ucd():
+    L = O.lib()
+    for cp in list(range(0, 0x3400)) + list(range(0x3400, 0x110000, 7)):
+        assert bool(L.oracle_is_letter(cp)) == _is_l(cp), hex(cp)
+
+
+def test_latin1_letters_match_go_properties():
+    want = set(range(0x41, 0x5B)) | set(range(0x61, 0x7B)) | {0xAA, 0xB5, 0xBA} | set(range(0xC0, 0xD7)) \
+        | set(range(0xD8, 0xF7)) | set(range(0xF8, 0x100))
+    assert {cp for cp in range(256) if _is_l(cp)} == want
+    assert len(want) == 117
+    assert not _is_l(0xFFFD)
