@@ -1,0 +1,263 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json's metric on its configs[1] workload.
+
+metric : word-count input GB/s (map+shuffle+reduce) at 1/2/4/8 MI355X; % HBM roofline
+step   : one whole wc job over one GPU's input split, device-resident in HBM:
+         map (tokenize + LDS combine + HBM hash aggregation) -> [RCCL all-to-all
+         shuffle keyed by ihash % nReduce when N > 1] -> reduce (sort, format
+         every mr-out-r) -> output bytes copied to host.
+workload (configs[1] = SURVEY.md §8d C2): 10 GB synthetic Zipf(s=1.07, V=1e6)
+         ASCII corpus (40 files x 250 MB) per GPU, nReduce = 10.  Weak scaling:
+         every rank maps its own 10 GB (seed per rank); value = all ranks' input
+         bytes x steps / max-over-ranks time.
+
+Run:  python bench.py [--gpus N --steps K --warmup W]
+      N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+             --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "distributed-systems-implemented_amd"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402  (import before mrgpu: one shared HIP runtime)
+import torch.distributed as dist  # noqa: E402
+
+from mrgpu import MRG_APP_WC, Context, ihash  # noqa: E402
+from mrgpu import corpus as C  # noqa: E402
+
+METRIC = "word-count input GB/s (map+shuffle+reduce) at 1/2/4/8 MI355X; % HBM roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def log(msg):
+    print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
+
+
+def gen_corpus(rank: int, file_mb: int, nfiles: int, seed_base: int):
+    """nfiles generated files back to back in one buffer.  Every file ends with '\n',
+    so the concatenation is word-for-word the same input as separate wc splits."""
+    voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
+    sizes = [file_mb * 1_000_000] * nfiles
+    seeds = [seed_base + 1000 * rank + i for i in range(nfiles)]
+    buf = np.empty(sum(sizes), dtype=np.uint8)
+    voc.fill_files(sizes, seeds, C.wc_params(), threads=min(16, os.cpu_count() or 1), out=buf)
+    return buf
+
+
+def check_output(parts: list[bytes], nreduce: int, sample: int = 20000) -> dict:
+    """Size-independent properties of the full-size output: every partition sorted
+    bytewise with unique keys, every sampled key in the right partition, counts > 0."""
+    ok_sorted = ok_part = True
+    total = 0
+    rng = np.random.default_rng(0)
+    for r, p in enumerate(parts):
+        lines = p.split(b"\n")[:-1] if p else []
+        keys = [l.rsplit(b" ", 1)[0] for l in lines]
+        total += sum(int(l.rsplit(b" ", 1)[1]) for l in lines)
+        if any(keys[i] >= keys[i + 1] for i in range(len(keys) - 1)):
+            ok_sorted = False
+        if keys:
+            for i in rng.integers(0, len(keys), size=min(sample // nreduce, len(keys))):
+                if ihash(keys[i]) % nreduce != r:
+                    ok_part = False
+    return {"sorted_unique": ok_sorted, "partition_ok": ok_part, "total_words": total}
+
+
+def cpu_baseline(sample_files: int, sample_mb: int, nreduce: int, ctx: Context) -> dict | None:
+    """The oracle's distributed restatement (oracle/_build/mrcpu: coordinator + N worker
+    processes, JSON-lines intermediates — mr/coordinator.go + mr/worker.go) on a bounded
+    sample of the same workload; its outputs are also compared with the GPU's."""
+    exe = os.path.join(ROOT, "oracle", "_build", "mrcpu")
+    if not os.path.exists(exe):
+        log("cpu_baseline skipped: oracle/_build/mrcpu not built")
+        return None
+    workers = min(16, os.cpu_count() or 1)
+    base = "/dev/shm" if os.path.isdir("/dev/shm") else None
+    tmp = tempfile.mkdtemp(prefix="mrcpu-", dir=base)
+    try:
+        voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
+        sizes = [sample_mb * 1_000_000] * sample_files
+        files = voc.fill_files(sizes, [2 + i for i in range(sample_files)], C.wc_params())
+        paths = []
+        for i, f in enumerate(files):
+            p = os.path.join(tmp, f"pg-{i}.txt")
+            f.tofile(p)
+            paths.append(p)
+        wdir = os.path.join(tmp, "work")
+        os.makedirs(wdir)
+        res = subprocess.run([exe, "--app", "wc", "--nreduce", str(nreduce), "--workers", str(workers), "--dir", wdir]
+                             + paths, capture_output=True, text=True, timeout=600)
+        if res.returncode != 0:
+            log(f"mrcpu failed: {res.stderr[-500:]}")
+            return None
+        info = json.loads(res.stdout.strip().splitlines()[-1])
+        cpu_out = [open(os.path.join(wdir, f"mr-out-{r}"), "rb").read() for r in range(nreduce)]
+        joined = b"\n".join(bytes(f) for f in files)
+        gpu_out = ctx.run_job(MRG_APP_WC, joined, nreduce=nreduce)
+        return {"value": round(info["bytes"] / info["seconds"] / 1e9, 4), "unit": "GB/s", "cores": workers,
+                "kind": "port",
+                "sample": f"{sample_files} files x {sample_mb} MB of the same Zipf corpus "
+                          f"({info['bytes'] / 1e9:.2f} GB), mrcpu = restated mrcoordinator + {workers} mrworker "
+                          f"processes with JSON-lines mr-X-Y shuffle, nReduce={nreduce}; "
+                          f"{info['seconds']:.1f} s",
+                "gpu_output_identical": gpu_out == cpu_out}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--file-mb", type=int, default=250)
+    ap.add_argument("--files", type=int, default=40)
+    ap.add_argument("--nreduce", type=int, default=10)
+    ap.add_argument("--cpu-sample-files", type=int, default=16)
+    ap.add_argument("--cpu-sample-mb", type=int, default=64)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"--gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    if world > 1:
+        dist.init_process_group("gloo")  # control plane only; the shuffle is RCCL inside libmrgpu
+    torch.cuda.set_device(local)
+
+    t0 = time.time()
+    host = gen_corpus(rank, args.file_mb, args.files, seed_base=2)
+    nbytes = int(host.size)
+    log(f"generated {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
+
+    ctx = Context(local)
+    if world > 1:
+        obj = [Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.comm_init(obj[0], world, rank)
+    dptr = ctx.device_alloc(nbytes)
+    step = 1 << 30
+    for off in range(0, nbytes, step):
+        n = min(step, nbytes - off)
+        ctx.h2d(dptr + off, host[off:off + n], n)
+    ctx.sync()
+
+    def run_step():
+        return ctx.run_job(MRG_APP_WC, device_ptr=dptr, nbytes=nbytes, nreduce=args.nreduce, copy_out=False)
+
+    for _ in range(args.warmup):
+        run_step()
+
+    digests, kern_ms, stats = [], [], []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.sync()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        p, n, offs = run_step()
+        st = ctx.stats()
+        kern_ms.append(st["map_kernel_ms"])
+        stats.append(st)
+        digests.append((p, n))
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+
+    t_max = elapsed
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+
+    # output of the last step (context-owned buffer) -> properties at full size
+    import ctypes
+    p, n, offs = run_step()
+    out = ctypes.string_at(p, n) if n else b""
+    parts = [out[offs[i]:offs[i + 1]] for i in range(args.nreduce)]
+    checks = check_output(parts, args.nreduce)
+    checks["deterministic"] = hashlib.sha256(out).hexdigest() == hashlib.sha256(
+        ctypes.string_at(*run_step()[:2])).hexdigest()
+    if world > 1:
+        tw = torch.tensor([checks["total_words"]], dtype=torch.int64)
+        dist.all_reduce(tw)
+        checks["total_words"] = int(tw.item())
+
+    total_bytes = nbytes * world * args.steps
+    value = total_bytes / t_max / 1e9
+    avg_kern = sum(kern_ms) / len(kern_ms)
+    achieved = nbytes / (avg_kern / 1e3) / 1e9
+    last = stats[-1]
+
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "traffic_r01.json")
+    if os.path.exists(tpath):
+        try:
+            tj = json.load(open(tpath))
+            if tj.get("input_bytes") == nbytes:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_sample_files, args.cpu_sample_mb, args.nreduce, ctx)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_max / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (deterministic Zipf corpus from csrc/corpus.c; reference pg-*.txt not bundled)",
+            "config": {"workload": f"C2: wc over {nbytes / 1e9:.2f} GB per GPU ({args.files} files x {args.file_mb} MB, "
+                                   "Zipf s=1.07 over 1e6 ASCII words), device-resident input",
+                       "nreduce": args.nreduce, "input_bytes_per_gpu": nbytes, "parallelism": f"dp{world}",
+                       "shuffle": "RCCL all-to-all" if world > 1 else "none (single GPU)"},
+            "roofline": {"bound": "hbm", "kernel": "wc_map_kernel", "achieved": round(achieved, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": traffic,
+                         "note": "achieved = input bytes per launch / mean HIP-event duration of wc_map_kernel on "
+                                 "the library stream over the timed steps"},
+            "phases_ms": {"map_kernel": round(avg_kern, 3), "map_total": round(last["map_total_ms"], 3),
+                          "exchange": round(last["exchange_ms"], 3), "reduce": round(last["reduce_ms"], 3),
+                          "d2h": round(last["d2h_ms"], 3)},
+            "distinct_keys": int(last["distinct_keys"]),
+            "lds_overflow_words": int(last["lds_overflow"]),
+            "output_bytes": int(last["output_bytes"]),
+            "checks": checks,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    ctx.device_free(dptr)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -6,11 +6,11 @@
 // is the bytewise key order and the "%v %v\n" formatting.
 //
 // Order: Go string '<' is unsigned bytewise with a shorter prefix first.  Keys
-// are sorted by (partition, first 16 bytes big-endian, length) with stable LSD
-// radix passes; zero padding makes that order exact for keys <= 16 bytes and
-// for any two keys whose 16-byte prefixes differ.  Remaining ties (keys > 16
-// bytes sharing a 16-byte prefix and a length) are resolved by a full bytewise
-// comparison inside each tied run.
+// are sorted by (partition, first 16 bytes zero-padded, big-endian) with
+// stable LSD radix passes; a strictly smaller padded prefix implies a smaller
+// key, so that order is exact whenever prefixes differ.  Runs of equal
+// prefixes (keys > 16 bytes, or grep lines containing NUL bytes) are then
+// ordered by a full bytewise comparison inside each run.
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
@@ -110,16 +110,18 @@ __device__ int rec_cmp(const Recs& r, uint32_t a, uint32_t b) {
     return (la > lb) - (la < lb);
 }
 
-__device__ __forceinline__ bool same_sort_key(const Recs& r, uint32_t a, uint32_t b) {
-    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && r.k1[a] == r.k1[b] && r.len[a] == r.len[b];
+__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b) {
+    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && r.k1[a] == r.k1[b];
 }
 
-// tie[i] = 1 when sorted position i has the same (part, prefix, len) as i-1
+// tie[i] = 1 when sorted position i has the same (part, 16-byte prefix) as i-1:
+// distinct keys with equal zero-padded prefixes (a key > 16 bytes, or a grep
+// line with NUL bytes) are only ordered by a full bytewise comparison.
 __global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8_t* tie, unsigned long long* flags) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint8_t t = 0;
-        if (i > 0 && r.len[perm[i]] > 16 && same_sort_key(r, perm[i - 1], perm[i])) t = 1;
+        if (i > 0 && same_prefix(r, perm[i - 1], perm[i])) t = 1;
         tie[i] = t;
         if (t) atomicOr(&flags[2], 1ull);
     }
@@ -290,7 +292,6 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         return e;
     };
     int e;
-    if (has_long && (e = pass32(0, 32))) return e;
     if (has_k1 && (e = pass64(1))) return e;
     if ((e = pass64(2))) return e;
     if (all && nreduce > 1) {
@@ -298,7 +299,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         while ((1ull << bits) < nreduce) bits++;
         if ((e = pass32(3, bits))) return e;
     }
-    if (has_long) {
+    if (has_long || app != 1) {
         uint8_t* tie = ws->key_a.as<uint8_t>();
         mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags);
         fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie);
