@@ -247,7 +247,9 @@ def main():
                           "exchange": round(last["exchange_ms"], 3), "reduce": round(last["reduce_ms"], 3),
                           "d2h": round(last["d2h_ms"], 3)},
             "distinct_keys": int(last["distinct_keys"]),
-            "lds_overflow_words": int(last["lds_overflow"]),
+            "spilled_words": int(last["lds_overflow"]),
+            "spill_region_full_words": int(last["spill_ovf"]),
+            "aggregator_miss_words": int(last["agg_miss"]),
             "output_bytes": int(last["output_bytes"]),
             "checks": checks,
             "cpu_baseline": cpu,

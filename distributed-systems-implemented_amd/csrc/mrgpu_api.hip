@@ -61,7 +61,9 @@ struct mrg_ctx {
     std::string err;
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
-    DevBuf sh, lo, list, ctr, staging, pat;
+    DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
+    uint64_t spill_region_keys = 0;
+    int64_t spill_force_blocks = 0;
     int sh_log2 = 22, lo_log2 = 14;
     uint64_t list_cap = 1u << 20;
     int grid = 256;
@@ -121,7 +123,33 @@ static Tables make_tables(mrg_ctx* c) {
     t.list = (uint64_t*)c->list.p;
     t.list_cap = c->list_cap;
     t.ctr = (Counters*)c->ctr.p;
+    t.sp.pool = (uint4*)c->spool.p;
+    t.sp.region_keys = c->spill_region_keys;
+    t.sp.region_blocks = c->spill_region_keys / kSpillBlock;
+    t.sp.bcur = (unsigned long long*)c->spmeta.p;
+    t.sp.fills = c->spmeta.p ? (uint32_t*)((char*)c->spmeta.p + kSpillBuckets * sizeof(unsigned long long)) : nullptr;
     return t;
+}
+
+// Spill pool for LDS-combiner misses: ~1.5 bytes of pool per input byte (C2
+// spills ~1 byte per input byte); a bucket that fills its region degrades to
+// HBM-table inserts, so the size only affects speed, never results.
+static int ensure_spill(mrg_ctx* c, uint64_t n) {
+    uint64_t keys = (n + n / 2) / 16 / kSpillBuckets;
+    keys = ((keys + kSpillBlock - 1) / kSpillBlock + 2) * kSpillBlock;
+    if (c->spill_force_blocks > 0) {  // test knob: tiny regions exercise the region-full path
+        c->spill_region_keys = (uint64_t)c->spill_force_blocks * kSpillBlock;
+        keys = std::max<uint64_t>(keys, c->spill_region_keys);
+        HCHK(c, c->spool.ensure(keys * kSpillBuckets * sizeof(uint4)));
+        HCHK(c, c->spmeta.ensure(kSpillBuckets * sizeof(unsigned long long) + kSpillBuckets * (keys / kSpillBlock) * 4));
+        return MRG_OK;
+    }
+    if (keys > c->spill_region_keys || !c->spool.p) {
+        c->spill_region_keys = keys;
+        HCHK(c, c->spool.ensure(keys * kSpillBuckets * sizeof(uint4)));
+        HCHK(c, c->spmeta.ensure(kSpillBuckets * sizeof(unsigned long long) + kSpillBuckets * (keys / kSpillBlock) * 4));
+    }
+    return MRG_OK;
 }
 
 static int ensure_tables(mrg_ctx* c) {
@@ -249,7 +277,7 @@ void mrg_close(mrg_ctx* c) {
     hipSetDevice(c->device);
     if (c->s) hipStreamSynchronize(c->s);
     if (c->comm) ncclCommDestroy(c->comm);
-    DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat};
+    DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spmeta};
     for (DevBuf* b : bs) b->release();
     if (c->d_l1) hipFree(c->d_l1);
     if (c->d_l2) hipFree(c->d_l2);
@@ -270,6 +298,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "long_table_log2")) c->lo_log2 = v > 0 ? (int)v : 14;
     else if (!strcmp(name, "list_cap")) c->list_cap = v > 0 ? (uint64_t)v : (1u << 20);
     else if (!strcmp(name, "map_grid")) c->grid = v > 0 ? (int)v : map_grid_size(c->device);
+    else if (!strcmp(name, "spill_region_blocks")) { c->spill_force_blocks = v > 0 ? v : 0; if (!v) c->spill_region_keys = 0; }
     else return fail(c, MRG_EINVAL, "unknown option %s", name);
     return MRG_OK;
 }
@@ -360,6 +389,7 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         grep_nl = plen && memchr(pat, '\n', plen) != nullptr;  // no line can contain '\n'
     }
     LetterTables lt{c->d_l1, c->d_l2};
+    if (app == MRG_APP_WC && (rc = ensure_spill(c, len))) return rc;
     for (int attempt = 0; attempt < 8; attempt++) {
         if ((rc = ensure_tables(c))) return rc;
         Tables t = make_tables(c);
@@ -367,12 +397,14 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         HCHK(c, hipEventRecord(c->ev[0], c->s));
         if (app == MRG_APP_WC) {
             launch_wc_map(in, len, t, lt, c->grid, 0, c->s);
+            HCHK(c, hipEventRecord(c->ev[1], c->s));
+            launch_wc_agg(t, c->s);
         } else if (!grep_nl) {
             if (plen) launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);
             else launch_grep_all_lines(in, len, t, c->grid, c->s);
         }
         HCHK(c, hipGetLastError());
-        HCHK(c, hipEventRecord(c->ev[1], c->s));
+        if (app != MRG_APP_WC) HCHK(c, hipEventRecord(c->ev[1], c->s));
         if ((rc = read_counters(c))) return rc;
         if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
         uint64_t nlist = c->h_ctr->nlist;
@@ -385,7 +417,9 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         if (st & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", st);
         if (grow_on_overflow(c, st)) continue;
         c->stats.map_kernel_ms = ev_ms(c->ev[0], c->ev[1]);
-        c->stats.lds_overflow = c->h_ctr->lds_miss;
+        c->stats.lds_overflow = c->h_ctr->spilled + c->h_ctr->spill_ovf;
+        c->stats.spill_ovf = c->h_ctr->spill_ovf;
+        c->stats.agg_miss = c->h_ctr->agg_miss;
         mrg_parts* p = nullptr;
         if ((rc = collect_parts(c, app, nreduce, &p))) return rc;
         HCHK(c, hipEventRecord(c->ev[3], c->s));

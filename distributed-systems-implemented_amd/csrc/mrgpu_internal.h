@@ -50,7 +50,24 @@ struct Counters {
     unsigned long long nlong_rec;  // collect: long records
     unsigned long long chunks_utf8;// chunks that took the UTF-8 decode path
     unsigned long long long_bytes; // total bytes of distinct long keys (arena size)
-    unsigned long long pad[6];
+    unsigned long long spilled;    // keys written to the spill pool
+    unsigned long long spill_ovf;  // keys that found their bucket region full (went to the HBM table)
+    unsigned long long agg_miss;   // spill keys that missed the bucket aggregator's LDS table
+    unsigned long long pad[3];
+};
+
+// Spill of LDS-combiner misses, hash-partitioned into kSpillBuckets buckets.
+// Bucket b owns keys [b*region_keys, (b+1)*region_keys) of `pool` (16-B keys
+// {k0,k1}); it is filled in blocks of kSpillBlock keys, each block written by
+// one workgroup; fills[b*region_blocks + j] = valid keys in block j.
+constexpr int kSpillBuckets = 256;
+constexpr int kSpillBlock = 2048;
+struct Spill {
+    uint4* pool;
+    uint64_t region_keys;            // multiple of kSpillBlock
+    unsigned long long* bcur;        // [kSpillBuckets] keys reserved per bucket
+    uint32_t* fills;                 // [kSpillBuckets * region_blocks]
+    uint64_t region_blocks;
 };
 
 struct Tables {
@@ -61,6 +78,7 @@ struct Tables {
     uint64_t* list;      // u64 offsets (long-word starts / grep match positions)
     uint64_t list_cap;
     Counters* ctr;
+    Spill sp;
 };
 
 struct Recs {
@@ -84,6 +102,7 @@ struct LetterTables {
 void clear_tables(const Tables& t, hipStream_t s);
 void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int lds_slots,
                    hipStream_t s);
+void launch_wc_agg(const Tables& t, hipStream_t s);
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
                      hipStream_t s);

@@ -34,11 +34,16 @@ constexpr int kWavesPerWG = 8;
 constexpr int kThreads = kWavesPerWG * kWave;
 constexpr int kListCap = kChunk / 2;              // max word starts in a chunk
 constexpr int kNMask = 136;                       // [0]=look-back piece, [1..128]=chunk, [129..131]=look-ahead
-constexpr int kLdsSlots = 4096;
+constexpr int kLdsSlots = 4096;                   // map-side combiner (per workgroup)
 constexpr int kLdsLimit = kLdsSlots * 7 / 8;
 constexpr int kLdsProbes = 24;
+constexpr int kAggSlots = 6144;                   // bucket aggregator (whole LDS)
+constexpr int kAggLimit = kAggSlots * 15 / 16;
 constexpr int kGlobalProbes = 4096;
 constexpr uint32_t kSpinLimit = 1u << 22;
+constexpr int kSpillCap = kSpillBlock;            // misses staged per workgroup round (<= one block)
+constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
+constexpr uint32_t kOvfBlock = 0xFFFFFFFEu;
 
 struct alignas(16) WaveLds {
     uint8_t buf[kBuf];
@@ -51,6 +56,20 @@ struct alignas(16) MapLds {
     unsigned long long k0[kLdsSlots];
     unsigned long long k1[kLdsSlots];
     uint32_t cnt[kLdsSlots];
+    uint4 spill[kSpillCap];          // this round's combiner misses
+    uint16_t rank[kSpillCap];        // rank of each miss within its bucket this round
+    uint32_t hist[kSpillBuckets];    // misses per bucket this round
+    uint32_t fill[kSpillBuckets];    // keys already in the current block of each bucket stream
+    uint32_t blkA[kSpillBuckets];    // current block of each bucket stream
+    uint32_t blkB[kSpillBuckets];    // next block (when this round's run overflows blkA)
+    uint32_t nspill;
+    uint32_t occ;
+};
+
+struct alignas(16) AggLds {
+    unsigned long long k0[kAggSlots];
+    unsigned long long k1[kAggSlots];
+    uint32_t cnt[kAggSlots];
     uint32_t occ;
 };
 
@@ -263,38 +282,44 @@ __device__ __forceinline__ void list_append(const Tables& t, uint64_t v) {
 }
 
 // ------------------------------------------------------------ LDS table
-// Same claim/publish protocol inside the workgroup's LDS (the combiner).
-__device__ __forceinline__ bool lds_insert(MapLds& L, uint64_t k0, uint64_t k1, uint32_t h) {
-    uint32_t i = h >> (32 - 12);
+// Same claim/publish protocol inside a workgroup's LDS (the combiner).
+// index = umulhi(h, nslots) so nslots need not be a power of two.
+__device__ __forceinline__ bool lds_insert(unsigned long long* K0, unsigned long long* K1, uint32_t* CNT, uint32_t* occ,
+                                           uint32_t nslots, uint32_t limit, uint32_t probes_max, uint64_t k0,
+                                           uint64_t k1, uint32_t h, uint32_t add) {
+    uint32_t i = __umulhi(h, nslots);
     uint32_t probes = 0, spins = 0;
     while (true) {
-        uint64_t cur = __hip_atomic_load(&L.k0[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint64_t cur = __hip_atomic_load(&K0[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         if (cur == 0) {
-            if (__hip_atomic_load(&L.occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= (uint32_t)kLdsLimit)
-                return false;
-            uint64_t prev = atomicCAS(&L.k0[i], 0ull, (unsigned long long)k0);
+            if (__hip_atomic_load(occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= limit) return false;
+            uint64_t prev = atomicCAS(&K0[i], 0ull, (unsigned long long)k0);
             if (prev == 0) {
-                __hip_atomic_store(&L.k1[i], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                atomicAdd(&L.cnt[i], 1u);
-                atomicAdd(&L.occ, 1u);
+                __hip_atomic_store(&K1[i], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                atomicAdd(&CNT[i], add);
+                atomicAdd(occ, 1u);
                 return true;
             }
             cur = prev;
         }
         if (cur == k0) {
-            uint64_t v = __hip_atomic_load(&L.k1[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            uint64_t v = __hip_atomic_load(&K1[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             if (v == kUnwritten) {
                 if (++spins > kSpinLimit) return false;
                 continue;
             }
             if (v == k1) {
-                atomicAdd(&L.cnt[i], 1u);
+                atomicAdd(&CNT[i], add);
                 return true;
             }
         }
-        if (++probes >= (uint32_t)kLdsProbes) return false;
-        i = (i + 1) & (kLdsSlots - 1);
+        if (++probes >= probes_max) return false;
+        i = (i + 1 == nslots) ? 0 : i + 1;
     }
+}
+
+__device__ __forceinline__ uint32_t spill_bucket(uint64_t k0, uint64_t k1) {
+    return (uint32_t)(short_hash64(k0, k1) >> 56);  // top 8 bits; the HBM table indexes by low bits
 }
 
 // ------------------------------------------------------------ chunk loading
@@ -338,6 +363,69 @@ __device__ __forceinline__ void stage_chunk(WaveLds& W, const ChunkRegs& r, uint
 }
 
 // ------------------------------------------------------------ wc map kernel
+__device__ __forceinline__ uint32_t spill_grab(const Tables& t, uint32_t b) {
+    const unsigned long long k = atomicAdd(&t.sp.bcur[b], (unsigned long long)kSpillBlock);
+    return (k + kSpillBlock <= t.sp.region_keys) ? (uint32_t)(k / kSpillBlock) : kOvfBlock;
+}
+
+// End of a round: write the round's combiner misses into their bucket streams.
+// Every thread of the workgroup calls this (contains __syncthreads).
+__device__ void flush_spill(MapLds& L, const Tables& t, uint32_t tid, uint64_t& ovf) {
+    const uint32_t ns = min(L.nspill, (uint32_t)kSpillCap);
+    for (uint32_t i = tid; i < ns; i += kThreads) {
+        const uint4 k = L.spill[i];
+        const uint32_t b = spill_bucket(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z);
+        L.rank[i] = (uint16_t)atomicAdd(&L.hist[b], 1u);
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
+        const uint32_t h = L.hist[b];
+        if (!h) continue;
+        if (L.blkA[b] == kNoBlock) L.blkA[b] = spill_grab(t, b);
+        if (L.fill[b] + h > (uint32_t)kSpillBlock && L.blkA[b] != kOvfBlock) L.blkB[b] = spill_grab(t, b);
+    }
+    __syncthreads();
+    for (uint32_t i = tid; i < ns; i += kThreads) {
+        const uint4 k = L.spill[i];
+        const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
+        const uint32_t b = spill_bucket(k0, k1);
+        const uint32_t pos = L.fill[b] + L.rank[i];
+        const bool first = pos < (uint32_t)kSpillBlock;
+        const uint32_t blk = first ? L.blkA[b] : L.blkB[b];
+        if (blk >= kOvfBlock) {  // bucket region exhausted: count in the HBM table instead
+            short_insert(t, k0, k1, 1);
+            ovf++;
+        } else {
+            t.sp.pool[(uint64_t)b * t.sp.region_keys + (uint64_t)blk * kSpillBlock + (first ? pos : pos - kSpillBlock)] = k;
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
+        const uint32_t h = L.hist[b];
+        if (!h) continue;
+        const uint32_t f = L.fill[b] + h;
+        if (L.blkA[b] == kOvfBlock) {
+            L.fill[b] = 0;
+        } else if (f >= (uint32_t)kSpillBlock) {
+            t.sp.fills[(uint64_t)b * t.sp.region_blocks + L.blkA[b]] = kSpillBlock;
+            if (f > (uint32_t)kSpillBlock) { L.blkA[b] = L.blkB[b]; L.fill[b] = f - kSpillBlock; }
+            else { L.blkA[b] = kNoBlock; L.fill[b] = 0; }
+        } else {
+            L.fill[b] = f;
+        }
+        L.hist[b] = 0;
+        L.blkB[b] = kNoBlock;
+    }
+    if (tid == 0) {
+        if (ns) atomicAdd(&t.ctr->spilled, (unsigned long long)ns);
+        L.nspill = 0;
+    }
+    __syncthreads();
+}
+
+// Rounds: in round r workgroup g's 8 waves take chunks (r*G + g)*8 + wave, so
+// every thread runs the same number of rounds and the per-round spill flush
+// can use workgroup barriers.
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
                                                           Tables t, LetterTables lt) {
     __shared__ MapLds L;
@@ -351,101 +439,168 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         L.k1[i] = kUnwritten;
         L.cnt[i] = 0;
     }
-    if (tid == 0) L.occ = 0;
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
+        L.hist[b] = 0;
+        L.fill[b] = 0;
+        L.blkA[b] = kNoBlock;
+        L.blkB[b] = kNoBlock;
+    }
+    if (tid == 0) { L.occ = 0; L.nspill = 0; }
     __syncthreads();
 
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
-    uint64_t c = (uint64_t)blockIdx.x * kWavesPerWG + wv;
-    uint64_t miss = 0, utf8_chunks = 0;
+    const uint64_t nrounds = (nchunks + stride - 1) / stride;
+    const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
+    uint64_t ovf = 0, utf8_chunks = 0;
     ChunkRegs cur, nxt;
-    if (c < nchunks) load_chunk(in, n, c * kChunk, lane, cur);
+    if (c0 < nchunks) load_chunk(in, n, c0 * kChunk, lane, cur);
 
-    for (; c < nchunks; c += stride) {
-        const uint64_t cs = c * kChunk;
-        if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);  // prefetch
+    for (uint64_t r = 0; r < nrounds; r++) {
+        const uint64_t c = c0 + r * stride;
+        if (c < nchunks) {
+            const uint64_t cs = c * kChunk;
+            if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);  // prefetch next round
 
-        stage_chunk(W, cur, lane);
-        uint32_t hi = (cur.a.x | cur.a.y | cur.a.z | cur.a.w | cur.b.x | cur.b.y | cur.b.z | cur.b.w | cur.h.x |
-                       cur.h.y | cur.h.z | cur.h.w) & 0x80808080u;
-        const bool ascii = __ballot(hi != 0) == 0;
-        uint32_t mA, mB, mH = 0;
-        if (ascii) {
-            mA = ascii_mask16(cur.a);
-            mB = ascii_mask16(cur.b);
-            if (lane < 5) mH = ascii_mask16(cur.h);
-        } else {
-            utf8_chunks++;
-            wave_sync();
-            mA = utf8_letter_mask<16>(W.buf, kBack + 16 * lane, lt);
-            mB = utf8_letter_mask<16>(W.buf, kBack + 1024 + 16 * lane, lt);
-            if (lane < 3) mH = utf8_letter_mask<16>(W.buf, kBack + 2048 + 16 * lane, lt);
-            else if (lane == 4) mH = utf8_letter_mask<8>(W.buf, 8, lt) << 8;  // look-back bits 8..15
-        }
-        W.mask[1 + lane] = (uint16_t)mA;
-        W.mask[65 + lane] = (uint16_t)mB;
-        if (lane < 4) W.mask[129 + lane] = (uint16_t)mH;
-        else if (lane == 4) W.mask[0] = (uint16_t)mH;
-
-        // word starts: letter byte whose predecessor byte is not a letter byte
-        const uint32_t prevA_m = __shfl(mA, (int)((lane + 63) & 63));
-        const uint32_t prevB_m = __shfl(mB, (int)((lane + 63) & 63));
-        const uint32_t lastA = __shfl(mA, 63);
-        const uint32_t back = __shfl(mH, 4);
-        const uint32_t pa = (lane == 0 ? back : prevA_m) >> 15 & 1u;
-        const uint32_t pb = (lane == 0 ? lastA : prevB_m) >> 15 & 1u;
-        uint32_t SA = mA & ~((mA << 1) | pa) & 0xFFFFu;
-        uint32_t SB = mB & ~((mB << 1) | pb) & 0xFFFFu;
-        uint32_t total;
-        uint32_t j = wave_excl_scan5(__popc(SA) + __popc(SB), &total);
-        while (SA) {
-            uint32_t bit = __builtin_ctz(SA);
-            W.list[j++] = (uint16_t)(16 * lane + bit);
-            SA &= SA - 1;
-        }
-        while (SB) {
-            uint32_t bit = __builtin_ctz(SB);
-            W.list[j++] = (uint16_t)(1024 + 16 * lane + bit);
-            SB &= SB - 1;
-        }
-        wave_sync();
-
-        for (uint32_t w = lane; w < total; w += 64) {
-            const uint32_t s = W.list[w];
-            const uint32_t p = s >> 4, bsh = s & 15;
-            const uint64_t win = (uint64_t)W.mask[p + 1] | ((uint64_t)W.mask[p + 2] << 16) | ((uint64_t)W.mask[p + 3] << 32);
-            const uint32_t len = (uint32_t)__builtin_ctzll(~(win >> bsh));
-            if (len > 16) {
-                list_append(t, cs + s);
-                continue;
+            stage_chunk(W, cur, lane);
+            uint32_t hi = (cur.a.x | cur.a.y | cur.a.z | cur.a.w | cur.b.x | cur.b.y | cur.b.z | cur.b.w | cur.h.x |
+                           cur.h.y | cur.h.z | cur.h.w) & 0x80808080u;
+            const bool ascii = __ballot(hi != 0) == 0;
+            uint32_t mA, mB, mH = 0;
+            if (ascii) {
+                mA = ascii_mask16(cur.a);
+                mB = ascii_mask16(cur.b);
+                if (lane < 5) mH = ascii_mask16(cur.h);
+            } else {
+                utf8_chunks++;
+                wave_sync();
+                mA = utf8_letter_mask<16>(W.buf, kBack + 16 * lane, lt);
+                mB = utf8_letter_mask<16>(W.buf, kBack + 1024 + 16 * lane, lt);
+                if (lane < 3) mH = utf8_letter_mask<16>(W.buf, kBack + 2048 + 16 * lane, lt);
+                else if (lane == 4) mH = utf8_letter_mask<8>(W.buf, 8, lt) << 8;  // look-back bits 8..15
             }
-            const uint32_t q = kBack + s;
-            const uint32_t* d = reinterpret_cast<const uint32_t*>(W.buf + (q & ~3u));
-            const uint32_t sh = q & 3u;
-            const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
-            uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-            uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-            uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
-            uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
-            uint64_t k0 = ((uint64_t)w1 << 32) | w0;
-            uint64_t k1 = ((uint64_t)w3 << 32) | w2;
-            k0 &= len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1);
-            k1 &= len >= 16 ? ~0ull : (len <= 8 ? 0ull : ((1ull << (8 * (len - 8))) - 1));
-            const uint32_t h = fold32((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-            if (!lds_insert(L, k0, k1, h)) {
+            W.mask[1 + lane] = (uint16_t)mA;
+            W.mask[65 + lane] = (uint16_t)mB;
+            if (lane < 4) W.mask[129 + lane] = (uint16_t)mH;
+            else if (lane == 4) W.mask[0] = (uint16_t)mH;
+
+            // word starts: letter byte whose predecessor byte is not a letter byte
+            const uint32_t prevA_m = __shfl(mA, (int)((lane + 63) & 63));
+            const uint32_t prevB_m = __shfl(mB, (int)((lane + 63) & 63));
+            const uint32_t lastA = __shfl(mA, 63);
+            const uint32_t back = __shfl(mH, 4);
+            const uint32_t pa = (lane == 0 ? back : prevA_m) >> 15 & 1u;
+            const uint32_t pb = (lane == 0 ? lastA : prevB_m) >> 15 & 1u;
+            uint32_t SA = mA & ~((mA << 1) | pa) & 0xFFFFu;
+            uint32_t SB = mB & ~((mB << 1) | pb) & 0xFFFFu;
+            uint32_t total;
+            uint32_t j = wave_excl_scan5(__popc(SA) + __popc(SB), &total);
+            while (SA) {
+                W.list[j++] = (uint16_t)(16 * lane + __builtin_ctz(SA));
+                SA &= SA - 1;
+            }
+            while (SB) {
+                W.list[j++] = (uint16_t)(1024 + 16 * lane + __builtin_ctz(SB));
+                SB &= SB - 1;
+            }
+            wave_sync();
+
+            for (uint32_t w = lane; w < total; w += 64) {
+                const uint32_t s = W.list[w];
+                const uint32_t p = s >> 4, bsh = s & 15;
+                const uint64_t win =
+                    (uint64_t)W.mask[p + 1] | ((uint64_t)W.mask[p + 2] << 16) | ((uint64_t)W.mask[p + 3] << 32);
+                const uint32_t len = (uint32_t)__builtin_ctzll(~(win >> bsh));
+                if (len > 16) {
+                    list_append(t, cs + s);
+                    continue;
+                }
+                const uint32_t q = kBack + s;
+                const uint32_t* d = reinterpret_cast<const uint32_t*>(W.buf + (q & ~3u));
+                const uint32_t sh = q & 3u;
+                const uint32_t d0 = d[0], d1 = d[1], d2 = d[2], d3 = d[3], d4 = d[4];
+                const uint32_t w0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+                const uint32_t w1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+                const uint32_t w2 = __builtin_amdgcn_alignbyte(d3, d2, sh);
+                const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
+                uint64_t k0 = ((uint64_t)w1 << 32) | w0;
+                uint64_t k1 = ((uint64_t)w3 << 32) | w2;
+                k0 &= len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1);
+                k1 &= len >= 16 ? ~0ull : (len <= 8 ? 0ull : ((1ull << (8 * (len - 8))) - 1));
+                const uint32_t h = fold32((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                const bool hit = lds_insert(L.k0, L.k1, L.cnt, &L.occ, kLdsSlots, kLdsLimit, kLdsProbes, k0, k1, h, 1);
+                const uint64_t mm = __ballot(!hit);
+                if (mm) {  // wave-aggregated append of the misses to this round's spill list
+                    const uint32_t leader = (uint32_t)__builtin_ctzll(mm);
+                    uint32_t base = 0;
+                    if (lane == leader) base = atomicAdd(&L.nspill, (uint32_t)__popcll(mm));
+                    base = __shfl(base, (int)leader);
+                    if (!hit) {
+                        const uint32_t slot = base + mbcnt64(mm);
+                        if (slot < (uint32_t)kSpillCap) {
+                            L.spill[slot] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                        } else {
+                            short_insert(t, k0, k1, 1);
+                            ovf++;
+                        }
+                    }
+                }
+            }
+            wave_sync();
+            cur = nxt;
+        }
+        __syncthreads();
+        flush_spill(L, t, tid, ovf);
+    }
+
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads)
+        if (L.blkA[b] < kOvfBlock && L.fill[b] > 0) t.sp.fills[(uint64_t)b * t.sp.region_blocks + L.blkA[b]] = L.fill[b];
+    for (uint32_t i = tid; i < kLdsSlots; i += kThreads) {
+        const uint64_t k0 = L.k0[i];
+        if (k0 != 0) short_insert(t, k0, L.k1[i], L.cnt[i]);
+    }
+    if (ovf) atomicAdd(&t.ctr->spill_ovf, (unsigned long long)ovf);
+    if (utf8_chunks && lane == 0) atomicAdd(&t.ctr->chunks_utf8, (unsigned long long)utf8_chunks);
+}
+
+// Bucket aggregation: one workgroup per spill bucket counts its keys in an LDS
+// table (a bucket holds ~1/256 of the distinct spilled keys), then adds the
+// per-key totals to the HBM ShortTable — one HBM atomic per distinct key per
+// bucket instead of one per occurrence.
+__global__ void __launch_bounds__(kThreads) wc_agg_kernel(Tables t) {
+    __shared__ AggLds A;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < kAggSlots; i += kThreads) {
+        A.k0[i] = 0;
+        A.k1[i] = kUnwritten;
+        A.cnt[i] = 0;
+    }
+    if (tid == 0) A.occ = 0;
+    __syncthreads();
+    const uint32_t b = blockIdx.x;
+    uint64_t reserved = t.sp.bcur[b];
+    if (reserved > t.sp.region_keys) reserved = t.sp.region_keys;
+    const uint64_t nblk = reserved / kSpillBlock;
+    const uint4* base = t.sp.pool + (uint64_t)b * t.sp.region_keys;
+    uint64_t miss = 0;
+    for (uint64_t j = 0; j < nblk; j++) {
+        const uint32_t f = t.sp.fills[(uint64_t)b * t.sp.region_blocks + j];
+        const uint4* blk = base + j * kSpillBlock;
+        for (uint32_t i = tid; i < f; i += kThreads) {
+            const uint4 k = blk[i];
+            const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
+            const uint32_t h = fold32(k.x, k.y, k.z, k.w);
+            if (!lds_insert(A.k0, A.k1, A.cnt, &A.occ, kAggSlots, kAggLimit, 32, k0, k1, h, 1)) {
                 short_insert(t, k0, k1, 1);
                 miss++;
             }
         }
-        cur = nxt;
     }
-
     __syncthreads();
-    for (uint32_t i = tid; i < kLdsSlots; i += kThreads) {
-        uint64_t k0 = L.k0[i];
-        if (k0 != 0) short_insert(t, k0, L.k1[i], L.cnt[i]);
+    for (uint32_t i = tid; i < kAggSlots; i += kThreads) {
+        const uint64_t k0 = A.k0[i];
+        if (k0 != 0) short_insert(t, k0, A.k1[i], A.cnt[i]);
     }
-    if (miss) atomicAdd(&t.ctr->lds_miss, (unsigned long long)miss);
-    if (utf8_chunks && lane == 0) atomicAdd(&t.ctr->chunks_utf8, (unsigned long long)utf8_chunks);
+    if (miss) atomicAdd(&t.ctr->agg_miss, (unsigned long long)miss);
 }
 
 // Words longer than 16 bytes: decode forward from the start (one lane per word).
@@ -639,6 +794,7 @@ int map_grid_size(int device) {
 
 void clear_tables(const Tables& t, hipStream_t s) {
     hipMemsetAsync(t.ctr, 0, sizeof(Counters), s);
+    if (t.sp.bcur) hipMemsetAsync(t.sp.bcur, 0, kSpillBuckets * sizeof(unsigned long long), s);
     clear_tables_kernel<<<2048, 256, 0, s>>>(t);
 }
 
@@ -648,6 +804,10 @@ void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
     if (g > (uint64_t)grid) g = (uint64_t)grid;
     wc_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt);
+}
+
+void launch_wc_agg(const Tables& t, hipStream_t s) {
+    wc_agg_kernel<<<kSpillBuckets, kThreads, 0, s>>>(t);
 }
 
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s) {

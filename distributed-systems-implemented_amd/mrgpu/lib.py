@@ -58,6 +58,8 @@ class Stats(ctypes.Structure):
         ("output_bytes", c_uint64),
         ("long_keys", c_uint64),
         ("lds_overflow", c_uint64),
+        ("spill_ovf", c_uint64),
+        ("agg_miss", c_uint64),
     ]
 
     def as_dict(self):

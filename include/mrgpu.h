@@ -77,7 +77,9 @@ typedef struct {
     uint64_t distinct_keys;   /* distinct keys after aggregation */
     uint64_t output_bytes;    /* total mr-out bytes */
     uint64_t long_keys;       /* keys > 16 bytes (slow path) */
-    uint64_t lds_overflow;    /* occurrences that missed the LDS table and went to HBM */
+    uint64_t lds_overflow;    /* occurrences that missed the map-side LDS combiner (spilled) */
+    uint64_t spill_ovf;       /* spilled occurrences that found their bucket region full */
+    uint64_t agg_miss;        /* spilled occurrences that missed the bucket aggregator's LDS table */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);

@@ -90,6 +90,24 @@ def test_wc_lds_overflow_and_table_growth(ctx):
         ctx.set_option("short_table_log2", 0)
 
 
+def test_wc_spill_region_full(ctx):
+    """Tiny spill regions: buckets overflow and their keys take the HBM-table path."""
+    files = cases.synthetic(C.KIND_ASCII, 1_000_000, [6_000_000], 15)
+    ctx.set_option("spill_region_blocks", 1)
+    try:
+        check(ctx, "wc", files, nreduces=(10,))
+        assert ctx.stats()["spill_ovf"] > 0
+    finally:
+        ctx.set_option("spill_region_blocks", 0)
+
+
+def test_wc_bucket_aggregator_overflow(ctx):
+    """More distinct spilled keys per bucket than the aggregator's LDS table holds."""
+    files = cases.synthetic(C.KIND_ASCII, 8_000_000, [24_000_000], 16)
+    check(ctx, "wc", files, nreduces=(10,))
+    assert ctx.stats()["agg_miss"] > 0
+
+
 def test_wc_large_vs_oracle(ctx):
     """64 MB C2-style corpus: full bytes vs the C oracle."""
     voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
