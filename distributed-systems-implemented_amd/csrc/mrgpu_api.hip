@@ -64,6 +64,7 @@ struct mrg_ctx {
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
     uint64_t spill_region_keys = 0;
     int64_t spill_force_blocks = 0;
+    int map_mode = 0;  // benchmark ablation of wc_map_kernel phases (0 = normal)
     int sh_log2 = 22, lo_log2 = 14;
     uint64_t list_cap = 1u << 20;
     int grid = 256;
@@ -298,6 +299,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "long_table_log2")) c->lo_log2 = v > 0 ? (int)v : 14;
     else if (!strcmp(name, "list_cap")) c->list_cap = v > 0 ? (uint64_t)v : (1u << 20);
     else if (!strcmp(name, "map_grid")) c->grid = v > 0 ? (int)v : map_grid_size(c->device);
+    else if (!strcmp(name, "map_mode")) c->map_mode = (int)v;
     else if (!strcmp(name, "spill_region_blocks")) { c->spill_force_blocks = v > 0 ? v : 0; if (!v) c->spill_region_keys = 0; }
     else return fail(c, MRG_EINVAL, "unknown option %s", name);
     return MRG_OK;
@@ -396,7 +398,7 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         clear_tables(t, c->s);
         HCHK(c, hipEventRecord(c->ev[0], c->s));
         if (app == MRG_APP_WC) {
-            launch_wc_map(in, len, t, lt, c->grid, 0, c->s);
+            launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s);
             HCHK(c, hipEventRecord(c->ev[1], c->s));
             launch_wc_agg(t, c->s);
         } else if (!grep_nl) {

@@ -100,7 +100,7 @@ struct LetterTables {
 
 // ---- launchers (mrgpu_map.hip) ----
 void clear_tables(const Tables& t, hipStream_t s);
-void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int lds_slots,
+void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode,
                    hipStream_t s);
 void launch_wc_agg(const Tables& t, hipStream_t s);
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);

@@ -103,7 +103,8 @@ def test_wc_spill_region_full(ctx):
 
 def test_wc_bucket_aggregator_overflow(ctx):
     """More distinct spilled keys per bucket than the aggregator's LDS table holds."""
-    files = cases.synthetic(C.KIND_ASCII, 8_000_000, [24_000_000], 16)
+    voc = C.Vocab(C.KIND_ASCII, 1.07, 3_000_000, 16)  # every word of a 3M vocabulary at least once
+    files = [bytes(voc.fill_files([26_000_000], [16], C.wc_params(vocab_lo=0, vocab_hi=3_000_000))[0])]
     check(ctx, "wc", files, nreduces=(10,))
     assert ctx.stats()["agg_miss"] > 0
 
