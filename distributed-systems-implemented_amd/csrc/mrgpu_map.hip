@@ -34,11 +34,10 @@ constexpr int kWavesPerWG = 8;
 constexpr int kThreads = kWavesPerWG * kWave;
 constexpr int kListCap = kChunk / 2;              // max word starts in a chunk
 constexpr int kNMask = 136;                       // [0]=look-back piece, [1..128]=chunk, [129..131]=look-ahead
-constexpr int kLdsSlots = 4096;                   // map-side combiner (per workgroup), 8-way groups
-constexpr int kLdsLimit = kLdsSlots * 15 / 16;
-constexpr int kAggSlots = 7168;                   // bucket aggregator (whole LDS)
-constexpr int kAggLimit = kAggSlots * 15 / 16;
-constexpr int kGroupProbes = 4;                   // groups visited before a lookup counts as a miss
+constexpr int kLdsSets = 1024;                    // map-side combiner (per workgroup): 4-way sets
+constexpr int kLdsLimit = kLdsSets * 4 * 15 / 16;
+constexpr int kAggSets = 1920;                    // bucket aggregator (whole LDS)
+constexpr int kAggLimit = kAggSets * 4 * 15 / 16;
 constexpr int kGlobalProbes = 4096;
 constexpr int kSpillCap = 1536;                   // misses staged per workgroup round (<= one block)
 constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
@@ -50,22 +49,21 @@ struct alignas(16) WaveLds {
     uint16_t list[kListCap];
 };
 
-// LDS hash table in 8-slot groups: 16-bit tags (0 = empty) filter a group with
-// one ds_read_b128; k0/k1/cnt hold the key and its count.  A slot is claimed
-// by a 32-bit CAS on its tag word, then k1 and k0 are written (k0 last: k0 != 0
-// marks the key as published).
-template <int NS>
-struct alignas(16) GTable {
-    uint32_t tags[NS / 2];
-    unsigned long long k0[NS];
-    unsigned long long k1[NS];
-    uint32_t cnt[NS];
+// LDS hash table, 4-way set associative: the 4 k0 of a set are 32 contiguous
+// bytes (two ds_read_b128), so a lookup is a handful of VALU ops and no probe
+// loop.  A way is claimed by CAS on its k0 (0 -> key), then k1 is published
+// (k1 == kUnwritten until then; 0xFF bytes never occur in a UTF-8 key).
+template <int NSETS>
+struct alignas(16) STable {
+    unsigned long long k0[NSETS * 4];
+    unsigned long long k1[NSETS * 4];
+    uint32_t cnt[NSETS * 4];
     uint32_t occ;
 };
 
 struct alignas(16) MapLds {
     WaveLds w[kWavesPerWG];
-    GTable<kLdsSlots> T;
+    STable<kLdsSets> T;
     uint4 spill[kSpillCap];          // this round's combiner misses
     uint16_t rank[kSpillCap];        // rank of each miss within its bucket this round
     uint32_t hist[kSpillBuckets];    // misses per bucket this round
@@ -76,7 +74,7 @@ struct alignas(16) MapLds {
 };
 
 struct alignas(16) AggLds {
-    GTable<kAggSlots> T;
+    STable<kAggSets> T;
 };
 
 // ---------------------------------------------------------------- helpers
@@ -312,85 +310,54 @@ __device__ __forceinline__ void list_append(const Tables& t, uint64_t v) {
 }
 
 // ------------------------------------------------------------ LDS table
-// 8 16-bit tags (one uint4) -> 8-bit masks of positions equal to `tag` / empty.
-__device__ __forceinline__ void tag_masks(uint4 tw, uint32_t tag, uint32_t* mt, uint32_t* me) {
-    const uint32_t ws[4] = {tw.x, tw.y, tw.z, tw.w};
-    const uint32_t rep = tag * 0x00010001u;
-    uint32_t m = 0, e = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const uint32_t x = ws[k] ^ rep;
-        const uint32_t zx = ~(((x & 0x7FFF7FFFu) + 0x7FFF7FFFu) | x) & 0x80008000u;          // halves == tag
-        const uint32_t zw = ~(((ws[k] & 0x7FFF7FFFu) + 0x7FFF7FFFu) | ws[k]) & 0x80008000u;  // halves == 0
-        m |= (((zx >> 15) & 1u) | ((zx >> 30) & 2u)) << (2 * k);
-        e |= (((zw >> 15) & 1u) | ((zw >> 30) & 2u)) << (2 * k);
-    }
-    *mt = m;
-    *me = e;
-}
-
 // Count `add` occurrences of key (k0,k1) in a workgroup LDS table.  Returns
 // false (a miss: the caller spills or forwards the key, where it is still
-// counted exactly) when the table is at its occupancy limit, the key's probe
-// groups are full, the key's slot is claimed but not yet published, or a claim
-// CAS races — the table never waits on another lane (see short_try).
-template <int NS>
-__device__ __forceinline__ bool gt_insert(GTable<NS>& T, uint32_t limit, uint64_t k0, uint64_t k1, uint32_t h,
+// counted exactly) when the key is absent and its set is full or the table is
+// at its occupancy limit, when the key's way is claimed but not yet published,
+// or when a claim CAS races — the table never waits on another lane (see
+// short_try).
+template <int NSETS>
+__device__ __forceinline__ bool st_insert(STable<NSETS>& T, uint32_t limit, uint64_t k0, uint64_t k1, uint32_t h,
                                           uint32_t add) {
-    constexpr uint32_t ng = NS / 8;
-    uint32_t g = __umulhi(h, ng);
-    uint32_t tag = (h * 0x85EBCA6Bu) >> 16;
-    tag = tag ? tag : 1u;
-    for (int probe = 0; probe < kGroupProbes; probe++) {
-        typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-        const u32x4 tv = *reinterpret_cast<const volatile u32x4*>(&T.tags[g * 4]);  // one ds_read_b128
-        const uint4 tw = make_uint4(tv.x, tv.y, tv.z, tv.w);
-        uint32_t mt, me;
-        tag_masks(tw, tag, &mt, &me);
-        while (mt) {
-            const uint32_t slot = g * 8 + __builtin_ctz(mt);
-            mt &= mt - 1;
-            const uint64_t c0 = __hip_atomic_load(&T.k0[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (c0 == 0) return false;  // claimed, not yet published
-            if (c0 == k0 && __hip_atomic_load(&T.k1[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == k1) {
-                atomicAdd(&T.cnt[slot], add);
-                return true;
-            }
-        }
-        if (me) {
-            if (__hip_atomic_load(&T.occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= limit) return false;
-            const uint32_t pos = __builtin_ctz(me);
-            const uint32_t slot = g * 8 + pos;
-            const uint32_t ws[4] = {tw.x, tw.y, tw.z, tw.w};
-            const uint32_t old = ws[pos >> 1];
-            const uint32_t nw = old | (tag << (16 * (pos & 1)));
-            if (atomicCAS(&T.tags[slot >> 1], old, nw) != old) return false;
-            __hip_atomic_store(&T.k1[slot], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_store(&T.k0[slot], (unsigned long long)k0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    const uint32_t base = __umulhi(h, NSETS) * 4;
+    const u64x2 a = *reinterpret_cast<const volatile u64x2*>(&T.k0[base]);
+    const u64x2 b = *reinterpret_cast<const volatile u64x2*>(&T.k0[base + 2]);
+    uint32_t m = (a.x == k0 ? 1u : 0u) | (a.y == k0 ? 2u : 0u) | (b.x == k0 ? 4u : 0u) | (b.y == k0 ? 8u : 0u);
+    while (m) {  // usually one way; several only for long keys sharing their first 8 bytes
+        const uint32_t slot = base + __builtin_ctz(m);
+        m &= m - 1;
+        const uint64_t v = __hip_atomic_load(&T.k1[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (v == k1) {
             atomicAdd(&T.cnt[slot], add);
-            atomicAdd(&T.occ, 1u);
             return true;
         }
-        g = (g + 1 == ng) ? 0 : g + 1;
+        if (v == kUnwritten) return false;  // claimed, not yet published
     }
-    return false;
+    const uint32_t e = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u) | (b.x == 0 ? 4u : 0u) | (b.y == 0 ? 8u : 0u);
+    if (!e || __hip_atomic_load(&T.occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= limit) return false;
+    const uint32_t slot = base + __builtin_ctz(e);
+    if (atomicCAS(&T.k0[slot], 0ull, (unsigned long long)k0) != 0ull) return false;
+    __hip_atomic_store(&T.k1[slot], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    atomicAdd(&T.cnt[slot], add);
+    atomicAdd(&T.occ, 1u);
+    return true;
 }
 
-template <int NS>
-__device__ __forceinline__ void gt_init(GTable<NS>& T, uint32_t tid, uint32_t nthreads) {
-    for (uint32_t i = tid; i < (uint32_t)NS; i += nthreads) {
-        if (!(i & 1)) T.tags[i >> 1] = 0;
+template <int NSETS>
+__device__ __forceinline__ void st_init(STable<NSETS>& T, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t i = tid; i < (uint32_t)NSETS * 4; i += nthreads) {
         T.k0[i] = 0;
-        T.k1[i] = 0;
+        T.k1[i] = kUnwritten;
         T.cnt[i] = 0;
     }
     if (tid == 0) T.occ = 0;
 }
 
-// Add every published slot of the table to the HBM ShortTable.
-template <int NS>
-__device__ __forceinline__ void gt_flush(GTable<NS>& T, const Tables& t, uint32_t tid, uint32_t nthreads) {
-    for (uint32_t i = tid; i < (uint32_t)NS; i += nthreads) {
+// Add every occupied way of the table to the HBM ShortTable.
+template <int NSETS>
+__device__ __forceinline__ void st_flush(STable<NSETS>& T, const Tables& t, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t i = tid; i < (uint32_t)NSETS * 4; i += nthreads) {
         const uint64_t k0 = T.k0[i];
         if (k0 != 0) short_insert(t, k0, T.k1[i], T.cnt[i]);
     }
@@ -515,7 +482,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     const uint32_t wv = tid >> 6;
     WaveLds& W = L.w[wv];
 
-    gt_init(L.T, tid, kThreads);
+    st_init(L.T, tid, kThreads);
     for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
         L.hist[b] = 0;
         L.fill[b] = 0;
@@ -618,7 +585,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     acc += h;
                     continue;
                 }
-                const bool hit = gt_insert(L.T, kLdsLimit, k0, k1, h, 1);
+                const bool hit = st_insert(L.T, kLdsLimit, k0, k1, h, 1);
                 if (mode & 16) { acc += hit; continue; }
                 const uint64_t mm = __ballot(!hit);
                 if (mm) {  // wave-aggregated append of the misses to this round's spill list
@@ -651,7 +618,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 
     for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads)
         if (L.blkA[b] < kOvfBlock && L.fill[b] > 0) t.sp.fills[(uint64_t)b * t.sp.region_blocks + L.blkA[b]] = L.fill[b];
-    gt_flush(L.T, t, tid, kThreads);
+    st_flush(L.T, t, tid, kThreads);
     if (ovf) atomicAdd(&t.ctr->spill_ovf, (unsigned long long)ovf);
     if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
     if (utf8_chunks && lane == 0) atomicAdd(&t.ctr->chunks_utf8, (unsigned long long)utf8_chunks);
@@ -664,7 +631,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 __global__ void __launch_bounds__(kThreads) wc_agg_kernel(Tables t) {
     __shared__ AggLds A;
     const uint32_t tid = threadIdx.x;
-    gt_init(A.T, tid, kThreads);
+    st_init(A.T, tid, kThreads);
     __syncthreads();
     const uint32_t b = blockIdx.x;
     uint64_t reserved = t.sp.bcur[b];
@@ -679,14 +646,14 @@ __global__ void __launch_bounds__(kThreads) wc_agg_kernel(Tables t) {
             const uint4 k = blk[i];
             const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
             const uint32_t h = fold32(k.x, k.y, k.z, k.w);
-            if (!gt_insert(A.T, kAggLimit, k0, k1, h, 1)) {
+            if (!st_insert(A.T, kAggLimit, k0, k1, h, 1)) {
                 short_insert(t, k0, k1, 1);
                 miss++;
             }
         }
     }
     __syncthreads();
-    gt_flush(A.T, t, tid, kThreads);
+    st_flush(A.T, t, tid, kThreads);
     if (miss) atomicAdd(&t.ctr->agg_miss, (unsigned long long)miss);
 }
 
