@@ -57,7 +57,7 @@ constexpr uint64_t kHostMagic = 0x4D524748424F5354ull;  // "MRGHBOST"
 struct mrg_ctx {
     int device = 0;
     hipStream_t s = nullptr;
-    hipEvent_t ev[8] = {};
+    hipEvent_t ev[12] = {};
     std::string err;
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
@@ -401,12 +401,16 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
             launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s);
             HCHK(c, hipEventRecord(c->ev[1], c->s));
             launch_wc_agg(t, c->s);
+            HCHK(c, hipEventRecord(c->ev[8], c->s));
         } else if (!grep_nl) {
             if (plen) launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);
             else launch_grep_all_lines(in, len, t, c->grid, c->s);
         }
         HCHK(c, hipGetLastError());
-        if (app != MRG_APP_WC) HCHK(c, hipEventRecord(c->ev[1], c->s));
+        if (app != MRG_APP_WC) {
+            HCHK(c, hipEventRecord(c->ev[1], c->s));
+            HCHK(c, hipEventRecord(c->ev[8], c->s));
+        }
         if ((rc = read_counters(c))) return rc;
         if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
         uint64_t nlist = c->h_ctr->nlist;
@@ -427,6 +431,9 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         HCHK(c, hipEventRecord(c->ev[3], c->s));
         HCHK(c, hipEventSynchronize(c->ev[3]));
         c->stats.map_total_ms = ev_ms(c->ev[0], c->ev[3]);
+        c->stats.agg_ms = ev_ms(c->ev[1], c->ev[8]);
+        c->stats.long_ms = ev_ms(c->ev[8], c->ev[2]);
+        c->stats.collect_ms = ev_ms(c->ev[2], c->ev[3]);
         *out = p;
         return MRG_OK;
     }

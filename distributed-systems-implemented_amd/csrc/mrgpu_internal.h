@@ -60,7 +60,7 @@ struct Counters {
 // Bucket b owns keys [b*region_keys, (b+1)*region_keys) of `pool` (16-B keys
 // {k0,k1}); it is filled in blocks of kSpillBlock keys, each block written by
 // one workgroup; fills[b*region_blocks + j] = valid keys in block j.
-constexpr int kSpillBuckets = 256;
+constexpr int kSpillBuckets = 512;
 constexpr int kSpillBlock = 2048;
 struct Spill {
     uint4* pool;

@@ -26,17 +26,17 @@
 
 namespace mrg {
 
-constexpr int kChunk = 2048;
+constexpr int kChunk = 1024;                      // bytes per wave-chunk (16 B per lane)
 constexpr int kBack = 16;
 constexpr int kAhead = 64;
-constexpr int kBuf = kBack + kChunk + kAhead;  // 2128, multiple of 16
-constexpr int kWavesPerWG = 8;
+constexpr int kBuf = kBack + kChunk + kAhead;  // 1104, multiple of 16
+constexpr int kWavesPerWG = 16;
 constexpr int kThreads = kWavesPerWG * kWave;
 constexpr int kListCap = kChunk / 2;              // max word starts in a chunk
-constexpr int kNMask = 136;                       // [0]=look-back piece, [1..128]=chunk, [129..131]=look-ahead
 constexpr int kLdsSets = 1024;                    // map-side combiner (per workgroup): 4-way sets
 constexpr int kLdsLimit = kLdsSets * 4 * 15 / 16;
-constexpr int kAggSets = 1920;                    // bucket aggregator (whole LDS)
+constexpr int kAggThreads = 512;
+constexpr int kAggSets = 960;                     // bucket aggregator (half the LDS: 2 workgroups per CU)
 constexpr int kAggLimit = kAggSets * 4 * 15 / 16;
 constexpr int kGlobalProbes = 4096;
 constexpr int kSpillCap = 1536;                   // misses staged per workgroup round (<= one block)
@@ -45,7 +45,6 @@ constexpr uint32_t kOvfBlock = 0xFFFFFFFEu;
 
 struct alignas(16) WaveLds {
     uint8_t buf[kBuf];
-    uint16_t mask[kNMask];
     uint16_t list[kListCap];
 };
 
@@ -66,6 +65,7 @@ struct alignas(16) MapLds {
     STable<kLdsSets> T;
     uint4 spill[kSpillCap];          // this round's combiner misses
     uint16_t rank[kSpillCap];        // rank of each miss within its bucket this round
+    uint16_t bkt[kSpillCap];         // bucket of each miss
     uint32_t hist[kSpillBuckets];    // misses per bucket this round
     uint32_t fill[kSpillBuckets];    // keys already in the current block of each bucket stream
     uint32_t blkA[kSpillBuckets];    // current block of each bucket stream
@@ -363,13 +363,17 @@ __device__ __forceinline__ void st_flush(STable<NSETS>& T, const Tables& t, uint
     }
 }
 
-__device__ __forceinline__ uint32_t spill_bucket(uint64_t k0, uint64_t k1) {
-    return (uint32_t)(short_hash64(k0, k1) >> 56);  // top 8 bits; the HBM table indexes by low bits
+// Spill bucket from the combiner hash h = fold32(key): top byte of a second
+// multiplicative hash, so keys of one bucket still spread over all sets of the
+// aggregator's table (which indexes by the top bits of h).
+__device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
+    static_assert(kSpillBuckets == 512, "bucket = top 9 bits");
+    return (h * 0x85EBCA6Bu) >> 23;
 }
 
 // ------------------------------------------------------------ chunk loading
 struct ChunkRegs {
-    uint4 a, b, h;  // a: bytes [16l,16l+16), b: [1024+16l, ...), h: halo piece (lanes 0-4)
+    uint4 a, h;  // a: chunk bytes [16l, 16l+16); h: halo piece (lanes 0-3 look-ahead, lane 4 look-back)
 };
 
 __device__ __forceinline__ uint4 load16_bounded(const uint8_t* in, uint64_t n, int64_t off) {
@@ -386,14 +390,12 @@ __device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ in, uint6
     if (cs + kChunk + kAhead <= n && cs >= (uint64_t)kBack) {
         const uint4* p = reinterpret_cast<const uint4*>(in + cs);
         r.a = p[lane];
-        r.b = p[64 + lane];
-        if (lane < 4) r.h = p[128 + lane];
+        if (lane < 4) r.h = p[64 + lane];
         else if (lane == 4) r.h = p[-1];
         else r.h = make_uint4(0, 0, 0, 0);
     } else {
         r.a = load16_bounded(in, n, (int64_t)cs + 16 * lane);
-        r.b = load16_bounded(in, n, (int64_t)cs + 1024 + 16 * lane);
-        if (lane < 4) r.h = load16_bounded(in, n, (int64_t)cs + 2048 + 16 * lane);
+        if (lane < 4) r.h = load16_bounded(in, n, (int64_t)cs + kChunk + 16 * lane);
         else if (lane == 4) r.h = load16_bounded(in, n, (int64_t)cs - 16);
         else r.h = make_uint4(0, 0, 0, 0);
     }
@@ -402,8 +404,7 @@ __device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ in, uint6
 __device__ __forceinline__ void stage_chunk(WaveLds& W, const ChunkRegs& r, uint32_t lane) {
     uint4* b4 = reinterpret_cast<uint4*>(W.buf);
     b4[1 + lane] = r.a;
-    b4[65 + lane] = r.b;
-    if (lane < 4) b4[129 + lane] = r.h;
+    if (lane < 4) b4[65 + lane] = r.h;
     else if (lane == 4) b4[0] = r.h;
 }
 
@@ -418,8 +419,7 @@ __device__ __forceinline__ uint32_t spill_grab(const Tables& t, uint32_t b) {
 __device__ void flush_spill(MapLds& L, const Tables& t, uint32_t tid, uint64_t& ovf) {
     const uint32_t ns = min(L.nspill, (uint32_t)kSpillCap);
     for (uint32_t i = tid; i < ns; i += kThreads) {
-        const uint4 k = L.spill[i];
-        const uint32_t b = spill_bucket(((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z);
+        const uint32_t b = L.bkt[i];
         L.rank[i] = (uint16_t)atomicAdd(&L.hist[b], 1u);
     }
     __syncthreads();
@@ -433,7 +433,7 @@ __device__ void flush_spill(MapLds& L, const Tables& t, uint32_t tid, uint64_t& 
     for (uint32_t i = tid; i < ns; i += kThreads) {
         const uint4 k = L.spill[i];
         const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
-        const uint32_t b = spill_bucket(k0, k1);
+        const uint32_t b = L.bkt[i];
         const uint32_t pos = L.fill[b] + L.rank[i];
         const bool first = pos < (uint32_t)kSpillBlock;
         const uint32_t blk = first ? L.blkA[b] : L.blkB[b];
@@ -505,51 +505,44 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint64_t cs = c * kChunk;
             if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);  // prefetch next round
             if (mode & 1) {
-                acc ^= cur.a.x ^ cur.a.y ^ cur.a.z ^ cur.a.w ^ cur.b.x ^ cur.b.y ^ cur.b.z ^ cur.b.w ^ cur.h.x;
+                acc ^= cur.a.x ^ cur.a.y ^ cur.a.z ^ cur.a.w ^ cur.h.x;
                 cur = nxt;
                 continue;
             }
 
             stage_chunk(W, cur, lane);
-            uint32_t hi = (cur.a.x | cur.a.y | cur.a.z | cur.a.w | cur.b.x | cur.b.y | cur.b.z | cur.b.w | cur.h.x |
-                           cur.h.y | cur.h.z | cur.h.w) & 0x80808080u;
+            uint32_t hi = (cur.a.x | cur.a.y | cur.a.z | cur.a.w | cur.h.x | cur.h.y | cur.h.z | cur.h.w) & 0x80808080u;
             const bool ascii = __ballot(hi != 0) == 0;
-            uint32_t mA, mB, mH = 0;
+            uint32_t mA, mH = 0;
             if (ascii) {
                 mA = ascii_mask16(cur.a);
-                mB = ascii_mask16(cur.b);
                 if (lane < 5) mH = ascii_mask16(cur.h);
             } else {
                 utf8_chunks++;
                 wave_sync();
                 mA = utf8_letter_mask<16>(W.buf, kBack + 16 * lane, lt);
-                mB = utf8_letter_mask<16>(W.buf, kBack + 1024 + 16 * lane, lt);
-                if (lane < 3) mH = utf8_letter_mask<16>(W.buf, kBack + 2048 + 16 * lane, lt);
+                if (lane < 3) mH = utf8_letter_mask<16>(W.buf, kBack + kChunk + 16 * lane, lt);
                 else if (lane == 4) mH = utf8_letter_mask<8>(W.buf, 8, lt) << 8;  // look-back bits 8..15
             }
-            W.mask[1 + lane] = (uint16_t)mA;
-            W.mask[65 + lane] = (uint16_t)mB;
-            if (lane < 4) W.mask[129 + lane] = (uint16_t)mH;
-            else if (lane == 4) W.mask[0] = (uint16_t)mH;
-
-            // word starts: letter byte whose predecessor byte is not a letter byte
-            const uint32_t prevA_m = __shfl(mA, (int)((lane + 63) & 63));
-            const uint32_t prevB_m = __shfl(mB, (int)((lane + 63) & 63));
-            const uint32_t lastA = __shfl(mA, 63);
+            // word starts (letter byte whose predecessor is not a letter byte) and
+            // lengths (ctz over this piece + the next two pieces' masks), packed
+            // into the list as start | min(len, 31) << 11
+            const uint32_t lm1 = (lane + 63) & 63, lp1 = (lane + 1) & 63, lp2 = (lane + 2) & 63;
+            const uint32_t prevA_m = __shfl(mA, (int)lm1);
             const uint32_t back = __shfl(mH, 4);
+            const uint32_t x1 = __shfl(mA, (int)lp1), z1 = __shfl(mH, (int)lp1);
+            const uint32_t x2 = __shfl(mA, (int)lp2), z2 = __shfl(mH, (int)lp2);
+            const uint64_t winA = (uint64_t)mA | ((uint64_t)(lane < 63 ? x1 : z1) << 16) |
+                                  ((uint64_t)(lane < 62 ? x2 : z2) << 32);
             const uint32_t pa = (lane == 0 ? back : prevA_m) >> 15 & 1u;
-            const uint32_t pb = (lane == 0 ? lastA : prevB_m) >> 15 & 1u;
             uint32_t SA = mA & ~((mA << 1) | pa) & 0xFFFFu;
-            uint32_t SB = mB & ~((mB << 1) | pb) & 0xFFFFu;
             uint32_t total;
-            uint32_t j = wave_excl_scan5(__popc(SA) + __popc(SB), &total);
+            uint32_t j = wave_excl_scan5(__popc(SA), &total);
             while (SA) {
-                W.list[j++] = (uint16_t)(16 * lane + __builtin_ctz(SA));
+                const uint32_t bit = __builtin_ctz(SA);
+                const uint32_t len = min((uint32_t)__builtin_ctzll(~(winA >> bit)), 31u);
+                W.list[j++] = (uint16_t)((16 * lane + bit) | (len << 11));
                 SA &= SA - 1;
-            }
-            while (SB) {
-                W.list[j++] = (uint16_t)(1024 + 16 * lane + __builtin_ctz(SB));
-                SB &= SB - 1;
             }
             wave_sync();
             if (mode & 2) {
@@ -559,11 +552,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             }
 
             for (uint32_t w = lane; w < total; w += 64) {
-                const uint32_t s = W.list[w];
-                const uint32_t p = s >> 4, bsh = s & 15;
-                const uint64_t win =
-                    (uint64_t)W.mask[p + 1] | ((uint64_t)W.mask[p + 2] << 16) | ((uint64_t)W.mask[p + 3] << 32);
-                const uint32_t len = (uint32_t)__builtin_ctzll(~(win >> bsh));
+                const uint32_t e = W.list[w];
+                const uint32_t s = e & 0x7FFu, len = e >> 11;
                 if (len > 16) {
                     list_append(t, cs + s);
                     continue;
@@ -597,6 +587,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint32_t slot = base + mbcnt64(mm);
                         if (slot < (uint32_t)kSpillCap) {
                             L.spill[slot] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                            L.bkt[slot] = (uint16_t)spill_bucket(h);
                         } else {
                             short_insert(t, k0, k1, 1);
                             ovf++;
@@ -628,10 +619,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 // table (a bucket holds ~1/256 of the distinct spilled keys), then adds the
 // per-key totals to the HBM ShortTable — one HBM atomic per distinct key per
 // bucket instead of one per occurrence.
-__global__ void __launch_bounds__(kThreads) wc_agg_kernel(Tables t) {
+__global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t) {
     __shared__ AggLds A;
     const uint32_t tid = threadIdx.x;
-    st_init(A.T, tid, kThreads);
+    st_init(A.T, tid, kAggThreads);
     __syncthreads();
     const uint32_t b = blockIdx.x;
     uint64_t reserved = t.sp.bcur[b];
@@ -642,18 +633,28 @@ __global__ void __launch_bounds__(kThreads) wc_agg_kernel(Tables t) {
     for (uint64_t j = 0; j < nblk; j++) {
         const uint32_t f = t.sp.fills[(uint64_t)b * t.sp.region_blocks + j];
         const uint4* blk = base + j * kSpillBlock;
-        for (uint32_t i = tid; i < f; i += kThreads) {
-            const uint4 k = blk[i];
-            const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
-            const uint32_t h = fold32(k.x, k.y, k.z, k.w);
-            if (!st_insert(A.T, kAggLimit, k0, k1, h, 1)) {
-                short_insert(t, k0, k1, 1);
-                miss++;
+        for (uint32_t i0 = tid; i0 < f; i0 += 4 * kAggThreads) {
+            uint4 kk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {  // issue the 4 loads before any insert
+                const uint32_t i = i0 + u * kAggThreads;
+                kk[u] = i < f ? blk[i] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint4 k = kk[u];
+                if (k.x == 0 && k.y == 0) continue;  // past the block's fill (keys have k0 != 0)
+                const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
+                const uint32_t h = fold32(k.x, k.y, k.z, k.w);
+                if (!st_insert(A.T, kAggLimit, k0, k1, h, 1)) {
+                    short_insert(t, k0, k1, 1);
+                    miss++;
+                }
             }
         }
     }
     __syncthreads();
-    st_flush(A.T, t, tid, kThreads);
+    st_flush(A.T, t, tid, kAggThreads);
     if (miss) atomicAdd(&t.ctr->agg_miss, (unsigned long long)miss);
 }
 
@@ -708,11 +709,9 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
         if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);
         stage_chunk(W, cur, lane);
         wave_sync();
-        uint32_t cand[2] = {eq_mask16(cur.a, rep), eq_mask16(cur.b, rep)};
-#pragma unroll
-        for (int piece = 0; piece < 2; piece++) {
-            uint32_t m = cand[piece];
-            const uint32_t base = piece * 1024 + 16 * lane;
+        {
+            uint32_t m = eq_mask16(cur.a, rep);
+            const uint32_t base = 16 * lane;
             while (m) {
                 const uint32_t bit = __builtin_ctz(m);
                 m &= m - 1;
@@ -861,7 +860,7 @@ void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
 }
 
 void launch_wc_agg(const Tables& t, hipStream_t s) {
-    wc_agg_kernel<<<kSpillBuckets, kThreads, 0, s>>>(t);
+    wc_agg_kernel<<<kSpillBuckets, kAggThreads, 0, s>>>(t);
 }
 
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s) {

@@ -60,6 +60,9 @@ class Stats(ctypes.Structure):
         ("lds_overflow", c_uint64),
         ("spill_ovf", c_uint64),
         ("agg_miss", c_uint64),
+        ("agg_ms", ctypes.c_double),
+        ("long_ms", ctypes.c_double),
+        ("collect_ms", ctypes.c_double),
     ]
 
     def as_dict(self):

@@ -80,6 +80,9 @@ typedef struct {
     uint64_t lds_overflow;    /* occurrences that missed the map-side LDS combiner (spilled) */
     uint64_t spill_ovf;       /* spilled occurrences that found their bucket region full */
     uint64_t agg_miss;        /* spilled occurrences that missed the bucket aggregator's LDS table */
+    double agg_ms;            /* wc: per-bucket aggregation kernel */
+    double long_ms;           /* long-word / grep-line resolution, incl. its host round trip */
+    double collect_ms;        /* distinct keys -> records (partition = ihash % nReduce) */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);
