@@ -62,8 +62,9 @@ struct mrg_ctx {
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
-    uint64_t spill_region_keys = 0;
-    int64_t spill_force_blocks = 0;
+    uint64_t spill_sub_keys = 0;
+    uint32_t spill_nwg = 1;
+    int64_t spill_force_sub = 0;
     int map_mode = 0;  // benchmark ablation of wc_map_kernel phases (0 = normal)
     int sh_log2 = 22, lo_log2 = 14;
     uint64_t list_cap = 1u << 20;
@@ -125,31 +126,25 @@ static Tables make_tables(mrg_ctx* c) {
     t.list_cap = c->list_cap;
     t.ctr = (Counters*)c->ctr.p;
     t.sp.pool = (uint4*)c->spool.p;
-    t.sp.region_keys = c->spill_region_keys;
-    t.sp.region_blocks = c->spill_region_keys / kSpillBlock;
-    t.sp.bcur = (unsigned long long*)c->spmeta.p;
-    t.sp.fills = c->spmeta.p ? (uint32_t*)((char*)c->spmeta.p + kSpillBuckets * sizeof(unsigned long long)) : nullptr;
+    t.sp.sub_keys = c->spill_sub_keys;
+    t.sp.nwg = c->spill_nwg;
+    t.sp.counts = (uint32_t*)c->spmeta.p;
     return t;
 }
 
-// Spill pool for LDS-combiner misses: ~1.5 bytes of pool per input byte (C2
-// spills ~1 byte per input byte); a bucket that fills its region degrades to
-// HBM-table inserts, so the size only affects speed, never results.
+// Spill pool for LDS-combiner misses: 1.5 bytes of pool per input byte (C2
+// spills ~1 byte of keys per input byte), split into kSpillBuckets x nwg
+// streams.  A stream that fills up sends the rest of its keys to the HBM
+// table, so the size only affects speed, never results.
 static int ensure_spill(mrg_ctx* c, uint64_t n) {
-    uint64_t keys = (n + n / 2) / 16 / kSpillBuckets;
-    keys = ((keys + kSpillBlock - 1) / kSpillBlock + 2) * kSpillBlock;
-    if (c->spill_force_blocks > 0) {  // test knob: tiny regions exercise the region-full path
-        c->spill_region_keys = (uint64_t)c->spill_force_blocks * kSpillBlock;
-        keys = std::max<uint64_t>(keys, c->spill_region_keys);
-        HCHK(c, c->spool.ensure(keys * kSpillBuckets * sizeof(uint4)));
-        HCHK(c, c->spmeta.ensure(kSpillBuckets * sizeof(unsigned long long) + kSpillBuckets * (keys / kSpillBlock) * 4));
-        return MRG_OK;
-    }
-    if (keys > c->spill_region_keys || !c->spool.p) {
-        c->spill_region_keys = keys;
-        HCHK(c, c->spool.ensure(keys * kSpillBuckets * sizeof(uint4)));
-        HCHK(c, c->spmeta.ensure(kSpillBuckets * sizeof(unsigned long long) + kSpillBuckets * (keys / kSpillBlock) * 4));
-    }
+    const uint32_t nwg = wc_map_grid(n, c->grid);
+    uint64_t sub = (n + n / 2) / 16 / ((uint64_t)kSpillBuckets * nwg) + 64;
+    sub = (sub + 63) & ~63ull;
+    if (c->spill_force_sub > 0) sub = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
+    c->spill_nwg = nwg;
+    c->spill_sub_keys = sub;
+    HCHK(c, c->spool.ensure(sub * kSpillBuckets * nwg * sizeof(uint4)));
+    HCHK(c, c->spmeta.ensure((size_t)kSpillBuckets * nwg * sizeof(uint32_t)));
     return MRG_OK;
 }
 
@@ -300,7 +295,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "list_cap")) c->list_cap = v > 0 ? (uint64_t)v : (1u << 20);
     else if (!strcmp(name, "map_grid")) c->grid = v > 0 ? (int)v : map_grid_size(c->device);
     else if (!strcmp(name, "map_mode")) c->map_mode = (int)v;
-    else if (!strcmp(name, "spill_region_blocks")) { c->spill_force_blocks = v > 0 ? v : 0; if (!v) c->spill_region_keys = 0; }
+    else if (!strcmp(name, "spill_stream_keys")) c->spill_force_sub = v > 0 ? v : 0;
     else return fail(c, MRG_EINVAL, "unknown option %s", name);
     return MRG_OK;
 }

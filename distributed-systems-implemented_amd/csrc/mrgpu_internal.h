@@ -57,17 +57,16 @@ struct Counters {
 };
 
 // Spill of LDS-combiner misses, hash-partitioned into kSpillBuckets buckets.
-// Bucket b owns keys [b*region_keys, (b+1)*region_keys) of `pool` (16-B keys
-// {k0,k1}); it is filled in blocks of kSpillBlock keys, each block written by
-// one workgroup; fills[b*region_blocks + j] = valid keys in block j.
+// Every (bucket b, map workgroup g) pair owns a fixed stream of `sub_keys`
+// 16-B keys {k0,k1} at pool[(b*nwg + g)*sub_keys]; the workgroup appends with
+// an LDS cursor (no HBM atomics, no barriers) and records the stream length in
+// counts[b*nwg + g].  Keys beyond sub_keys go to the HBM table instead.
 constexpr int kSpillBuckets = 512;
-constexpr int kSpillBlock = 2048;
 struct Spill {
     uint4* pool;
-    uint64_t region_keys;            // multiple of kSpillBlock
-    unsigned long long* bcur;        // [kSpillBuckets] keys reserved per bucket
-    uint32_t* fills;                 // [kSpillBuckets * region_blocks]
-    uint64_t region_blocks;
+    uint64_t sub_keys;
+    uint32_t* counts;                // [kSpillBuckets * nwg]
+    uint32_t nwg;
 };
 
 struct Tables {
@@ -103,6 +102,7 @@ void clear_tables(const Tables& t, hipStream_t s);
 void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode,
                    hipStream_t s);
 void launch_wc_agg(const Tables& t, hipStream_t s);
+uint32_t wc_map_grid(uint64_t n, int grid);
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
                      hipStream_t s);

@@ -33,15 +33,12 @@ constexpr int kBuf = kBack + kChunk + kAhead;  // 1104, multiple of 16
 constexpr int kWavesPerWG = 16;
 constexpr int kThreads = kWavesPerWG * kWave;
 constexpr int kListCap = kChunk / 2;              // max word starts in a chunk
-constexpr int kLdsSets = 1024;                    // map-side combiner (per workgroup): 4-way sets
+constexpr int kLdsSets = 1536;                    // map-side combiner (per workgroup): 4-way sets
 constexpr int kLdsLimit = kLdsSets * 4 * 15 / 16;
 constexpr int kAggThreads = 512;
 constexpr int kAggSets = 960;                     // bucket aggregator (half the LDS: 2 workgroups per CU)
 constexpr int kAggLimit = kAggSets * 4 * 15 / 16;
 constexpr int kGlobalProbes = 4096;
-constexpr int kSpillCap = 1536;                   // misses staged per workgroup round (<= one block)
-constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
-constexpr uint32_t kOvfBlock = 0xFFFFFFFEu;
 
 struct alignas(16) WaveLds {
     uint8_t buf[kBuf];
@@ -63,14 +60,7 @@ struct alignas(16) STable {
 struct alignas(16) MapLds {
     WaveLds w[kWavesPerWG];
     STable<kLdsSets> T;
-    uint4 spill[kSpillCap];          // this round's combiner misses
-    uint16_t rank[kSpillCap];        // rank of each miss within its bucket this round
-    uint16_t bkt[kSpillCap];         // bucket of each miss
-    uint32_t hist[kSpillBuckets];    // misses per bucket this round
-    uint32_t fill[kSpillBuckets];    // keys already in the current block of each bucket stream
-    uint32_t blkA[kSpillBuckets];    // current block of each bucket stream
-    uint32_t blkB[kSpillBuckets];    // next block (when this round's run overflows blkA)
-    uint32_t nspill;
+    uint32_t cur[kSpillBuckets];     // keys appended to this workgroup's stream of each bucket
 };
 
 struct alignas(16) AggLds {
@@ -409,72 +399,12 @@ __device__ __forceinline__ void stage_chunk(WaveLds& W, const ChunkRegs& r, uint
 }
 
 // ------------------------------------------------------------ wc map kernel
-__device__ __forceinline__ uint32_t spill_grab(const Tables& t, uint32_t b) {
-    const unsigned long long k = atomicAdd(&t.sp.bcur[b], (unsigned long long)kSpillBlock);
-    return (k + kSpillBlock <= t.sp.region_keys) ? (uint32_t)(k / kSpillBlock) : kOvfBlock;
-}
-
-// End of a round: write the round's combiner misses into their bucket streams.
-// Every thread of the workgroup calls this (contains __syncthreads).
-__device__ void flush_spill(MapLds& L, const Tables& t, uint32_t tid, uint64_t& ovf) {
-    const uint32_t ns = min(L.nspill, (uint32_t)kSpillCap);
-    for (uint32_t i = tid; i < ns; i += kThreads) {
-        const uint32_t b = L.bkt[i];
-        L.rank[i] = (uint16_t)atomicAdd(&L.hist[b], 1u);
-    }
-    __syncthreads();
-    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
-        const uint32_t h = L.hist[b];
-        if (!h) continue;
-        if (L.blkA[b] == kNoBlock) L.blkA[b] = spill_grab(t, b);
-        if (L.fill[b] + h > (uint32_t)kSpillBlock && L.blkA[b] != kOvfBlock) L.blkB[b] = spill_grab(t, b);
-    }
-    __syncthreads();
-    for (uint32_t i = tid; i < ns; i += kThreads) {
-        const uint4 k = L.spill[i];
-        const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
-        const uint32_t b = L.bkt[i];
-        const uint32_t pos = L.fill[b] + L.rank[i];
-        const bool first = pos < (uint32_t)kSpillBlock;
-        const uint32_t blk = first ? L.blkA[b] : L.blkB[b];
-        if (blk >= kOvfBlock) {  // bucket region exhausted: count in the HBM table instead
-            short_insert(t, k0, k1, 1);
-            ovf++;
-        } else {
-            t.sp.pool[(uint64_t)b * t.sp.region_keys + (uint64_t)blk * kSpillBlock + (first ? pos : pos - kSpillBlock)] = k;
-        }
-    }
-    __syncthreads();
-    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
-        const uint32_t h = L.hist[b];
-        if (!h) continue;
-        const uint32_t f = L.fill[b] + h;
-        if (L.blkA[b] == kOvfBlock) {
-            L.fill[b] = 0;
-        } else if (f >= (uint32_t)kSpillBlock) {
-            t.sp.fills[(uint64_t)b * t.sp.region_blocks + L.blkA[b]] = kSpillBlock;
-            if (f > (uint32_t)kSpillBlock) { L.blkA[b] = L.blkB[b]; L.fill[b] = f - kSpillBlock; }
-            else { L.blkA[b] = kNoBlock; L.fill[b] = 0; }
-        } else {
-            L.fill[b] = f;
-        }
-        L.hist[b] = 0;
-        L.blkB[b] = kNoBlock;
-    }
-    if (tid == 0) {
-        if (ns) atomicAdd(&t.ctr->spilled, (unsigned long long)ns);
-        L.nspill = 0;
-    }
-    __syncthreads();
-}
-
-// Rounds: in round r workgroup g's 8 waves take chunks (r*G + g)*8 + wave, so
-// every thread runs the same number of rounds and the per-round spill flush
-// can use workgroup barriers.
+// Each wave walks its chunks independently (grid stride over waves, one chunk
+// prefetched ahead); the only workgroup barriers are at start and end.
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
                                                           Tables t, LetterTables lt, uint32_t mode) {
     // mode (benchmark ablation only; results are wrong unless 0): 1 = read input only,
-    // 8 = drop the per-round spill flush, 16 = drop combiner misses (no spill append),
+    // 16 = drop combiner misses (no spill append),
     // 2 = tokenize only (no per-word work), 4 = per-word key extraction without the table
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
@@ -483,25 +413,19 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     WaveLds& W = L.w[wv];
 
     st_init(L.T, tid, kThreads);
-    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
-        L.hist[b] = 0;
-        L.fill[b] = 0;
-        L.blkA[b] = kNoBlock;
-        L.blkB[b] = kNoBlock;
-    }
-    if (tid == 0) L.nspill = 0;
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) L.cur[b] = 0;
     __syncthreads();
 
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
-    const uint64_t nrounds = (nchunks + stride - 1) / stride;
     const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
+    const uint64_t my_stream0 = (uint64_t)blockIdx.x * t.sp.sub_keys;  // + b*nwg*sub_keys
+    const uint64_t bstride = (uint64_t)t.sp.nwg * t.sp.sub_keys;
     uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
     ChunkRegs cur, nxt;
     if (c0 < nchunks) load_chunk(in, n, c0 * kChunk, lane, cur);
 
-    for (uint64_t r = 0; r < nrounds; r++) {
-        const uint64_t c = c0 + r * stride;
-        if (c < nchunks) {
+    for (uint64_t c = c0; c < nchunks; c += stride) {
+        {
             const uint64_t cs = c * kChunk;
             if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);  // prefetch next round
             if (mode & 1) {
@@ -577,38 +501,31 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 }
                 const bool hit = st_insert(L.T, kLdsLimit, k0, k1, h, 1);
                 if (mode & 16) { acc += hit; continue; }
-                const uint64_t mm = __ballot(!hit);
-                if (mm) {  // wave-aggregated append of the misses to this round's spill list
-                    const uint32_t leader = (uint32_t)__builtin_ctzll(mm);
-                    uint32_t base = 0;
-                    if (lane == leader) base = atomicAdd(&L.nspill, (uint32_t)__popcll(mm));
-                    base = __shfl(base, (int)leader);
-                    if (!hit) {
-                        const uint32_t slot = base + mbcnt64(mm);
-                        if (slot < (uint32_t)kSpillCap) {
-                            L.spill[slot] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-                            L.bkt[slot] = (uint16_t)spill_bucket(h);
-                        } else {
-                            short_insert(t, k0, k1, 1);
-                            ovf++;
-                        }
+                if (!hit) {  // append to this workgroup's stream of the key's bucket
+                    const uint32_t b = spill_bucket(h);
+                    const uint32_t pos = atomicAdd(&L.cur[b], 1u);
+                    if (pos < t.sp.sub_keys) {
+                        t.sp.pool[my_stream0 + b * bstride + pos] =
+                            make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                    } else {
+                        short_insert(t, k0, k1, 1);
+                        ovf++;
                     }
                 }
             }
             wave_sync();
             cur = nxt;
         }
-        __syncthreads();
-        if (mode & 8) {
-            if (tid == 0) L.nspill = 0;
-            __syncthreads();
-        } else {
-            flush_spill(L, t, tid, ovf);
-        }
     }
 
-    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads)
-        if (L.blkA[b] < kOvfBlock && L.fill[b] > 0) t.sp.fills[(uint64_t)b * t.sp.region_blocks + L.blkA[b]] = L.fill[b];
+    __syncthreads();
+    unsigned long long spilled = 0;
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
+        const uint32_t k = min(L.cur[b], (uint32_t)t.sp.sub_keys);
+        t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x] = k;
+        spilled += k;
+    }
+    if (spilled) atomicAdd(&t.ctr->spilled, spilled);
     st_flush(L.T, t, tid, kThreads);
     if (ovf) atomicAdd(&t.ctr->spill_ovf, (unsigned long long)ovf);
     if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
@@ -625,14 +542,10 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t) {
     st_init(A.T, tid, kAggThreads);
     __syncthreads();
     const uint32_t b = blockIdx.x;
-    uint64_t reserved = t.sp.bcur[b];
-    if (reserved > t.sp.region_keys) reserved = t.sp.region_keys;
-    const uint64_t nblk = reserved / kSpillBlock;
-    const uint4* base = t.sp.pool + (uint64_t)b * t.sp.region_keys;
     uint64_t miss = 0;
-    for (uint64_t j = 0; j < nblk; j++) {
-        const uint32_t f = t.sp.fills[(uint64_t)b * t.sp.region_blocks + j];
-        const uint4* blk = base + j * kSpillBlock;
+    for (uint32_t g = 0; g < t.sp.nwg; g++) {
+        const uint32_t f = t.sp.counts[(uint64_t)b * t.sp.nwg + g];
+        const uint4* blk = t.sp.pool + ((uint64_t)b * t.sp.nwg + g) * t.sp.sub_keys;
         for (uint32_t i0 = tid; i0 < f; i0 += 4 * kAggThreads) {
             uint4 kk[4];
 #pragma unroll
@@ -643,7 +556,7 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t) {
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint4 k = kk[u];
-                if (k.x == 0 && k.y == 0) continue;  // past the block's fill (keys have k0 != 0)
+                if (k.x == 0 && k.y == 0) continue;  // past the stream's end (keys have k0 != 0)
                 const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
                 const uint32_t h = fold32(k.x, k.y, k.z, k.w);
                 if (!st_insert(A.T, kAggLimit, k0, k1, h, 1)) {
@@ -847,15 +760,21 @@ int map_grid_size(int device) {
 
 void clear_tables(const Tables& t, hipStream_t s) {
     hipMemsetAsync(t.ctr, 0, sizeof(Counters), s);
-    if (t.sp.bcur) hipMemsetAsync(t.sp.bcur, 0, kSpillBuckets * sizeof(unsigned long long), s);
+    if (t.sp.counts) hipMemsetAsync(t.sp.counts, 0, (size_t)kSpillBuckets * t.sp.nwg * sizeof(uint32_t), s);
     clear_tables_kernel<<<2048, 256, 0, s>>>(t);
+}
+
+uint32_t wc_map_grid(uint64_t n, int grid) {
+    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
+    if (g > (uint64_t)grid) g = (uint64_t)grid;
+    return (uint32_t)(g ? g : 1);
 }
 
 void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode, hipStream_t s) {
     const uint64_t nchunks = (n + kChunk - 1) / kChunk;
     if (nchunks == 0) return;
-    uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
-    if (g > (uint64_t)grid) g = (uint64_t)grid;
+    const uint64_t g = wc_map_grid(n, grid);
     wc_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt, (uint32_t)mode);
 }
 

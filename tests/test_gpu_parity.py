@@ -91,14 +91,14 @@ def test_wc_lds_overflow_and_table_growth(ctx):
 
 
 def test_wc_spill_region_full(ctx):
-    """Tiny spill regions: buckets overflow and their keys take the HBM-table path."""
+    """Tiny spill streams: they overflow and the rest of their keys take the HBM-table path."""
     files = cases.synthetic(C.KIND_ASCII, 1_000_000, [6_000_000], 15)
-    ctx.set_option("spill_region_blocks", 1)
+    ctx.set_option("spill_stream_keys", 8)
     try:
         check(ctx, "wc", files, nreduces=(10,))
         assert ctx.stats()["spill_ovf"] > 0
     finally:
-        ctx.set_option("spill_region_blocks", 0)
+        ctx.set_option("spill_stream_keys", 0)
 
 
 def test_wc_bucket_aggregator_overflow(ctx):
