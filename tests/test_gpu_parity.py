@@ -159,3 +159,28 @@ def test_exchange_single_rank(ctx):
     p = ctx.map(MRG_APP_WC, files[0], nreduce=4)
     q = ctx.exchange(p)
     assert ctx.reduce_all(q) == O.c_partitioned("wc", files, 4)
+
+
+def test_exchange_rccl_one_rank():
+    """The RCCL path of mrg_exchange (pack, ncclAllToAll counts, ncclAllToAllv payload,
+    unpack, re-aggregate) with a 1-rank communicator, in its own context."""
+    from mrgpu import Context
+    files = cases.synthetic(C.KIND_UTF8, 20000, [600_000], 17, 0.001)
+    with Context(0) as c2:
+        c2.comm_init(Context.unique_id(), 1, 0)
+        p = c2.map(MRG_APP_WC, files[0], nreduce=6)
+        q = c2.exchange(p)
+        assert c2.reduce_all(q) == O.c_partitioned("wc", files, 6)
+        assert c2.run_job(MRG_APP_WC, files[0], nreduce=6) == O.c_partitioned("wc", files, 6)
+
+
+def test_export_matches_host_codec(ctx):
+    """mrg_parts_export bytes decode (mrgpu.intermediate) to the oracle's word counts."""
+    import collections
+    from mrgpu import intermediate as I
+    files = cases.synthetic(C.KIND_UTF8, 20000, [300_000], 18, 0.001)
+    p = ctx.map(MRG_APP_WC, files[0], nreduce=7)
+    d = I.decode(ctx.export(p))
+    want = collections.Counter(O.mr_oracle.wc_map(files[0]))
+    assert dict(zip(d["keys"], (int(c) for c in d["count"]))) == dict(want)
+    assert all(int(pp) == O.c_ihash(k) % 7 for k, pp in zip(d["keys"], d["kpart"]))
