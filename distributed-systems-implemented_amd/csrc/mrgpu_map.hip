@@ -309,10 +309,14 @@ __device__ __forceinline__ void list_append(const Tables& t, uint64_t v) {
 template <int NSETS>
 __device__ __forceinline__ bool st_insert(STable<NSETS>& T, uint32_t limit, uint64_t k0, uint64_t k1, uint32_t h,
                                           uint32_t add) {
+    // Explicit LDS address space: through a generic (or volatile) pointer hipcc
+    // emits flat_load ... sc0 sc1 + s_waitcnt vmcnt(0), i.e. every lookup would
+    // wait for all of the wave's outstanding HBM loads and stores.
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+    typedef const __attribute__((address_space(3))) u64x2 lds_u64x2;
     const uint32_t base = __umulhi(h, NSETS) * 4;
-    const u64x2 a = *reinterpret_cast<const volatile u64x2*>(&T.k0[base]);
-    const u64x2 b = *reinterpret_cast<const volatile u64x2*>(&T.k0[base + 2]);
+    const u64x2 a = *(lds_u64x2*)(&T.k0[base]);
+    const u64x2 b = *(lds_u64x2*)(&T.k0[base + 2]);
     uint32_t m = (a.x == k0 ? 1u : 0u) | (a.y == k0 ? 2u : 0u) | (b.x == k0 ? 4u : 0u) | (b.y == k0 ? 8u : 0u);
     while (m) {  // usually one way; several only for long keys sharing their first 8 bytes
         const uint32_t slot = base + __builtin_ctz(m);
@@ -505,8 +509,15 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     const uint32_t b = spill_bucket(h);
                     const uint32_t pos = atomicAdd(&L.cur[b], 1u);
                     if (pos < t.sp.sub_keys) {
-                        t.sp.pool[my_stream0 + b * bstride + pos] =
-                            make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                        const uint4 kv = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                        uint4* dst = &t.sp.pool[my_stream0 + b * bstride + pos];
+                        if (mode & 32) acc += kv.x;
+                        else if (mode & 64) {
+                            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                            const u32x4 v = {kv.x, kv.y, kv.z, kv.w};
+                            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+                        }
+                        else *dst = kv;
                     } else {
                         short_insert(t, k0, k1, 1);
                         ovf++;
