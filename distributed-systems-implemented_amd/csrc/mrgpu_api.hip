@@ -141,6 +141,7 @@ static int ensure_spill(mrg_ctx* c, uint64_t n) {
     uint64_t sub = (n + n / 2) / 16 / ((uint64_t)kSpillBuckets * nwg) + 64;
     sub = (sub + 63) & ~63ull;
     if (c->spill_force_sub > 0) sub = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
+    if (sub * nwg >= (1ull << 32)) sub = ((1ull << 32) - 1) / nwg;  // the map kernel's stream stride is 32-bit
     c->spill_nwg = nwg;
     c->spill_sub_keys = sub;
     HCHK(c, c->spool.ensure(sub * kSpillBuckets * nwg * sizeof(uint4)));

@@ -34,10 +34,8 @@ constexpr int kWavesPerWG = 16;
 constexpr int kThreads = kWavesPerWG * kWave;
 constexpr int kListCap = kChunk / 2;              // max word starts in a chunk
 constexpr int kLdsSets = 1536;                    // map-side combiner (per workgroup): 4-way sets
-constexpr int kLdsLimit = kLdsSets * 4 * 15 / 16;
 constexpr int kAggThreads = 512;
 constexpr int kAggSets = 960;                     // bucket aggregator (half the LDS: 2 workgroups per CU)
-constexpr int kAggLimit = kAggSets * 4 * 15 / 16;
 constexpr int kGlobalProbes = 4096;
 
 struct alignas(16) WaveLds {
@@ -54,7 +52,6 @@ struct alignas(16) STable {
     unsigned long long k0[NSETS * 4];
     unsigned long long k1[NSETS * 4];
     uint32_t cnt[NSETS * 4];
-    uint32_t occ;
 };
 
 struct alignas(16) MapLds {
@@ -300,42 +297,56 @@ __device__ __forceinline__ void list_append(const Tables& t, uint64_t v) {
 }
 
 // ------------------------------------------------------------ LDS table
-// Count `add` occurrences of key (k0,k1) in a workgroup LDS table.  Returns
-// false (a miss: the caller spills or forwards the key, where it is still
-// counted exactly) when the key is absent and its set is full or the table is
-// at its occupancy limit, when the key's way is claimed but not yet published,
+// Count `add` occurrences of key (k0,k1) in a workgroup LDS table.  One probe,
+// no loop: the key is looked up in the first way of its set whose k0 matches.
+// Returns false (a miss: the caller spills or forwards the key, where it is
+// still counted exactly) when that way holds a different k1 (another key with
+// the same first 8 bytes in the same set: ~4/NSETS of such pairs), when it is
+// claimed but not yet published, when the key is absent and its set is full,
 // or when a claim CAS races — the table never waits on another lane (see
-// short_try).
+// short_try).  Kept branch-light on purpose: each divergent `if` costs a
+// handful of SALU exec-mask instructions per wave, and the map kernel is
+// issue-bound.
 template <int NSETS>
-__device__ __forceinline__ bool st_insert(STable<NSETS>& T, uint32_t limit, uint64_t k0, uint64_t k1, uint32_t h,
-                                          uint32_t add) {
+__device__ __forceinline__ bool st_lookup_add(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add,
+                                              uint32_t& base, uint32_t& empty) {
     // Explicit LDS address space: through a generic (or volatile) pointer hipcc
     // emits flat_load ... sc0 sc1 + s_waitcnt vmcnt(0), i.e. every lookup would
     // wait for all of the wave's outstanding HBM loads and stores.
     typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
     typedef const __attribute__((address_space(3))) u64x2 lds_u64x2;
-    const uint32_t base = __umulhi(h, NSETS) * 4;
+    typedef const __attribute__((address_space(3))) unsigned long long lds_u64;
+    base = __umulhi(h, NSETS) * 4;
     const u64x2 a = *(lds_u64x2*)(&T.k0[base]);
     const u64x2 b = *(lds_u64x2*)(&T.k0[base + 2]);
-    uint32_t m = (a.x == k0 ? 1u : 0u) | (a.y == k0 ? 2u : 0u) | (b.x == k0 ? 4u : 0u) | (b.y == k0 ? 8u : 0u);
-    while (m) {  // usually one way; several only for long keys sharing their first 8 bytes
-        const uint32_t slot = base + __builtin_ctz(m);
-        m &= m - 1;
-        const uint64_t v = __hip_atomic_load(&T.k1[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (v == k1) {
-            atomicAdd(&T.cnt[slot], add);
-            return true;
-        }
-        if (v == kUnwritten) return false;  // claimed, not yet published
-    }
-    const uint32_t e = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u) | (b.x == 0 ? 4u : 0u) | (b.y == 0 ? 8u : 0u);
-    if (!e || __hip_atomic_load(&T.occ, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) >= limit) return false;
-    const uint32_t slot = base + __builtin_ctz(e);
-    if (atomicCAS(&T.k0[slot], 0ull, (unsigned long long)k0) != 0ull) return false;
-    __hip_atomic_store(&T.k1[slot], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    atomicAdd(&T.cnt[slot], add);
-    atomicAdd(&T.occ, 1u);
+    const uint32_t m = (a.x == k0 ? 1u : 0u) | (a.y == k0 ? 2u : 0u) | (b.x == k0 ? 4u : 0u) | (b.y == k0 ? 8u : 0u);
+    const uint32_t z = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u) | (b.x == 0 ? 4u : 0u) | (b.y == 0 ? 8u : 0u);
+    const uint32_t slot = base + (__builtin_ctz(m | 16u) & 3u);
+    const uint64_t v = *(lds_u64*)(&T.k1[slot]);  // read unconditionally (way 0 when m == 0)
+    const bool hit = (m != 0) & (v == k1);
+    empty = m != 0 ? 0u : z;  // claimable ways, only when the key's k0 is absent from the set
+    if (hit) atomicAdd(&T.cnt[slot], add);
+    return hit;
+}
+
+// Claim the first empty way of the set for the key (after st_lookup_add found
+// its k0 absent).  False when the CAS races with another lane's claim.
+template <int NSETS>
+__device__ __forceinline__ bool st_claim(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t base, uint32_t empty,
+                                         uint32_t add) {
+    const uint32_t es = base + __builtin_ctz(empty);
+    if (atomicCAS(&T.k0[es], 0ull, (unsigned long long)k0) != 0ull) return false;
+    __hip_atomic_store(&T.k1[es], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    atomicAdd(&T.cnt[es], add);
     return true;
+}
+
+template <int NSETS>
+__device__ __forceinline__ bool st_insert(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
+    uint32_t base, empty;
+    bool ok = st_lookup_add(T, k0, k1, h, add, base, empty);
+    if (empty != 0) ok = st_claim(T, k0, k1, base, empty, add);
+    return ok;
 }
 
 template <int NSETS>
@@ -345,7 +356,6 @@ __device__ __forceinline__ void st_init(STable<NSETS>& T, uint32_t tid, uint32_t
         T.k1[i] = kUnwritten;
         T.cnt[i] = 0;
     }
-    if (tid == 0) T.occ = 0;
 }
 
 // Add every occupied way of the table to the HBM ShortTable.
@@ -405,11 +415,13 @@ __device__ __forceinline__ void stage_chunk(WaveLds& W, const ChunkRegs& r, uint
 // ------------------------------------------------------------ wc map kernel
 // Each wave walks its chunks independently (grid stride over waves, one chunk
 // prefetched ahead); the only workgroup barriers are at start and end.
+template <uint32_t mode>
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
-                                                          Tables t, LetterTables lt, uint32_t mode) {
-    // mode (benchmark ablation only; results are wrong unless 0): 1 = read input only,
-    // 16 = drop combiner misses (no spill append),
-    // 2 = tokenize only (no per-word work), 4 = per-word key extraction without the table
+                                                          Tables t, LetterTables lt) {
+    // mode (benchmark ablation only, compile-time; results are wrong unless 0):
+    // 1 = read input only, 2 = tokenize only (no per-word work), 4 = per-word key
+    // extraction without the table, 16 = drop combiner misses (no spill append),
+    // 32 = spill without the store, 64 = non-temporal spill stores
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -423,7 +435,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
     const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
     const uint64_t my_stream0 = (uint64_t)blockIdx.x * t.sp.sub_keys;  // + b*nwg*sub_keys
-    const uint64_t bstride = (uint64_t)t.sp.nwg * t.sp.sub_keys;
+    const uint32_t bstride = t.sp.nwg * (uint32_t)t.sp.sub_keys;  // < 2^32 (ensure_spill)
+    const uint32_t sub = (uint32_t)t.sp.sub_keys;
     uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
     ChunkRegs cur, nxt;
     if (c0 < nchunks) load_chunk(in, n, c0 * kChunk, lane, cur);
@@ -432,7 +445,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         {
             const uint64_t cs = c * kChunk;
             if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);  // prefetch next round
-            if (mode & 1) {
+            if constexpr ((mode & 1) != 0) {
                 acc ^= cur.a.x ^ cur.a.y ^ cur.a.z ^ cur.a.w ^ cur.h.x;
                 cur = nxt;
                 continue;
@@ -473,7 +486,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 SA &= SA - 1;
             }
             wave_sync();
-            if (mode & 2) {
+            if constexpr ((mode & 2) != 0) {
                 acc += total;
                 cur = nxt;
                 continue;
@@ -496,23 +509,25 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 const uint32_t w3 = __builtin_amdgcn_alignbyte(d4, d3, sh);
                 uint64_t k0 = ((uint64_t)w1 << 32) | w0;
                 uint64_t k1 = ((uint64_t)w3 << 32) | w2;
-                k0 &= len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1);
-                k1 &= len >= 16 ? ~0ull : (len <= 8 ? 0ull : ((1ull << (8 * (len - 8))) - 1));
+                // keep the first len bytes (1 <= len <= 16), branch-free
+                const uint32_t l1 = len > 8 ? len - 8 : 0u;
+                k0 &= len >= 8 ? ~0ull : ~(~0ull << (8 * len));
+                k1 &= l1 >= 8 ? ~0ull : ~(~0ull << (8 * l1));
                 const uint32_t h = fold32((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-                if (mode & 4) {
+                if constexpr ((mode & 4) != 0) {
                     acc += h;
                     continue;
                 }
-                const bool hit = st_insert(L.T, kLdsLimit, k0, k1, h, 1);
-                if (mode & 16) { acc += hit; continue; }
+                const bool hit = st_insert(L.T, k0, k1, h, 1);
+                if constexpr ((mode & 16) != 0) { acc += hit; continue; }
                 if (!hit) {  // append to this workgroup's stream of the key's bucket
                     const uint32_t b = spill_bucket(h);
                     const uint32_t pos = atomicAdd(&L.cur[b], 1u);
-                    if (pos < t.sp.sub_keys) {
+                    if (pos < sub) {
                         const uint4 kv = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-                        uint4* dst = &t.sp.pool[my_stream0 + b * bstride + pos];
-                        if (mode & 32) acc += kv.x;
-                        else if (mode & 64) {
+                        uint4* dst = &t.sp.pool[my_stream0 + (uint64_t)b * bstride + pos];
+                        if constexpr ((mode & 32) != 0) acc += kv.x;
+                        else if constexpr ((mode & 64) != 0) {
                             typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
                             const u32x4 v = {kv.x, kv.y, kv.z, kv.w};
                             __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
@@ -567,12 +582,13 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t) {
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint4 k = kk[u];
-                if (k.x == 0 && k.y == 0) continue;  // past the stream's end (keys have k0 != 0)
-                const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
-                const uint32_t h = fold32(k.x, k.y, k.z, k.w);
-                if (!st_insert(A.T, kAggLimit, k0, k1, h, 1)) {
-                    short_insert(t, k0, k1, 1);
-                    miss++;
+                if ((k.x | k.y) != 0) {  // else past the stream's end (keys have k0 != 0)
+                    const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
+                    const uint32_t h = fold32(k.x, k.y, k.z, k.w);
+                    if (!st_insert(A.T, k0, k1, h, 1)) {
+                        short_insert(t, k0, k1, 1);
+                        miss++;
+                    }
                 }
             }
         }
@@ -786,7 +802,13 @@ void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     const uint64_t nchunks = (n + kChunk - 1) / kChunk;
     if (nchunks == 0) return;
     const uint64_t g = wc_map_grid(n, grid);
-    wc_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt, (uint32_t)mode);
+    switch (mode) {
+#define MRG_MAP_MODE(M) \
+    case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
+        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32) MRG_MAP_MODE(64)
+#undef MRG_MAP_MODE
+        default: wc_map_kernel<0><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
+    }
 }
 
 void launch_wc_agg(const Tables& t, hipStream_t s) {
