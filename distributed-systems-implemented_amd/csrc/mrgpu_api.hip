@@ -62,7 +62,7 @@ struct mrg_ctx {
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
-    uint64_t spill_sub_keys = 0;
+    uint64_t spill_sub_keys = 0, spill_sub8 = 0, spill_amiss_cap = 0;
     uint32_t spill_nwg = 1;
     int64_t spill_force_sub = 0;
     int map_mode = 0;  // benchmark ablation of wc_map_kernel phases (0 = normal)
@@ -127,25 +127,36 @@ static Tables make_tables(mrg_ctx* c) {
     t.ctr = (Counters*)c->ctr.p;
     t.sp.pool = (uint4*)c->spool.p;
     t.sp.sub_keys = c->spill_sub_keys;
+    t.sp.sub8 = c->spill_sub8;
+    t.sp.pool8 = c->spool.p ? (uint64_t*)((uint4*)c->spool.p + c->spill_sub_keys * kSpillBuckets * c->spill_nwg)
+                            : nullptr;
     t.sp.nwg = c->spill_nwg;
     t.sp.counts = (uint32_t*)c->spmeta.p;
+    t.sp.counts8 = c->spmeta.p ? t.sp.counts + (size_t)kSpillBuckets * c->spill_nwg : nullptr;
+    t.sp.amiss = c->spool.p ? (uint4*)(t.sp.pool8 + c->spill_sub8 * kSpillBuckets * c->spill_nwg) : nullptr;
+    t.sp.amiss_cap = (uint32_t)c->spill_amiss_cap;
     return t;
 }
 
 // Spill pool for LDS-combiner misses: 1.5 bytes of pool per input byte (C2
-// spills ~1 byte of keys per input byte), split into kSpillBuckets x nwg
-// streams.  A stream that fills up sends the rest of its keys to the HBM
-// table, so the size only affects speed, never results.
+// spills ~0.5 bytes of records per input byte), split into kSpillBuckets x nwg
+// streams of 16-byte records (0.75 B/B) and as many of 8-byte records (0.75 B/B).
+// A stream that fills up sends the rest of its keys to the HBM table, so the
+// size only affects speed, never results.
 static int ensure_spill(mrg_ctx* c, uint64_t n) {
     const uint32_t nwg = wc_map_grid(n, c->grid);
-    uint64_t sub = (n + n / 2) / 16 / ((uint64_t)kSpillBuckets * nwg) + 64;
+    uint64_t sub = (n - n / 4) / 16 / ((uint64_t)kSpillBuckets * nwg) + 64;
     sub = (sub + 63) & ~63ull;
-    if (c->spill_force_sub > 0) sub = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
-    if (sub * nwg >= (1ull << 32)) sub = ((1ull << 32) - 1) / nwg;  // the map kernel's stream stride is 32-bit
+    uint64_t sub8 = 2 * sub;
+    if (c->spill_force_sub > 0) sub = sub8 = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
+    if (sub8 * nwg >= (1ull << 32)) sub = sub8 = ((1ull << 32) - 1) / nwg;  // the map kernel's stream stride is 32-bit
     c->spill_nwg = nwg;
     c->spill_sub_keys = sub;
-    HCHK(c, c->spool.ensure(sub * kSpillBuckets * nwg * sizeof(uint4)));
-    HCHK(c, c->spmeta.ensure((size_t)kSpillBuckets * nwg * sizeof(uint32_t)));
+    c->spill_sub8 = sub8;
+    c->spill_amiss_cap = c->spill_force_sub > 0 ? sub : 8 * sub;  // per bucket; beyond it misses insert inline
+    HCHK(c, c->spool.ensure((sub * sizeof(uint4) + sub8 * sizeof(uint64_t)) * kSpillBuckets * nwg +
+                            c->spill_amiss_cap * sizeof(uint4) * kSpillBuckets));
+    HCHK(c, c->spmeta.ensure((size_t)2 * kSpillBuckets * nwg * sizeof(uint32_t)));
     return MRG_OK;
 }
 
@@ -396,7 +407,7 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         if (app == MRG_APP_WC) {
             launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s);
             HCHK(c, hipEventRecord(c->ev[1], c->s));
-            launch_wc_agg(t, c->s);
+            launch_wc_agg(t, c->map_mode, c->s);
             HCHK(c, hipEventRecord(c->ev[8], c->s));
         } else if (!grep_nl) {
             if (plen) launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);

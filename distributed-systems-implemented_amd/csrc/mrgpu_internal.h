@@ -62,10 +62,17 @@ struct Counters {
 // an LDS cursor (no HBM atomics, no barriers) and records the stream length in
 // counts[b*nwg + g].  Keys beyond sub_keys go to the HBM table instead.
 constexpr int kSpillBuckets = 512;
+// Keys of at most 8 bytes (k1 == 0) are spilled as 8-byte records into pool8,
+// longer ones as 16-byte records into pool: the combiner's misses are mostly
+// tail words, and most words are short, so this roughly halves spill traffic.
 struct Spill {
-    uint4* pool;
-    uint64_t sub_keys;
-    uint32_t* counts;                // [kSpillBuckets * nwg]
+    uint4* pool;                     // [kSpillBuckets][nwg][sub_keys] 16-byte records (k0, k1)
+    uint64_t* pool8;                 // [kSpillBuckets][nwg][sub8] 8-byte records (k0; k1 == 0)
+    uint64_t sub_keys, sub8;         // stream capacities (records)
+    uint32_t* counts;                // [kSpillBuckets * nwg] records in each 16-byte stream
+    uint32_t* counts8;               // [kSpillBuckets * nwg] records in each 8-byte stream
+    uint4* amiss;                    // [kSpillBuckets][amiss_cap] aggregator misses, inserted after its loop
+    uint32_t amiss_cap;
     uint32_t nwg;
 };
 
@@ -101,7 +108,7 @@ struct LetterTables {
 void clear_tables(const Tables& t, hipStream_t s);
 void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode,
                    hipStream_t s);
-void launch_wc_agg(const Tables& t, hipStream_t s);
+void launch_wc_agg(const Tables& t, int mode, hipStream_t s);
 uint32_t wc_map_grid(uint64_t n, int grid);
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,

@@ -57,11 +57,13 @@ struct alignas(16) STable {
 struct alignas(16) MapLds {
     WaveLds w[kWavesPerWG];
     STable<kLdsSets> T;
-    uint32_t cur[kSpillBuckets];     // keys appended to this workgroup's stream of each bucket
+    uint32_t cur[kSpillBuckets];     // records appended to this workgroup's 16-byte stream of each bucket
+    uint32_t cur8[kSpillBuckets];    // ... and to its 8-byte stream
 };
 
 struct alignas(16) AggLds {
     STable<kAggSets> T;
+    uint32_t nmiss;  // keys appended to the bucket's miss list
 };
 
 // ---------------------------------------------------------------- helpers
@@ -309,7 +311,7 @@ __device__ __forceinline__ void list_append(const Tables& t, uint64_t v) {
 // issue-bound.
 template <int NSETS>
 __device__ __forceinline__ bool st_lookup_add(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add,
-                                              uint32_t& base, uint32_t& empty) {
+                                              uint32_t& base, uint32_t& empty, uint32_t& m_out) {
     // Explicit LDS address space: through a generic (or volatile) pointer hipcc
     // emits flat_load ... sc0 sc1 + s_waitcnt vmcnt(0), i.e. every lookup would
     // wait for all of the wave's outstanding HBM loads and stores.
@@ -325,6 +327,7 @@ __device__ __forceinline__ bool st_lookup_add(STable<NSETS>& T, uint64_t k0, uin
     const uint64_t v = *(lds_u64*)(&T.k1[slot]);  // read unconditionally (way 0 when m == 0)
     const bool hit = (m != 0) & (v == k1);
     empty = m != 0 ? 0u : z;  // claimable ways, only when the key's k0 is absent from the set
+    m_out = m | (z << 4);     // 0: the key's k0 is absent and the set is full
     if (hit) atomicAdd(&T.cnt[slot], add);
     return hit;
 }
@@ -343,9 +346,27 @@ __device__ __forceinline__ bool st_claim(STable<NSETS>& T, uint64_t k0, uint64_t
 
 template <int NSETS>
 __device__ __forceinline__ bool st_insert(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
-    uint32_t base, empty;
-    bool ok = st_lookup_add(T, k0, k1, h, add, base, empty);
+    uint32_t base, empty, m;
+    bool ok = st_lookup_add(T, k0, k1, h, add, base, empty, m);
     if (empty != 0) ok = st_claim(T, k0, k1, base, empty, add);
+    return ok;
+}
+
+// Two-choice variant (bucket aggregator, whose table is about half full): a
+// key whose first set is full and does not hold its k0 lives in a second set.
+// Ways are never freed, so once the first set is full a key absent from it can
+// never appear there later — lookups and claims agree on the key's set.
+template <int NSETS>
+__device__ __forceinline__ bool st_insert2(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
+    uint32_t base, empty, m;
+    bool ok = st_lookup_add(T, k0, k1, h, add, base, empty, m);
+    if (empty != 0) {
+        ok = st_claim(T, k0, k1, base, empty, add);
+    } else if (m == 0) {  // first set full, key absent
+        const uint32_t h2 = __builtin_amdgcn_alignbit(h, h, 16) * 0xC2B2AE3Du;
+        ok = st_lookup_add(T, k0, k1, h2, add, base, empty, m);
+        if (empty != 0) ok = st_claim(T, k0, k1, base, empty, add);
+    }
     return ok;
 }
 
@@ -421,7 +442,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
     // 1 = read input only, 2 = tokenize only (no per-word work), 4 = per-word key
     // extraction without the table, 16 = drop combiner misses (no spill append),
-    // 32 = spill without the store, 64 = non-temporal spill stores
+    // 32 = spill without the store
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -429,14 +450,16 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     WaveLds& W = L.w[wv];
 
     st_init(L.T, tid, kThreads);
-    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) L.cur[b] = 0;
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) L.cur[b] = L.cur8[b] = 0;
     __syncthreads();
 
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
     const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
     const uint64_t my_stream0 = (uint64_t)blockIdx.x * t.sp.sub_keys;  // + b*nwg*sub_keys
+    const uint64_t my_stream8 = (uint64_t)blockIdx.x * t.sp.sub8;
     const uint32_t bstride = t.sp.nwg * (uint32_t)t.sp.sub_keys;  // < 2^32 (ensure_spill)
-    const uint32_t sub = (uint32_t)t.sp.sub_keys;
+    const uint32_t bstride8 = t.sp.nwg * (uint32_t)t.sp.sub8;
+    const uint32_t sub = (uint32_t)t.sp.sub_keys, sub8 = (uint32_t)t.sp.sub8;
     uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
     ChunkRegs cur, nxt;
     if (c0 < nchunks) load_chunk(in, n, c0 * kChunk, lane, cur);
@@ -522,17 +545,13 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 if constexpr ((mode & 16) != 0) { acc += hit; continue; }
                 if (!hit) {  // append to this workgroup's stream of the key's bucket
                     const uint32_t b = spill_bucket(h);
-                    const uint32_t pos = atomicAdd(&L.cur[b], 1u);
-                    if (pos < sub) {
-                        const uint4 kv = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-                        uint4* dst = &t.sp.pool[my_stream0 + (uint64_t)b * bstride + pos];
-                        if constexpr ((mode & 32) != 0) acc += kv.x;
-                        else if constexpr ((mode & 64) != 0) {
-                            typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-                            const u32x4 v = {kv.x, kv.y, kv.z, kv.w};
-                            __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
-                        }
-                        else *dst = kv;
+                    const bool small = k1 == 0;  // key of at most 8 bytes: 8-byte record
+                    const uint32_t pos = atomicAdd(small ? &L.cur8[b] : &L.cur[b], 1u);
+                    if (pos < (small ? sub8 : sub)) {
+                        if constexpr ((mode & 32) != 0) acc += (uint32_t)k0;
+                        else if (small) t.sp.pool8[my_stream8 + (uint64_t)b * bstride8 + pos] = k0;
+                        else t.sp.pool[my_stream0 + (uint64_t)b * bstride + pos] =
+                            make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
                     } else {
                         short_insert(t, k0, k1, 1);
                         ovf++;
@@ -547,9 +566,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     __syncthreads();
     unsigned long long spilled = 0;
     for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
-        const uint32_t k = min(L.cur[b], (uint32_t)t.sp.sub_keys);
+        const uint32_t k = min(L.cur[b], sub), k8 = min(L.cur8[b], sub8);
         t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x] = k;
-        spilled += k;
+        t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x] = k8;
+        spilled += k + k8;
     }
     if (spilled) atomicAdd(&t.ctr->spilled, spilled);
     st_flush(L.T, t, tid, kThreads);
@@ -559,43 +579,92 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 }
 
 // Bucket aggregation: one workgroup per spill bucket counts its keys in an LDS
-// table (a bucket holds ~1/256 of the distinct spilled keys), then adds the
+// table (a bucket holds ~1/512 of the distinct spilled keys), then adds the
 // per-key totals to the HBM ShortTable — one HBM atomic per distinct key per
-// bucket instead of one per occurrence.
+// bucket instead of one per occurrence.  The bucket's nwg streams (one per map
+// workgroup) are walked as one sequence of kAggGroup-record groups with the
+// next group's loads in flight while the current one is inserted.
+constexpr uint32_t kAggUnroll = 4;
+constexpr uint32_t kAggGroup = kAggUnroll * kAggThreads;
+
+__device__ __forceinline__ void agg_load(const uint4* blk, uint32_t i, uint32_t f, uint4& r) {
+    r = i < f ? blk[i] : make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void agg_load(const uint64_t* blk, uint32_t i, uint32_t f, uint4& r) {
+    const uint64_t k = i < f ? blk[i] : 0;
+    r = make_uint4((uint32_t)k, (uint32_t)(k >> 32), 0, 0);
+}
+
+template <uint32_t amode, typename Rec>
+__device__ __forceinline__ void agg_streams(AggLds& A, const Tables& t, const Rec* pool, const uint32_t* counts,
+                                            uint64_t sub, uint64_t& miss) {
+    const uint32_t nwg = t.sp.nwg, tid = threadIdx.x;
+    // (g, base, f): current stream, first record of the group, records in the stream
+    uint32_t g = 0, base = 0, f = nwg ? counts[0] : 0;
+    while (g < nwg && base >= f) { g++; f = g < nwg ? counts[g] : 0; }
+    uint4 cur[kAggUnroll], nxt[kAggUnroll];
+    if (g < nwg) {
+#pragma unroll
+        for (uint32_t u = 0; u < kAggUnroll; u++) agg_load(pool + (uint64_t)g * sub, base + u * kAggThreads + tid, f, cur[u]);
+    }
+    while (g < nwg) {
+        uint32_t g2 = g, base2 = base + kAggGroup, f2 = f;
+        while (g2 < nwg && base2 >= f2) { g2++; base2 = 0; f2 = g2 < nwg ? counts[g2] : 0; }
+        if (g2 < nwg) {
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++)
+                agg_load(pool + (uint64_t)g2 * sub, base2 + u * kAggThreads + tid, f2, nxt[u]);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kAggUnroll; u++) {
+            const uint4 k = cur[u];
+            if ((k.x | k.y) != 0) {  // else past the stream's end (keys have k0 != 0)
+                const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
+                const uint32_t h = fold32(k.x, k.y, k.z, k.w);
+                if constexpr ((amode & 128) != 0) {
+                    miss += h;
+                } else if constexpr ((amode & 256) != 0) {
+                    uint32_t base, empty, mm;
+                    miss += st_lookup_add(A.T, k0, k1, h, 0, base, empty, mm) + empty;
+                } else if (!st_insert2(A.T, k0, k1, h, 1)) {
+                    const uint32_t pos = atomicAdd(&A.nmiss, 1u);  // defer: no HBM round trip in the loop
+                    if (pos < t.sp.amiss_cap)
+                        t.sp.amiss[(uint64_t)blockIdx.x * t.sp.amiss_cap + pos] =
+                            make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                    else
+                        short_insert(t, k0, k1, 1);
+                    miss++;
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kAggUnroll; u++) cur[u] = nxt[u];
+        g = g2; base = base2; f = f2;
+    }
+}
+
+// amode (benchmark ablation only, compile-time; results are wrong unless 0):
+// 128 = read + hash the records only, 256 = table lookups without adds/claims
+template <uint32_t amode>
 __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t) {
     __shared__ AggLds A;
     const uint32_t tid = threadIdx.x;
     st_init(A.T, tid, kAggThreads);
+    if (tid == 0) A.nmiss = 0;
     __syncthreads();
-    const uint32_t b = blockIdx.x;
+    const uint64_t b = blockIdx.x;
     uint64_t miss = 0;
-    for (uint32_t g = 0; g < t.sp.nwg; g++) {
-        const uint32_t f = t.sp.counts[(uint64_t)b * t.sp.nwg + g];
-        const uint4* blk = t.sp.pool + ((uint64_t)b * t.sp.nwg + g) * t.sp.sub_keys;
-        for (uint32_t i0 = tid; i0 < f; i0 += 4 * kAggThreads) {
-            uint4 kk[4];
-#pragma unroll
-            for (int u = 0; u < 4; u++) {  // issue the 4 loads before any insert
-                const uint32_t i = i0 + u * kAggThreads;
-                kk[u] = i < f ? blk[i] : make_uint4(0, 0, 0, 0);
-            }
-#pragma unroll
-            for (int u = 0; u < 4; u++) {
-                const uint4 k = kk[u];
-                if ((k.x | k.y) != 0) {  // else past the stream's end (keys have k0 != 0)
-                    const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
-                    const uint32_t h = fold32(k.x, k.y, k.z, k.w);
-                    if (!st_insert(A.T, k0, k1, h, 1)) {
-                        short_insert(t, k0, k1, 1);
-                        miss++;
-                    }
-                }
-            }
-        }
-    }
+    agg_streams<amode>(A, t, t.sp.pool8 + b * t.sp.nwg * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg, t.sp.sub8, miss);
+    agg_streams<amode>(A, t, t.sp.pool + b * t.sp.nwg * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg, t.sp.sub_keys, miss);
     __syncthreads();
     st_flush(A.T, t, tid, kAggThreads);
-    if (miss) atomicAdd(&t.ctr->agg_miss, (unsigned long long)miss);
+    const uint32_t nm = min(A.nmiss, t.sp.amiss_cap);
+    for (uint32_t i = tid; i < nm; i += kAggThreads) {  // deferred misses, all lanes in flight
+        const uint4 k = t.sp.amiss[b * t.sp.amiss_cap + i];
+        short_insert(t, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, 1);
+    }
+    if (amode != 0 && miss == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // no DCE in ablation builds
+    else if (amode == 0 && miss) atomicAdd(&t.ctr->agg_miss, (unsigned long long)miss);
 }
 
 // Words longer than 16 bytes: decode forward from the start (one lane per word).
@@ -787,7 +856,7 @@ int map_grid_size(int device) {
 
 void clear_tables(const Tables& t, hipStream_t s) {
     hipMemsetAsync(t.ctr, 0, sizeof(Counters), s);
-    if (t.sp.counts) hipMemsetAsync(t.sp.counts, 0, (size_t)kSpillBuckets * t.sp.nwg * sizeof(uint32_t), s);
+    if (t.sp.counts) hipMemsetAsync(t.sp.counts, 0, (size_t)2 * kSpillBuckets * t.sp.nwg * sizeof(uint32_t), s);
     clear_tables_kernel<<<2048, 256, 0, s>>>(t);
 }
 
@@ -805,14 +874,16 @@ void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     switch (mode) {
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
-        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32) MRG_MAP_MODE(64)
+        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32)
 #undef MRG_MAP_MODE
         default: wc_map_kernel<0><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
     }
 }
 
-void launch_wc_agg(const Tables& t, hipStream_t s) {
-    wc_agg_kernel<<<kSpillBuckets, kAggThreads, 0, s>>>(t);
+void launch_wc_agg(const Tables& t, int mode, hipStream_t s) {
+    if (mode & 128) wc_agg_kernel<128><<<kSpillBuckets, kAggThreads, 0, s>>>(t);
+    else if (mode & 256) wc_agg_kernel<256><<<kSpillBuckets, kAggThreads, 0, s>>>(t);
+    else wc_agg_kernel<0><<<kSpillBuckets, kAggThreads, 0, s>>>(t);
 }
 
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s) {
