@@ -244,9 +244,11 @@ def main():
                          "note": "achieved = input bytes per launch / mean HIP-event duration of wc_map_kernel on "
                                  "the library stream over the timed steps"},
             "phases_ms": {"map_kernel": round(avg_kern, 3), "map_total": round(last["map_total_ms"], 3),
+                          "dict": round(last["dict_ms"], 3), "agg": round(last["agg_ms"], 3),
                           "exchange": round(last["exchange_ms"], 3), "reduce": round(last["reduce_ms"], 3),
                           "d2h": round(last["d2h_ms"], 3)},
             "distinct_keys": int(last["distinct_keys"]),
+            "dict_hit_words": int(last["dict_hits"]),
             "spilled_words": int(last["lds_overflow"]),
             "spill_region_full_words": int(last["spill_ovf"]),
             "aggregator_miss_words": int(last["agg_miss"]),

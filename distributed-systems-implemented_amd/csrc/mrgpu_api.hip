@@ -1,13 +1,15 @@
 // mrgpu_api.hip — the C ABI (include/mrgpu.h): contexts, map/reduce
 // orchestration, intermediate export/import and the RCCL shuffle.
 //
-// Call flow of mrg_map (replaces mr/worker.go:58-92 for a known app):
-//   [H2D copy of the split if host-resident] -> clear HBM tables ->
-//   wc_map_kernel (tokenize + LDS combine + HBM table) -> wc_long_kernel ->
-//   collect (distinct keys -> records, partition = ihash % nReduce).
-// If a table or list overflowed (the status word says which), the capacity is
-// multiplied by 4 and the map is re-run, so results never depend on the
-// initial sizing.
+// Call flow of mrg_map for wc (replaces mr/worker.go:58-92 + mrapps/wc.go):
+//   [H2D copy of the split if host-resident] -> hot-key dictionary from a
+//   sample (mrgpu_wc.hip stage 0) -> wc_map_kernel -> wc_agg_kernel (direct
+//   records) + dict_emit_kernel -> wc_long_kernel -> collect of whatever went
+//   through the HBM tables -> records (partition = ihash % nReduce).
+// grep: grep_map_kernel -> grep_lines_kernel (LongTable) -> collect.
+// If a table, list or the record buffer overflowed (the status word says
+// which), the capacity grows and the map is re-run, so results never depend on
+// the initial sizing.
 #include <rccl/rccl.h>
 
 #include <algorithm>
@@ -57,11 +59,18 @@ constexpr uint64_t kHostMagic = 0x4D524748424F5354ull;  // "MRGHBOST"
 struct mrg_ctx {
     int device = 0;
     hipStream_t s = nullptr;
-    hipEvent_t ev[12] = {};
+    hipEvent_t ev[12] = {};  // 0-3, 8-10: map phases; 4-5 reduce; 6-7 exchange / d2h
     std::string err;
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
+    DevBuf bflag, dict, dict_cnt, sample, recbuf, recarena, sortbuf, dbg;
+    bool debug_times = getenv("MRG_DEBUG_TIMES") != nullptr;
+    uint64_t rec_cap = 1u << 21;       // record output buffer capacity (grows on overflow)
+    bool sh_clean = false;             // ShortTable known to be empty (skip its clear)
+    int dict_mode = 0;                 // <0: never build the hot-key dictionary
+    uint64_t dict_min_bytes = 32ull << 20;
+    uint64_t dict_sample_bytes = 64ull << 20;
     uint64_t spill_sub_keys = 0, spill_sub8 = 0, spill_amiss_cap = 0;
     uint32_t spill_nwg = 1;
     int64_t spill_force_sub = 0;
@@ -135,7 +144,31 @@ static Tables make_tables(mrg_ctx* c) {
     t.sp.counts8 = c->spmeta.p ? t.sp.counts + (size_t)kSpillBuckets * c->spill_nwg : nullptr;
     t.sp.amiss = c->spool.p ? (uint4*)(t.sp.pool8 + c->spill_sub8 * kSpillBuckets * c->spill_nwg) : nullptr;
     t.sp.amiss_cap = (uint32_t)c->spill_amiss_cap;
+    t.out = Recs{};
+    t.out_cap = 0;
+    t.nreduce = 1;
+    t.bflag = (uint32_t*)c->bflag.p;
+    t.dict = nullptr;
+    t.dict_cnt = (uint32_t*)c->dict_cnt.p;
+    t.dbg = c->debug_times && c->dbg.ensure(2 * kMaxMapWGs * 8 * 4) == hipSuccess ? (unsigned long long*)c->dbg.p : nullptr;
     return t;
+}
+
+// SoA view of the context's record output buffer (capacity rec_cap).
+static Recs rec_view(mrg_ctx* c) {
+    Recs r{};
+    const uint64_t cap = c->rec_cap;
+    char* b = (char*)c->recbuf.p;
+    r.k0 = (uint64_t*)b; b += cap * 8;
+    r.k1 = (uint64_t*)b; b += cap * 8;
+    r.cnt = (uint64_t*)b; b += cap * 8;
+    r.koff = (uint64_t*)b; b += cap * 8;
+    r.len = (uint32_t*)b; b += cap * 4;
+    r.part = (uint32_t*)b;
+    r.arena = (uint8_t*)c->recarena.p;
+    r.arena_n = c->recarena.cap;
+    r.n = 0;
+    return r;
 }
 
 // Spill pool for LDS-combiner misses: 1.5 bytes of pool per input byte (C2
@@ -149,7 +182,7 @@ static int ensure_spill(mrg_ctx* c, uint64_t n) {
     sub = (sub + 63) & ~63ull;
     uint64_t sub8 = 2 * sub;
     if (c->spill_force_sub > 0) sub = sub8 = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
-    if (sub8 * nwg >= (1ull << 32)) sub = sub8 = ((1ull << 32) - 1) / nwg;  // the map kernel's stream stride is 32-bit
+    if (sub8 >= (1ull << 31)) sub = sub8 = (1ull << 31);  // in-stream positions are 32-bit
     c->spill_nwg = nwg;
     c->spill_sub_keys = sub;
     c->spill_sub8 = sub8;
@@ -161,7 +194,10 @@ static int ensure_spill(mrg_ctx* c, uint64_t n) {
 }
 
 static int ensure_tables(mrg_ctx* c) {
+    const void* old = c->sh.p;
     HCHK(c, c->sh.ensure(sizeof(ShortSlot) << c->sh_log2));
+    if (c->sh.p != old) c->sh_clean = false;  // fresh memory is not zeroed
+    HCHK(c, c->bflag.ensure(kSpillBuckets * sizeof(uint32_t)));
     HCHK(c, c->lo.ensure(sizeof(LongSlot) << c->lo_log2));
     HCHK(c, c->list.ensure(c->list_cap * sizeof(uint64_t)));
     HCHK(c, c->ctr.ensure(sizeof(Counters)));
@@ -171,7 +207,14 @@ static int ensure_tables(mrg_ctx* c) {
 static int read_counters(mrg_ctx* c) {
     HCHK(c, hipMemcpyAsync(c->h_ctr, c->ctr.p, sizeof(Counters), hipMemcpyDeviceToHost, c->s));
     HCHK(c, hipStreamSynchronize(c->s));
+    if (c->h_ctr->short_used) c->sh_clean = false;
     return MRG_OK;
+}
+
+// Reset the counters (and the ShortTable unless it is known to be empty).
+static void clear_for_run(mrg_ctx* c, const Tables& t) {
+    clear_tables(t, !c->sh_clean, c->s);
+    c->sh_clean = true;
 }
 
 static float ev_ms(hipEvent_t a, hipEvent_t b) {
@@ -216,12 +259,16 @@ static int collect_parts(mrg_ctx* c, int app, uint32_t nreduce, mrg_parts** out)
     mrg_parts* p = nullptr;
     if ((rc = parts_alloc(c, n, arena, app, nreduce, &p))) return rc;
     Tables t = make_tables(c);
+    t.out = p->r;
+    t.out_cap = n;
+    t.nreduce = nreduce;
+    const bool sh_used = h.short_used != 0, lo_used = h.long_used != 0;
     HCHK(c, hipMemsetAsync(&t.ctr->nrec, 0, 3 * sizeof(unsigned long long), c->s));
-    launch_collect(t, p->r, nreduce, c->s);
-    HCHK(c, hipGetLastError());
+    if (launch_collect(t, c->rws, 0, sh_used ? h.short_used : 0, lo_used, c->s))
+        return fail(c, MRG_EDEVICE, "collect failed");
     rc = read_counters(c);
     if (rc) { mrg_parts_free(p); return rc; }
-    if (h.nrec != n || h.arena != arena) {
+    if (h.nrec != n || h.arena != arena || (h.status & kStRecFull)) {
         mrg_parts_free(p);
         return fail(c, MRG_EDEVICE, "collect mismatch: %llu/%llu records, %llu/%llu arena bytes", h.nrec,
                     (unsigned long long)n, h.arena, (unsigned long long)arena);
@@ -238,7 +285,203 @@ static int grow_on_overflow(mrg_ctx* c, uint32_t st) {
     if (st & kStShortFull) { c->sh_log2 += 2; again = 1; }
     if (st & kStLongFull) { c->lo_log2 += 2; again = 1; }
     if (st & kStListFull) { c->list_cap = std::max<uint64_t>(c->list_cap * 4, c->h_ctr->nlist + 1024); again = 1; }
+    if (st & kStRecFull) { c->rec_cap = std::max<uint64_t>(c->rec_cap * 2, c->h_ctr->nrec + 4096); again = 1; }
     return again;
+}
+
+static int ensure_recbuf(mrg_ctx* c) {
+    HCHK(c, c->recbuf.ensure(c->rec_cap * 40));
+    return MRG_OK;
+}
+
+// Diagnostics: distribution of per-workgroup start/end stamps (100 MHz) of the
+// last aggregation kernel, relative to the earliest start.
+static void print_stamps(mrg_ctx* c, const char* what, uint32_t nblocks, uint32_t off = 0) {
+    if (!c->debug_times || !c->dbg.p) return;
+    std::vector<unsigned long long> h(2 * nblocks);
+    hipStreamSynchronize(c->s);
+    hipMemcpy(h.data(), (unsigned long long*)c->dbg.p + 2 * off, h.size() * 8, hipMemcpyDeviceToHost);
+    unsigned long long t0 = ~0ull, s_max = 0, e_min = ~0ull, e_max = 0;
+    for (uint32_t b = 0; b < nblocks; b++) t0 = std::min(t0, h[2 * b]);
+    std::vector<double> st, en;
+    for (uint32_t b = 0; b < nblocks; b++) {
+        s_max = std::max(s_max, h[2 * b] - t0);
+        e_min = std::min(e_min, h[2 * b + 1] - t0);
+        e_max = std::max(e_max, h[2 * b + 1] - t0);
+    }
+    std::vector<std::pair<unsigned long long, uint32_t>> ends;
+    for (uint32_t b = 0; b < nblocks; b++) ends.push_back({h[2 * b + 1] - t0, b});
+    std::sort(ends.begin(), ends.end());
+    fprintf(stderr, "[mrg stamps] %s: last start %.1f us, end p0 %.1f p50 %.1f p90 %.1f p100 %.1f us; slowest:", what,
+            s_max / 100.0, e_min / 100.0, ends[nblocks / 2].first / 100.0, ends[nblocks * 9 / 10].first / 100.0,
+            e_max / 100.0);
+    for (uint32_t k = 0; k < 5 && k < nblocks; k++) fprintf(stderr, " %u", ends[nblocks - 1 - k].second);
+    fprintf(stderr, "\n");
+    if (off == 0 && c->spmeta.p) {  // bucket sizes (aggregator stamps)
+        const uint32_t nwg = c->spill_nwg;
+        std::vector<uint32_t> cnt((size_t)2 * kSpillBuckets * nwg);
+        hipMemcpy(cnt.data(), c->spmeta.p, cnt.size() * 4, hipMemcpyDeviceToHost);
+        std::vector<uint64_t> tot(kSpillBuckets, 0);
+        for (uint32_t b = 0; b < kSpillBuckets; b++)
+            for (uint32_t g = 0; g < nwg; g++) tot[b] += cnt[(size_t)b * nwg + g] + cnt[(size_t)(kSpillBuckets + b) * nwg + g];
+        std::vector<uint64_t> so(tot);
+        std::sort(so.begin(), so.end());
+        fprintf(stderr, "[mrg stamps]   bucket records min %llu p50 %llu max %llu; slowest buckets' records:",
+                (unsigned long long)so[0], (unsigned long long)so[kSpillBuckets / 2], (unsigned long long)so.back());
+        for (uint32_t k = 0; k < 5; k++) fprintf(stderr, " %llu", (unsigned long long)tot[ends[nblocks - 1 - k].second]);
+        fprintf(stderr, "\n");
+    }
+}
+
+// Stage 0 of the wc pipeline (mrgpu_wc.hip): the hottest keys of an evenly
+// spaced sample of the split -> the dictionary image in c->dict.  Two levels:
+// a small sample mapped with no dictionary (every word spills, so the hottest
+// words crowd a few buckets — cheap only because the sample is small) gives a
+// first dictionary; the full sample is then mapped WITH it, so only its tail
+// spills, evenly over the buckets; its dictionary hits and aggregated tail
+// become the records the final dictionary is built from.  Only speed depends
+// on the dictionary: every key it misses is counted exactly through the spill.
+static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win, uint32_t nwin, LetterTables lt,
+                       bool with_dict, uint64_t* nrec_out) {
+    const uint64_t stride = ((len - win) / nwin) & ~15ull;
+    const uint64_t sn = (uint64_t)nwin * (win + 16);
+    HCHK(c, c->sample.ensure(sn + 64));
+    launch_sample_gather(in, len, win, stride, nwin, (uint8_t*)c->sample.p, c->s);
+    int rc;
+    if ((rc = ensure_tables(c)) || (rc = ensure_recbuf(c))) return rc;
+    Tables t = make_tables(c);
+    t.out = rec_view(c);
+    t.out_cap = c->rec_cap;
+    t.dict = with_dict ? (const uint4*)c->dict.p : nullptr;
+    clear_for_run(c, t);
+    // the spill layout was sized for the split's workgroup count (ensure_spill): never launch more
+    const uint32_t g = wc_map_grid(sn, (int)c->spill_nwg);
+    launch_wc_map((const uint8_t*)c->sample.p, sn, t, lt, (int)g, 0, c->s);
+    launch_wc_agg(t, c->map_mode & 512, 2, c->s);
+    if (with_dict) launch_dict_emit(t, g, c->s);
+    HCHK(c, hipGetLastError());
+    print_stamps(c, with_dict ? "sample agg (level 2)" : "sample agg (level 1)", kSpillBuckets);
+    if ((rc = read_counters(c))) return rc;
+    *nrec_out = std::min<uint64_t>(c->h_ctr->nrec, c->rec_cap);
+    return MRG_OK;
+}
+
+// Dictionary image from the nrec records in the record buffer (descending count).
+static int dict_from_recs(mrg_ctx* c, uint64_t nrec) {
+    HCHK(c, c->sortbuf.ensure(nrec * 16 + 64));
+    uint32_t* keys = (uint32_t*)c->sortbuf.p;
+    uint32_t* keys2 = keys + nrec;
+    uint32_t* idx = keys2 + nrec;
+    uint32_t* idx2 = idx + nrec;
+    Recs r = rec_view(c);
+    r.n = nrec;
+    launch_dict_keys(r, keys, idx, c->s);
+    if (sort_u32_pairs(c->rws, keys, keys2, idx, idx2, nrec, c->s)) return fail(c, MRG_EDEVICE, "dictionary sort failed");
+    launch_dict_build(r, idx2, nrec, (uint4*)c->dict.p, c->s);
+    HCHK(c, hipGetLastError());
+    return MRG_OK;
+}
+
+static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables lt, bool* have) {
+    *have = false;
+    uint64_t win = 256u << 10;
+    if (len < 2 * win) win = (len / 2) & ~15ull;
+    if (win < 4096) return MRG_OK;
+    HCHK(c, c->dict.ensure(sizeof(uint4) * kDictSets));
+    const uint64_t target = std::min<uint64_t>(c->dict_sample_bytes, std::max<uint64_t>(len / 64, 4u << 20));
+    const uint64_t small = std::min<uint64_t>(target, 2u << 20);
+    int rc;
+    uint64_t nrec = 0;
+    if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, small / win), lt, false, &nrec))) return rc;
+    if (nrec == 0) return MRG_OK;
+    if ((rc = dict_from_recs(c, nrec))) return rc;
+    if (target > small) {
+        if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, target / win), lt, true, &nrec))) return rc;
+        if (nrec && (rc = dict_from_recs(c, nrec))) return rc;
+    }
+    c->stats.dict_keys = nrec;
+    *have = true;
+    return MRG_OK;
+}
+
+// wc: dictionary, map, bucket aggregation, dictionary records, long words, collect.
+static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce, LetterTables lt, mrg_parts** out) {
+    int rc;
+    if ((rc = ensure_spill(c, len))) return rc;
+    const uint32_t nwg = c->spill_nwg;
+    HCHK(c, c->dict_cnt.ensure((size_t)nwg * kDictSlots * sizeof(uint32_t)));
+    HCHK(c, hipEventRecord(c->ev[9], c->s));
+    bool have_dict = false;
+    if (c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict))) return rc;
+    HCHK(c, hipEventRecord(c->ev[10], c->s));
+    for (int attempt = 0; attempt < 8; attempt++) {
+        if ((rc = ensure_tables(c)) || (rc = ensure_recbuf(c))) return rc;
+        Tables t = make_tables(c);
+        t.dict = have_dict ? (const uint4*)c->dict.p : nullptr;
+        t.nreduce = nreduce;
+        t.out = rec_view(c);
+        t.out_cap = c->rec_cap;
+        clear_for_run(c, t);
+        HCHK(c, hipEventRecord(c->ev[0], c->s));
+        launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s);
+        HCHK(c, hipEventRecord(c->ev[1], c->s));
+        print_stamps(c, "map", nwg, kSpillBuckets);
+        launch_wc_agg(t, c->map_mode, 1, c->s);
+        print_stamps(c, "agg", kSpillBuckets);
+        if (have_dict) launch_dict_emit(t, nwg, c->s);
+        HCHK(c, hipEventRecord(c->ev[8], c->s));
+        HCHK(c, hipGetLastError());
+        if ((rc = read_counters(c))) return rc;
+        if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
+        const uint64_t nlist = c->h_ctr->nlist;
+        launch_wc_long(in, len, t, lt, nlist, c->s);
+        HCHK(c, hipGetLastError());
+        HCHK(c, hipEventRecord(c->ev[2], c->s));
+        if ((rc = read_counters(c))) return rc;
+        Counters h = *c->h_ctr;
+        if (h.status & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", h.status);
+        if (grow_on_overflow(c, h.status & (kStShortFull | kStLongFull | kStRecFull))) continue;
+        HCHK(c, c->recarena.ensure(h.long_bytes + 16));
+        t.out = rec_view(c);
+        if ((h.short_used || h.long_used) && launch_collect(t, c->rws, h.nrec, h.short_used, h.long_used != 0, c->s))
+            return fail(c, MRG_EDEVICE, "collect failed");
+        if ((rc = read_counters(c))) return rc;
+        h = *c->h_ctr;
+        if (grow_on_overflow(c, h.status & kStRecFull)) continue;
+        const uint64_t n = h.nrec;
+        mrg_parts* p = nullptr;
+        if ((rc = parts_alloc(c, n, h.long_bytes, MRG_APP_WC, nreduce, &p))) return rc;
+        const Recs& s = t.out;
+        hipError_t e = hipSuccess;
+        auto cp = [&](void* d, const void* src, size_t b) {
+            if (e == hipSuccess && b) e = hipMemcpyAsync(d, src, b, hipMemcpyDeviceToDevice, c->s);
+        };
+        cp(p->r.k0, s.k0, n * 8);
+        cp(p->r.k1, s.k1, n * 8);
+        cp(p->r.cnt, s.cnt, n * 8);
+        cp(p->r.koff, s.koff, n * 8);
+        cp(p->r.len, s.len, n * 4);
+        cp(p->r.part, s.part, n * 4);
+        cp(p->r.arena, s.arena, h.long_bytes);
+        if (e != hipSuccess) { mrg_parts_free(p); return fail(c, MRG_EDEVICE, "record copy: %s", hipGetErrorString(e)); }
+        HCHK(c, hipEventRecord(c->ev[3], c->s));
+        HCHK(c, hipEventSynchronize(c->ev[3]));
+        c->stats.map_kernel_ms = ev_ms(c->ev[0], c->ev[1]);
+        c->stats.map_total_ms = ev_ms(c->ev[9], c->ev[3]);
+        c->stats.dict_ms = ev_ms(c->ev[9], c->ev[10]);
+        c->stats.agg_ms = ev_ms(c->ev[1], c->ev[8]);
+        c->stats.long_ms = ev_ms(c->ev[8], c->ev[2]);
+        c->stats.collect_ms = ev_ms(c->ev[2], c->ev[3]);
+        c->stats.lds_overflow = h.spilled + h.spill_ovf;
+        c->stats.spill_ovf = h.spill_ovf;
+        c->stats.agg_miss = h.agg_miss;
+        c->stats.dict_hits = h.dict_hits;
+        c->stats.distinct_keys = n;
+        c->stats.long_keys = h.nlong_rec;
+        *out = p;
+        return MRG_OK;
+    }
+    return fail(c, MRG_ENOMEM, "mrg_map: tables kept overflowing");
 }
 
 // ---------------------------------------------------------------- C ABI
@@ -285,7 +528,8 @@ void mrg_close(mrg_ctx* c) {
     hipSetDevice(c->device);
     if (c->s) hipStreamSynchronize(c->s);
     if (c->comm) ncclCommDestroy(c->comm);
-    DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spmeta};
+    DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spmeta,
+                    &c->bflag, &c->dict, &c->dict_cnt, &c->sample, &c->recbuf, &c->recarena, &c->sortbuf};
     for (DevBuf* b : bs) b->release();
     if (c->d_l1) hipFree(c->d_l1);
     if (c->d_l2) hipFree(c->d_l2);
@@ -308,6 +552,10 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "map_grid")) c->grid = v > 0 ? (int)v : map_grid_size(c->device);
     else if (!strcmp(name, "map_mode")) c->map_mode = (int)v;
     else if (!strcmp(name, "spill_stream_keys")) c->spill_force_sub = v > 0 ? v : 0;
+    else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
+    else if (!strcmp(name, "dict_min_bytes")) c->dict_min_bytes = v > 0 ? (uint64_t)v : (32ull << 20);
+    else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (64ull << 20);
+    else if (!strcmp(name, "rec_cap")) c->rec_cap = v > 0 ? (uint64_t)v : (1u << 21);
     else return fail(c, MRG_EINVAL, "unknown option %s", name);
     return MRG_OK;
 }
@@ -398,31 +646,23 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         grep_nl = plen && memchr(pat, '\n', plen) != nullptr;  // no line can contain '\n'
     }
     LetterTables lt{c->d_l1, c->d_l2};
-    if (app == MRG_APP_WC && (rc = ensure_spill(c, len))) return rc;
+    if (app == MRG_APP_WC) return wc_map(c, in, len, nreduce, lt, out);
     for (int attempt = 0; attempt < 8; attempt++) {
         if ((rc = ensure_tables(c))) return rc;
         Tables t = make_tables(c);
-        clear_tables(t, c->s);
+        clear_for_run(c, t);
         HCHK(c, hipEventRecord(c->ev[0], c->s));
-        if (app == MRG_APP_WC) {
-            launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s);
-            HCHK(c, hipEventRecord(c->ev[1], c->s));
-            launch_wc_agg(t, c->map_mode, c->s);
-            HCHK(c, hipEventRecord(c->ev[8], c->s));
-        } else if (!grep_nl) {
+        if (!grep_nl) {
             if (plen) launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);
             else launch_grep_all_lines(in, len, t, c->grid, c->s);
         }
         HCHK(c, hipGetLastError());
-        if (app != MRG_APP_WC) {
-            HCHK(c, hipEventRecord(c->ev[1], c->s));
-            HCHK(c, hipEventRecord(c->ev[8], c->s));
-        }
+        HCHK(c, hipEventRecord(c->ev[1], c->s));
+        HCHK(c, hipEventRecord(c->ev[8], c->s));
         if ((rc = read_counters(c))) return rc;
         if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
         uint64_t nlist = c->h_ctr->nlist;
-        if (app == MRG_APP_WC) launch_wc_long(in, len, t, lt, nlist, c->s);
-        else launch_grep_lines(in, len, (uint32_t)plen, t, nlist, c->s);
+        launch_grep_lines(in, len, (uint32_t)plen, t, nlist, c->s);
         HCHK(c, hipGetLastError());
         HCHK(c, hipEventRecord(c->ev[2], c->s));
         if ((rc = read_counters(c))) return rc;
@@ -473,7 +713,7 @@ static int aggregate(mrg_ctx* c, const std::vector<Recs>& srcs, int app, uint32_
     for (int attempt = 0; attempt < 8; attempt++) {
         if ((rc = ensure_tables(c))) return rc;
         Tables t = make_tables(c);
-        clear_tables(t, c->s);
+        clear_for_run(c, t);
         for (const Recs& r : srcs) launch_insert_recs(r, t, c->s);
         HCHK(c, hipGetLastError());
         if ((rc = read_counters(c))) return rc;

@@ -1,0 +1,424 @@
+// mrgpu_device.h — device-side building blocks shared by the map-side kernels
+// (mrgpu_map.hip: grep / long words / collect; mrgpu_wc.hip: the wc pipeline).
+//
+// Reference semantics reproduced here (paths under /root/reference/MapReduce):
+//   * UTF-8 decoding of Go's `for i, r := range s` inside strings.FieldsFunc
+//     (mrapps/wc.go:26): utf8.DecodeRune acceptance ranges, an invalid byte is
+//     U+FFFD of width 1;
+//   * unicode.IsLetter (mrapps/wc.go:23), Unicode 13.0.0, via a two-level bitmap;
+//   * ihash = FNV-1a-32 & 0x7fffffff (mr/worker.go:33-37).
+#pragma once
+#include "mrgpu_internal.h"
+
+namespace mrg {
+
+constexpr int kChunk = 1024;                      // bytes per wave-chunk (16 B per lane)
+constexpr int kBack = 16;                         // look-back halo (UTF-8 rune starts, word starts)
+constexpr int kAhead = 64;                        // look-ahead halo (word lengths, UTF-8 tails)
+constexpr int kBuf = kBack + kChunk + kAhead;     // 1104, multiple of 16
+constexpr int kWavesPerWG = 16;
+constexpr int kThreads = kWavesPerWG * kWave;
+constexpr int kListCap = kChunk / 2;              // max word starts in a chunk
+constexpr int kGlobalProbes = 4096;
+
+// Explicit LDS address-space views.  Through a generic pointer hipcc emits
+// flat_load ... + s_waitcnt vmcnt(0) lgkmcnt(0), i.e. every LDS access would also
+// wait for the wave's outstanding HBM loads and stores.
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) unsigned long long lds_u64;
+typedef __attribute__((address_space(3))) u64x2 lds_u64x2;
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) u32x4 lds_uint4;  // 16-byte LDS unit (HIP's uint4 has no addrspace operator=)
+__device__ __forceinline__ u32x4 to_v4(uint4 a) { return (u32x4){a.x, a.y, a.z, a.w}; }
+__device__ __forceinline__ uint4 from_v4(u32x4 a) { return make_uint4(a.x, a.y, a.z, a.w); }
+
+// ---------------------------------------------------------------- helpers
+__device__ __forceinline__ uint64_t ld_agent(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ const uint8_t* ld_agent_ptr(const uint8_t* const* p) {
+    return __hip_atomic_load(const_cast<const uint8_t**>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void set_status(Counters* c, uint32_t bits) { atomicOr(&c->status, bits); }
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
+
+__device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Exclusive prefix sum over the wave of c (0 <= c < 2^BITS) by ballot bit-planes.
+template <int BITS>
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t c, uint32_t* total) {
+    uint32_t base = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < BITS; k++) {
+        const uint64_t b = __ballot((c >> k) & 1u);
+        base += mbcnt64(b) << k;
+        tot += (uint32_t)__popcll(b) << k;
+    }
+    *total = tot;
+    return base;
+}
+
+// One wave-wide atomicAdd for the lanes with `want` set; returns each such
+// lane's slot (base + rank among the wanting lanes).  Replaces one same-address
+// atomic per lane (which serialises at the memory side) by one per wave.
+__device__ __forceinline__ unsigned long long wave_alloc(unsigned long long* ctr, bool want) {
+    const uint64_t m = __ballot(want);
+    if (m == 0) return 0;
+    const uint32_t leader = __builtin_ctzll(m);
+    unsigned long long base = 0;
+    if (lane_id() == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
+    base = __shfl(base, (int)leader);
+    return base + mbcnt64(m);
+}
+
+// Sum over the wave (every lane gets it).
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// Add each thread's v0..v3 to ctr[0..3] with ONE atomic per workgroup per
+// counter.  Same-address device atomics serialise at the memory side (~12 ns
+// each, MI355X_MICROARCH.md fan-in row): a per-thread atomic from every thread
+// of a 256-workgroup grid costs milliseconds.  Call from every thread of the
+// block (it synchronises); scratch = 4 * (waves per block) u64 of LDS.
+template <int NWAVES>
+__device__ __forceinline__ void block_add4(unsigned long long* c0, unsigned long long* c1, unsigned long long* c2,
+                                           unsigned long long* c3, uint64_t v0, uint64_t v1, uint64_t v2, uint64_t v3,
+                                           unsigned long long* scratch) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    v0 = wave_sum(v0); v1 = wave_sum(v1); v2 = wave_sum(v2); v3 = wave_sum(v3);
+    if (lane == 0) {
+        scratch[4 * wv + 0] = v0; scratch[4 * wv + 1] = v1; scratch[4 * wv + 2] = v2; scratch[4 * wv + 3] = v3;
+    }
+    __syncthreads();
+    if (threadIdx.x < 4) {
+        uint64_t s = 0;
+        for (int w = 0; w < NWAVES; w++) s += scratch[4 * w + threadIdx.x];
+        unsigned long long* c = threadIdx.x == 0 ? c0 : threadIdx.x == 1 ? c1 : threadIdx.x == 2 ? c2 : c3;
+        if (s && c) atomicAdd(c, (unsigned long long)s);
+    }
+    __syncthreads();
+}
+
+// Block-wide slot allocation: each thread wants `mine` consecutive slots of a
+// shared cursor; returns the first of them.  One atomic per workgroup.
+// scratch = NWAVES + 1 u64 of LDS.  Call from every thread of the block.
+template <int NWAVES>
+__device__ __forceinline__ unsigned long long block_alloc(unsigned long long* ctr, uint32_t mine,
+                                                          unsigned long long* scratch) {
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t incl = mine;  // inclusive wave scan
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off);
+        if (lane >= (uint32_t)off) incl += y;
+    }
+    if (lane == 63) scratch[wv] = incl;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long run = 0;
+        for (int w = 0; w < NWAVES; w++) {
+            const unsigned long long x = scratch[w];
+            scratch[w] = run;
+            run += x;
+        }
+        scratch[NWAVES] = run ? atomicAdd(ctr, run) : 0ull;
+    }
+    __syncthreads();
+    const unsigned long long base = scratch[NWAVES] + scratch[wv] + (incl - mine);
+    __syncthreads();
+    return base;
+}
+
+// DPP whole-wave lane shifts (gfx9 wave_shr:1 / wave_shl:1; lanes shifted in
+// from outside the wave read `fill`).
+__device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x138, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_shl1(uint32_t v, uint32_t fill) {
+    return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false);
+}
+
+// 4 ASCII bytes -> 4-bit letter mask ([A-Za-z]); requires every byte < 0x80.
+__device__ __forceinline__ uint32_t ascii_letters4(uint32_t x) {
+    const uint32_t y = x | 0x20202020u;
+    const uint32_t t = (y + 0x1F1F1F1Fu) & ~(y + 0x05050505u) & 0x80808080u;
+    return ((t >> 7) * 0x10204080u) >> 28;
+}
+__device__ __forceinline__ uint32_t ascii_mask16(uint4 v) {
+    return ascii_letters4(v.x) | (ascii_letters4(v.y) << 4) | (ascii_letters4(v.z) << 8) | (ascii_letters4(v.w) << 12);
+}
+
+__device__ __forceinline__ bool is_letter_cp(uint32_t cp, LetterTables lt) {
+    if (cp < 0x80) return ((cp | 0x20u) - 0x61u) < 26u;
+    const uint32_t idx = lt.l1[cp >> 8];
+    return (lt.l2[idx * 8 + ((cp >> 5) & 7)] >> (cp & 31)) & 1u;
+}
+
+// Go utf8 acceptance: length of the valid sequence starting with bytes c0..c3, or 0.
+__device__ __forceinline__ int utf8_valid_len(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3) {
+    if (c0 < 0x80) return 1;
+    if (c0 < 0xC2 || c0 > 0xF4) return 0;
+    uint32_t lo = 0x80, hi = 0xBF;
+    if (c0 == 0xE0) lo = 0xA0;
+    else if (c0 == 0xED) hi = 0x9F;
+    else if (c0 == 0xF0) lo = 0x90;
+    else if (c0 == 0xF4) hi = 0x8F;
+    if (c1 < lo || c1 > hi) return 0;
+    if (c0 < 0xE0) return 2;
+    if ((c2 & 0xC0) != 0x80) return 0;
+    if (c0 < 0xF0) return 3;
+    if ((c3 & 0xC0) != 0x80) return 0;
+    return 4;
+}
+
+__device__ __forceinline__ uint32_t utf8_decode(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, int n) {
+    if (n == 1) return c0;
+    if (n == 2) return ((c0 & 0x1F) << 6) | (c1 & 0x3F);
+    if (n == 3) return ((c0 & 0x0F) << 12) | ((c1 & 0x3F) << 6) | (c2 & 0x3F);
+    return ((c0 & 0x07) << 18) | ((c1 & 0x3F) << 12) | ((c2 & 0x3F) << 6) | (c3 & 0x3F);
+}
+
+// Letter mask of the W bytes at b[q0 .. q0+W) with Go decoding semantics.
+// Needs b[q0-6 .. q0+W+3) addressable (zeros outside the input act as
+// non-continuation terminators, matching Go's truncated-sequence rule).
+// Rune starts use the local rule: byte q starts a rune unless a valid sequence
+// of length > k starts at q-k, k in {1,2,3}.
+template <int W, typename P>
+__device__ uint32_t utf8_letter_mask(P b, int q0, LetterTables lt) {
+    uint32_t mask = 0;
+    int vl1 = 0, vl2 = 0, vl3 = 0;  // valid lengths at q-1, q-2, q-3
+    for (int q = q0 - 6; q < q0 + W; q++) {
+        const uint32_t c0 = b[q], c1 = b[q + 1], c2 = b[q + 2], c3 = b[q + 3];
+        const int vl = utf8_valid_len(c0, c1, c2, c3);
+        if (q >= q0 - 3) {
+            const bool start = !(vl1 >= 2 || vl2 >= 3 || vl3 >= 4);
+            if (start) {
+                const bool let = vl > 0 && is_letter_cp(utf8_decode(c0, c1, c2, c3, vl), lt);
+                if (let) {
+                    for (int k = 0; k < vl; k++) {
+                        const int pos = q + k - q0;
+                        if (pos >= 0 && pos < W) mask |= 1u << pos;
+                    }
+                }
+            }
+        }
+        vl3 = vl2; vl2 = vl1; vl1 = vl;
+    }
+    return mask;
+}
+
+// 32-bit mix of a <= 16-byte key given as four little-endian words.
+__device__ __forceinline__ uint32_t fold32(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
+    const uint32_t x = w0 ^ __builtin_rotateleft32(w1, 7) ^ __builtin_rotateleft32(w2, 13) ^ __builtin_rotateleft32(w3, 21);
+    return x * 0x9E3779B1u;
+}
+
+__device__ __forceinline__ uint64_t short_hash64(uint64_t k0, uint64_t k1) {
+    const uint64_t h = (k0 ^ (k1 * 0x9E3779B97F4A7C15ull)) * 0xD6E8FEB86659FD93ull;
+    return h ^ (h >> 32);
+}
+
+__device__ __forceinline__ uint64_t fnv1a64_step(uint64_t h, uint32_t b) { return (h ^ b) * 1099511628211ull; }
+constexpr uint64_t kFnv64Off = 14695981039346656037ull;
+
+// Byte length of a zero-padded key of at most 16 bytes (letters are never 0x00).
+__device__ __forceinline__ uint32_t key_len_short(uint64_t k0, uint64_t k1) {
+    if (k1) return 8 + (uint32_t)((71 - __builtin_clzll(k1)) >> 3);
+    return (uint32_t)((71 - __builtin_clzll(k0)) >> 3);
+}
+
+// ihash (mr/worker.go:33-37) of a zero-padded short key, % nreduce (worker.go:76).
+__device__ __forceinline__ uint32_t short_partition(uint64_t k0, uint64_t k1, uint32_t len, uint32_t nreduce) {
+    uint32_t h = 2166136261u;
+    for (uint32_t k = 0; k < len; k++) {
+        const uint64_t w = k < 8 ? k0 : k1;
+        h = fnv1a32_step(h, (uint32_t)(w >> (8 * (k & 7))) & 0xFFu);
+    }
+    return (h & 0x7fffffffu) % nreduce;
+}
+
+// ------------------------------------------------------- HBM table inserts
+// Lock-free insert of a short key.  Claim = CAS on k0 (0 -> key); the claimer
+// then publishes k1.  A prober that matches k0 before k1 is visible never waits
+// inside the probe loop: the compiler may place the claimer's publish on the
+// loop's exit path, after every other lane of its wave left the loop, so an
+// in-loop wait can stall a whole wave (measured: ~100 ms per 10 GB).  Instead
+// *_try returns kRetry and *_insert re-runs it from a wave-uniform outer loop,
+// which only iterates after the claimer's stores have executed.  All shared
+// words use agent-scope atomics (coherent across the 8 XCD L2s).
+enum : int { kDone = 0, kRetry = 1, kFull = 2, kClaimed = 3 };
+constexpr uint32_t kMaxRetries = 1u << 20;
+
+__device__ inline int short_try(const Tables& t, uint64_t k0, uint64_t k1, uint64_t cnt) {
+    uint64_t i = short_hash64(k0, k1) & t.sh_mask;
+    for (uint32_t probes = 0; probes <= (uint32_t)kGlobalProbes; probes++) {
+        ShortSlot* s = &t.sh[i];
+        uint64_t cur = ld_agent(&s->k0);
+        if (cur == 0) {
+            const uint64_t prev = atomicCAS((unsigned long long*)&s->k0, 0ull, (unsigned long long)k0);
+            if (prev == 0) {
+                st_agent(&s->k1, k1);
+                atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                return kClaimed;
+            }
+            cur = prev;
+        }
+        if (cur == k0) {
+            const uint64_t v = ld_agent(&s->k1);
+            if (v == kUnwritten) return kRetry;
+            if (v == k1) {
+                atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                return kDone;
+            }
+        }
+        i = (i + 1) & t.sh_mask;
+    }
+    return kFull;
+}
+
+// One atomic per wave for the claim counter (see block_add4); the fill check
+// uses the wave's post-increment total.
+__device__ __forceinline__ void count_claims(unsigned long long* used_ctr, uint64_t cap, bool claimed, Counters* ctr,
+                                             uint32_t full_bit) {
+    const uint64_t m = __ballot(claimed);
+    if (m == 0) return;
+    if (lane_id() == (uint32_t)__builtin_ctzll(m)) {
+        const unsigned long long k = (unsigned long long)__popcll(m);
+        const unsigned long long used = atomicAdd(used_ctr, k) + k;
+        if (used * 10 > cap * 7) set_status(ctr, full_bit);
+    }
+}
+
+__device__ inline void short_insert(const Tables& t, uint64_t k0, uint64_t k1, uint64_t cnt) {
+    bool pending = true;
+    uint32_t tries = 0;
+    while (__ballot(pending)) {  // wave-uniform: reconverges between attempts
+        bool claimed = false;
+        if (pending) {
+            const int r = short_try(t, k0, k1, cnt);
+            if (r == kFull) set_status(t.ctr, kStShortFull);
+            claimed = r == kClaimed;
+            pending = r == kRetry;
+            if (pending && ++tries > kMaxRetries) { set_status(t.ctr, kStSpin); pending = false; }
+        }
+        count_claims(&t.ctr->short_used, t.sh_mask + 1, claimed, t.ctr, kStShortFull);
+    }
+}
+
+// Long keys: claim = CAS on hash; publish len+1 and rep separately; a prober
+// that needs them before both are visible retries from the outer loop.
+__device__ inline int long_try(const Tables& t, uint64_t h, const uint8_t* rep, uint64_t len, uint64_t cnt) {
+    uint64_t i = (h * 0x9E3779B97F4A7C15ull >> 17) & t.lo_mask;
+    for (uint32_t probes = 0; probes <= (uint32_t)kGlobalProbes; probes++) {
+        LongSlot* s = &t.lo[i];
+        uint64_t cur = ld_agent(&s->hash);
+        if (cur == 0) {
+            const uint64_t prev = atomicCAS((unsigned long long*)&s->hash, 0ull, (unsigned long long)h);
+            if (prev == 0) {
+                st_agent(&s->len, len + 1);
+                __hip_atomic_store(const_cast<const uint8_t**>(&s->rep), rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                return kClaimed;
+            }
+            cur = prev;
+        }
+        if (cur == h) {
+            const uint8_t* r = ld_agent_ptr(&s->rep);
+            const uint64_t lp1 = ld_agent(&s->len);
+            if (r == nullptr || lp1 == 0) return kRetry;
+            if (lp1 == len + 1) {
+                bool eq = true;
+                for (uint64_t k = 0; k < len; k++)
+                    if (r[k] != rep[k]) { eq = false; break; }
+                if (eq) {
+                    atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                    return kDone;
+                }
+            }
+        }
+        i = (i + 1) & t.lo_mask;
+    }
+    return kFull;
+}
+
+__device__ inline void long_insert(const Tables& t, uint64_t h, const uint8_t* rep, uint64_t len, uint64_t cnt) {
+    h |= 1ull;
+    bool pending = true;
+    uint32_t tries = 0;
+    while (__ballot(pending)) {
+        bool claimed = false;
+        if (pending) {
+            const int r = long_try(t, h, rep, len, cnt);
+            if (r == kFull) set_status(t.ctr, kStLongFull);
+            claimed = r == kClaimed;
+            pending = r == kRetry;
+            if (pending && ++tries > kMaxRetries) { set_status(t.ctr, kStSpin); pending = false; }
+        }
+        if (claimed) atomicAdd(&t.ctr->long_bytes, (unsigned long long)len);  // distinct long keys only
+        count_claims(&t.ctr->long_used, t.lo_mask + 1, claimed, t.ctr, kStLongFull);
+    }
+}
+
+// Append v to the list (one atomic per wave: see wave_alloc).
+__device__ __forceinline__ void list_append(const Tables& t, uint64_t v) {
+    const unsigned long long idx = wave_alloc(&t.ctr->nlist, true);
+    if (idx < t.list_cap) t.list[idx] = v;
+    else set_status(t.ctr, kStListFull);
+}
+
+// ------------------------------------------------------------ chunk loading
+struct ChunkRegs {
+    uint4 a, h;  // a: chunk bytes [16l, 16l+16); h: halo piece (lanes 0-3 look-ahead, lane 4 look-back)
+};
+
+__device__ __forceinline__ uint4 load16_bounded(const uint8_t* in, uint64_t n, int64_t off) {
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (int k = 0; k < 16; k++) {
+        const int64_t o = off + k;
+        if (o >= 0 && (uint64_t)o < n) w[k >> 2] |= (uint32_t)in[o] << (8 * (k & 3));
+    }
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+__device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ in, uint64_t n, uint64_t cs, uint32_t lane,
+                                           ChunkRegs& r) {
+    if (cs + kChunk + kAhead <= n && cs >= (uint64_t)kBack) {
+        const uint4* p = reinterpret_cast<const uint4*>(in + cs);
+        r.a = p[lane];
+        if (lane < 4) r.h = p[64 + lane];
+        else if (lane == 4) r.h = p[-1];
+        else r.h = make_uint4(0, 0, 0, 0);
+    } else {
+        r.a = load16_bounded(in, n, (int64_t)cs + 16 * lane);
+        if (lane < 4) r.h = load16_bounded(in, n, (int64_t)cs + kChunk + 16 * lane);
+        else if (lane == 4) r.h = load16_bounded(in, n, (int64_t)cs - 16);
+        else r.h = make_uint4(0, 0, 0, 0);
+    }
+}
+
+// Stage a chunk into a wave's LDS buffer: [0,16) look-back, [16,1040) chunk, [1040,1104) look-ahead.
+__device__ __forceinline__ void stage_chunk(lds_uint4* b4, const ChunkRegs& r, uint32_t lane) {
+    b4[1 + lane] = to_v4(r.a);
+    if (lane < 4) b4[65 + lane] = to_v4(r.h);
+    else if (lane == 4) b4[0] = to_v4(r.h);
+}
+
+}  // namespace mrg

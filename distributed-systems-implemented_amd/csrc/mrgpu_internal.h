@@ -26,6 +26,7 @@ enum : uint32_t {
     kStLongFull = 1u << 1,
     kStListFull = 1u << 2,
     kStSpin = 1u << 3,
+    kStRecFull = 1u << 4,   // the record output buffer was too small
 };
 
 struct ShortSlot {
@@ -53,21 +54,26 @@ struct Counters {
     unsigned long long spilled;    // keys written to the spill pool
     unsigned long long spill_ovf;  // keys that found their bucket region full (went to the HBM table)
     unsigned long long agg_miss;   // spill keys that missed the bucket aggregator's LDS table
+    unsigned long long bflush;     // spill buckets merged through the HBM table (overflow somewhere)
+    unsigned long long dict_hits;  // occurrences counted by the hot-key dictionary
     unsigned long long pad[3];
 };
 
-// Spill of LDS-combiner misses, hash-partitioned into kSpillBuckets buckets.
-// Every (bucket b, map workgroup g) pair owns a fixed stream of `sub_keys`
-// 16-B keys {k0,k1} at pool[(b*nwg + g)*sub_keys]; the workgroup appends with
-// an LDS cursor (no HBM atomics, no barriers) and records the stream length in
-// counts[b*nwg + g].  Keys beyond sub_keys go to the HBM table instead.
+// Spill of dictionary misses, hash-partitioned into kSpillBuckets buckets.
+// Every (map workgroup g, bucket b) pair owns a fixed stream of `sub_keys`
+// 16-B keys {k0,k1} at pool[(g*kSpillBuckets + b)*sub_keys] (a workgroup's
+// streams are contiguous: its scattered appends touch few TLB pages); the
+// workgroup appends with an LDS cursor (no HBM atomics, no barriers) and
+// records the stream length in counts[b*nwg + g].  Keys beyond sub_keys go to
+// the HBM table instead.
 constexpr int kSpillBuckets = 512;
+constexpr int kMaxMapWGs = 512;   // map workgroups (spill streams per bucket) at most
 // Keys of at most 8 bytes (k1 == 0) are spilled as 8-byte records into pool8,
 // longer ones as 16-byte records into pool: the combiner's misses are mostly
 // tail words, and most words are short, so this roughly halves spill traffic.
 struct Spill {
-    uint4* pool;                     // [kSpillBuckets][nwg][sub_keys] 16-byte records (k0, k1)
-    uint64_t* pool8;                 // [kSpillBuckets][nwg][sub8] 8-byte records (k0; k1 == 0)
+    uint4* pool;                     // [nwg][kSpillBuckets][sub_keys] 16-byte records (k0, k1)
+    uint64_t* pool8;                 // [nwg][kSpillBuckets][sub8] 8-byte records (k0; k1 == 0)
     uint64_t sub_keys, sub8;         // stream capacities (records)
     uint32_t* counts;                // [kSpillBuckets * nwg] records in each 16-byte stream
     uint32_t* counts8;               // [kSpillBuckets * nwg] records in each 8-byte stream
@@ -76,16 +82,16 @@ struct Spill {
     uint32_t nwg;
 };
 
-struct Tables {
-    ShortSlot* sh;
-    uint64_t sh_mask;
-    LongSlot* lo;
-    uint64_t lo_mask;
-    uint64_t* list;      // u64 offsets (long-word starts / grep match positions)
-    uint64_t list_cap;
-    Counters* ctr;
-    Spill sp;
-};
+// Hot-key dictionary (wc): a static table of the most frequent keys of a
+// sample of the split, built once per map and copied into every map
+// workgroup's LDS.  Keys of 1-8 bytes live in 2-way sets of 8-byte keys, keys of
+// 9-16 bytes in 1-way sets of 16-byte keys; a key may sit in either of two sets
+// (two-choice), so a lookup is two aligned 16-byte LDS reads.  Count slot of
+// (set s, way w) = 2*s + w.  Zero = empty (letters are never 0x00).
+constexpr int kDictShortSets = 4096;
+constexpr int kDictMidSets = 512;
+constexpr int kDictSets = kDictShortSets + kDictMidSets;
+constexpr int kDictSlots = 2 * kDictSets;
 
 struct Recs {
     uint64_t* k0;
@@ -99,23 +105,58 @@ struct Recs {
     uint64_t arena_n;
 };
 
+struct Tables {
+    ShortSlot* sh;
+    uint64_t sh_mask;
+    LongSlot* lo;
+    uint64_t lo_mask;
+    uint64_t* list;      // u64 offsets (long-word starts / grep match positions)
+    uint64_t list_cap;
+    Counters* ctr;
+    Spill sp;
+    // wc record output: dict_emit / wc_agg (direct) / collect append at ctr->nrec
+    Recs out;
+    uint64_t out_cap;
+    uint32_t nreduce;
+    uint32_t* bflag;        // [kSpillBuckets] nonzero: a key of the bucket went to the HBM table
+    const uint4* dict;      // dictionary image [kDictSets] (nullptr: no dictionary)
+    uint32_t* dict_cnt;     // [nwg][kDictSlots] per-map-workgroup dictionary counts
+    unsigned long long* dbg;  // diagnostics (MRG_DEBUG_TIMES): per-workgroup s_memrealtime stamps, or nullptr
+};
+
 struct LetterTables {
     const uint8_t* l1;
     const uint32_t* l2;
 };
 
 // ---- launchers (mrgpu_map.hip) ----
-void clear_tables(const Tables& t, hipStream_t s);
+void clear_tables(const Tables& t, bool short_table, hipStream_t s);
+// ---- wc pipeline (mrgpu_wc.hip) ----
+uint32_t wc_map_grid(uint64_t n, int grid);
 void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode,
                    hipStream_t s);
-void launch_wc_agg(const Tables& t, int mode, hipStream_t s);
-uint32_t wc_map_grid(uint64_t n, int grid);
+// emit: 0 = flush every bucket table into the HBM table (legacy),
+//       1 = emit records directly unless the bucket overflowed (then merge through HBM),
+//       2 = sample mode: emit table keys, drop misses (approximate counts for the dictionary)
+void launch_wc_agg(const Tables& t, int mode, int emit, hipStream_t s);
+void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s);
+// Gather `nwin` windows of `win` bytes (stride `stride`) of in[0,n) into dst, each followed by '\n'.
+void launch_sample_gather(const uint8_t* in, uint64_t n, uint64_t win, uint64_t stride, uint32_t nwin, uint8_t* dst,
+                          hipStream_t s);
+// Build the dictionary image from sample records ordered by descending count.
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* dict, hipStream_t s);
+// Sort keys for the dictionary build: ~count (u32) of each record.
+void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t s);
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
                      hipStream_t s);
 void launch_grep_lines(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nlist, hipStream_t s);
 void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int grid, hipStream_t s);
-void launch_collect(const Tables& t, Recs r, uint32_t nreduce, hipStream_t s);
+struct ReduceWs;
+// Append the HBM tables' keys to t.out: the ShortTable's `short_used` keys at
+// records [base, base + short_used) (ctr->nrec must equal base), then the
+// LongTable's at ctr->nrec (arena offsets from ctr->arena).  Returns 0 or a hipError_t.
+int launch_collect(const Tables& t, ReduceWs* ws, uint64_t base, uint64_t short_used, bool long_table, hipStream_t s);
 void launch_insert_recs(const Recs& src, const Tables& t, hipStream_t s);
 int map_grid_size(int device);
 
@@ -127,6 +168,12 @@ void reduce_ws_free(ReduceWs*);
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
 int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,
                   uint64_t* out_n, uint64_t* h_offsets, hipStream_t s);
+// Indices of occupied ShortTable slots; *d_count (device) = how many.
+int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64_t max_used, uint32_t** d_idx,
+                      uint32_t** d_count, hipStream_t s);
+// Stable radix sort of (u32 key, u32 value) pairs; result in k_out / v_out.
+int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, uint64_t n,
+                   hipStream_t s);
 // Compact recs with part == p (or owner rank) into dst (device), returns count on host.
 int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst_host_desc, hipStream_t s);
 

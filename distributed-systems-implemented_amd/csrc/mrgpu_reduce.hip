@@ -14,6 +14,8 @@
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "mrgpu_internal.h"
 
@@ -234,6 +236,32 @@ static int sort_pass(ReduceWs* ws, K* keys_in, K* keys_out, uint32_t* v_in, uint
     RCHK(ws->tmp.ensure(tb));
     RCHK(rocprim::radix_sort_pairs(ws->tmp.p, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
     return 0;
+}
+
+// Indices of the occupied ShortTable slots (rocprim select over a counting
+// iterator): a dense compaction with no same-address atomics.
+struct ShortUsed {
+    const ShortSlot* sh;
+    __host__ __device__ bool operator()(const uint32_t& i) const { return sh[i].k0 != 0; }
+};
+
+int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64_t max_used, uint32_t** d_idx,
+                      uint32_t** d_count, hipStream_t s) {
+    RCHK(ws->sel.ensure((max_used + 1024) * 4));
+    RCHK(ws->offs.ensure(64));
+    *d_idx = ws->sel.as<uint32_t>();
+    *d_count = ws->offs.as<uint32_t>();
+    rocprim::counting_iterator<uint32_t> first(0);
+    size_t tb = 0;
+    RCHK(rocprim::select(nullptr, tb, first, *d_idx, *d_count, (size_t)nslots, ShortUsed{sh}, s));
+    RCHK(ws->tmp.ensure(tb));
+    RCHK(rocprim::select(ws->tmp.p, tb, first, *d_idx, *d_count, (size_t)nslots, ShortUsed{sh}, s));
+    return 0;
+}
+
+int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, uint64_t n,
+                   hipStream_t s) {
+    return sort_pass<uint32_t>(ws, k_in, k_out, v_in, v_out, n, 32, s);
 }
 
 int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst, hipStream_t s) {

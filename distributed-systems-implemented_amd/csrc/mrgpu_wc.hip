@@ -1,0 +1,727 @@
+// mrgpu_wc.hip — the wc Map pipeline on gfx950 (MapReduce/mrapps/wc.go:21-34 +
+// mr/worker.go:72-78 + the grouping half of worker.go:123-146).
+//
+// Stages (one launch each, all on the context stream):
+//   0. sample_gather + wc_map (no dictionary) + wc_agg (sample mode) +
+//      dict_build: the hottest keys of an evenly spaced sample of the split
+//      become a static two-choice LDS dictionary (mrgpu_internal.h).
+//   1. wc_map_kernel: one wave per 1 KiB chunk at a time.  Lanes load 16 B
+//      each (coalesced dwordx4), classify letters (ASCII SWAR, or a Go-exact
+//      UTF-8 decode + IsLetter bitmap), find word starts and lengths from the
+//      letter bitmaps (DPP whole-wave shifts for the neighbour lanes), compact
+//      them into an LDS list, then each lane takes 3 words at a time (all their
+//      LDS reads in flight together): the key bytes come from the staged chunk
+//      with aligned 8-byte LDS reads, the dictionary lookup is two aligned 16 B
+//      reads, a hit is one LDS add, a miss is appended to the key's spill bucket
+//      stream (8-byte records for keys <= 8 bytes, 16-byte otherwise).
+//   2. wc_agg_kernel: one workgroup per spill bucket counts the bucket's keys in
+//      an LDS table.  Every key of the bucket reaches this one workgroup
+//      (bucket = f(key)), so its table holds exact totals and is emitted
+//      directly as records — unless a key of the bucket also went to the HBM
+//      table (a stream or table overflow), in which case the bucket is merged
+//      through the HBM table instead, so no key is ever emitted twice.
+//   3. dict_emit_kernel: per dictionary slot, the sum of the map workgroups'
+//      counts -> one record.  Dictionary keys never spill (the lookup is a
+//      pure function of the key), so these records are disjoint from stage 2.
+// ihash (FNV-1a) % nReduce is computed once per distinct key at emission: the
+// partition is a pure function of the key, so this equals worker.go:76's
+// per-KV ihash.  Every wc value is "1", so Reduce(len(values)) = sum of counts
+// (mrapps/wc.go:41-44): the combining is exact.
+#include "mrgpu_device.h"
+
+namespace mrg {
+
+constexpr int kBatch = 3;                     // words per lane in flight
+constexpr int kBatchWords = kBatch * kWave;   // 192 words of a chunk per pass
+constexpr int kAggThreads = 512;
+constexpr int kAggSets = 960;                 // bucket aggregator (half the LDS: 2 workgroups per CU)
+
+struct alignas(16) WaveBuf {
+    uint8_t buf[kBuf];        // staged chunk with halos
+    uint16_t list[kListCap];  // word starts (10 bits) | min(len, 31) << 10
+};
+
+struct alignas(16) MapLds {
+    uint4 dset[kDictSets];               // dictionary image
+    uint32_t dcnt[kDictSlots + kWave];   // dictionary counts of this workgroup (+ per-lane miss dummies)
+    WaveBuf w[kWavesPerWG];
+    // spill cursors: [0, 512) 8-byte streams, [512, 1024) 16-byte streams, then per-lane dummies for hits
+    uint32_t curs[2 * kSpillBuckets + kWave];
+    unsigned long long red[4 * kWavesPerWG];  // block_add4 scratch
+};
+static_assert(sizeof(MapLds) <= 160 * 1024, "map LDS budget");
+
+// The two candidate dictionary sets of a key (hash h; mid = key of 9-16 bytes).
+__device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, uint32_t& s2) {
+    const uint32_t sh = mid ? 23u : 20u;
+    const uint32_t m = mid ? (uint32_t)(kDictMidSets - 1) : (uint32_t)(kDictShortSets - 1);
+    const uint32_t off = mid ? (uint32_t)kDictShortSets : 0u;
+    const uint32_t a = h >> sh;
+    s1 = off + a;
+    s2 = off + (a ^ (((h >> 4) & m) | 1u));
+}
+
+// Spill bucket of a key: bits 11..19 of its hash (the bucket aggregator's table
+// indexes by the top bits, so a bucket's keys still spread over all its sets).
+__device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
+    static_assert(kSpillBuckets == 512, "bucket = 9 bits");
+    return (h >> 11) & 511u;
+}
+
+// ------------------------------------------------------------ wc map kernel
+template <uint32_t mode>
+__global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
+                                                          Tables t, LetterTables lt) {
+    // mode (benchmark ablation only, compile-time; results are wrong unless 0):
+    // 1 = read input only, 2 = tokenize only (no per-word work), 4 = per-word key
+    // extraction without the dictionary, 16 = no spill append (misses dropped)
+    __shared__ MapLds L;
+    const uint32_t tid = threadIdx.x;
+    const uint32_t lane = tid & 63;
+    const uint32_t wv = tid >> 6;
+    lds_uint4* dset = (lds_uint4*)L.dset;
+    lds_u32* dcnt = (lds_u32*)L.dcnt;
+    lds_u8* buf = (lds_u8*)L.w[wv].buf;
+    lds_u16* list = (lds_u16*)L.w[wv].list;
+    lds_u32* curs = (lds_u32*)L.curs;
+
+    if (t.dbg && tid == 0) t.dbg[2 * (kSpillBuckets + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
+    const bool use_dict = t.dict != nullptr;
+    for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kThreads) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
+    for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kThreads) dcnt[i] = 0;
+    for (uint32_t b = tid; b < 2u * kSpillBuckets + kWave; b += kThreads) curs[b] = 0;
+    __syncthreads();
+
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
+    const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
+    // this workgroup's streams: [g][bucket][sub] (a workgroup's stores stay within
+    // a few MiB, so they hit few TLB pages; mrgpu_internal.h Spill)
+    const uint4* const my_pool = t.sp.pool + (uint64_t)blockIdx.x * kSpillBuckets * t.sp.sub_keys;
+    uint64_t* const my_pool8 = t.sp.pool8 + (uint64_t)blockIdx.x * kSpillBuckets * t.sp.sub8;
+    const uint32_t sub = (uint32_t)t.sp.sub_keys, sub8 = (uint32_t)t.sp.sub8;
+    uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
+    // two chunks in flight per wave while a third is processed (1 KiB per wave
+    // in flight leaves the loop bound by HBM latency, not bandwidth)
+    ChunkRegs cr, n1, n2;
+    if (c0 < nchunks) load_chunk(in, n, c0 * kChunk, lane, cr);
+    if (c0 + stride < nchunks) load_chunk(in, n, (c0 + stride) * kChunk, lane, n1);
+
+    for (uint64_t c = c0; c < nchunks; c += stride) {
+        const uint64_t cs = c * kChunk;
+        if (c + 2 * stride < nchunks) load_chunk(in, n, (c + 2 * stride) * kChunk, lane, n2);
+        if constexpr ((mode & 1) != 0) {
+            acc ^= cr.a.x ^ cr.a.y ^ cr.a.z ^ cr.a.w ^ cr.h.x;
+            cr = n1;
+            n1 = n2;
+            continue;
+        }
+
+        stage_chunk((lds_uint4*)buf, cr, lane);
+        const uint32_t hi = (cr.a.x | cr.a.y | cr.a.z | cr.a.w | cr.h.x | cr.h.y | cr.h.z | cr.h.w) & 0x80808080u;
+        const bool ascii = __ballot(hi != 0) == 0;
+        uint32_t mA, mH = 0;
+        if (ascii) {
+            mA = ascii_mask16(cr.a);
+            if (lane < 5) mH = ascii_mask16(cr.h);
+        } else {
+            utf8_chunks++;
+            wave_sync();
+            mA = utf8_letter_mask<16>(buf, kBack + 16 * lane, lt);
+            if (lane < 2) mH = utf8_letter_mask<16>(buf, kBack + kChunk + 16 * lane, lt);
+            else if (lane == 4) mH = utf8_letter_mask<8>(buf, 8, lt) << 8;  // look-back bits 8..15
+        }
+        // Word starts (a letter byte whose predecessor is not one) and lengths
+        // (ctz over this lane's mask and the next two lanes'), packed into the
+        // list as start | min(len, 31) << 10.  Neighbour masks by DPP; the
+        // chunk's edges come from the halo masks of lanes 0, 1 (ahead) and 4 (back).
+        const uint32_t mh0 = __builtin_amdgcn_readlane(mH, 0);
+        const uint32_t mh1 = __builtin_amdgcn_readlane(mH, 1);
+        const uint32_t back = __builtin_amdgcn_readlane(mH, 4);
+        const uint32_t x1 = wave_shl1(mA, mh0);
+        const uint32_t x2 = wave_shl1(x1, mh1);
+        const uint32_t pv = wave_shr1(mA, back);
+        const uint64_t win = (uint64_t)mA | ((uint64_t)x1 << 16) | ((uint64_t)x2 << 32);
+        uint32_t SA = mA & ~((mA << 1) | ((pv >> 15) & 1u)) & 0xFFFFu;
+        uint32_t total;
+        uint32_t j = wave_excl_scan<4>(__popc(SA), &total);
+        while (SA) {
+            const uint32_t bit = __builtin_ctz(SA);
+            const uint32_t len = min((uint32_t)__builtin_ctzll(~(win >> bit)), 31u);
+            list[j++] = (uint16_t)((16 * lane + bit) | (len << 10));
+            SA &= SA - 1;
+        }
+        wave_sync();
+        if constexpr ((mode & 2) != 0) {
+            acc += total;
+            cr = n1;
+            n1 = n2;
+            continue;
+        }
+
+        for (uint32_t base = 0; base < total; base += kBatchWords) {
+            // The batch runs in phases so that every LDS round trip of the
+            // kBatch words is in flight at once (list entries -> key bytes ->
+            // dictionary sets -> counters / spill cursors), with no branches
+            // on per-lane outcomes: misses add to a per-lane dummy counter and
+            // hits bump a per-lane dummy cursor.
+            uint32_t e[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                const uint32_t w = base + lane + 64u * u;
+                e[u] = list[w < total ? w : 0u];
+            }
+            uint64_t d0[kBatch], d1[kBatch], d2[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                const uint32_t q = kBack + (e[u] & 0x3FFu);
+                const lds_u64* p8 = (const lds_u64*)(buf + (q & ~7u));
+                d0[u] = p8[0];
+                d1[u] = p8[1];
+                d2[u] = p8[2];
+            }
+            uint64_t k0[kBatch], k1[kBatch];
+            uint32_t hh[kBatch];
+            bool ok[kBatch], lng[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                const uint32_t w = base + lane + 64u * u;
+                const bool valid = w < total;
+                const uint32_t s = e[u] & 0x3FFu, len = e[u] >> 10;
+                ok[u] = valid && len <= 16;
+                lng[u] = valid && len > 16;
+                // 16 key bytes at [q, q+16) from the three aligned 8-byte reads
+                const uint32_t q = kBack + s;
+                const bool r4 = (q & 4u) != 0;
+                const uint32_t sh = q & 3u;
+                const uint32_t D0 = (uint32_t)d0[u], D1 = (uint32_t)(d0[u] >> 32), D2 = (uint32_t)d1[u],
+                               D3 = (uint32_t)(d1[u] >> 32), D4 = (uint32_t)d2[u], D5 = (uint32_t)(d2[u] >> 32);
+                const uint32_t a0 = r4 ? D1 : D0, a1 = r4 ? D2 : D1, a2 = r4 ? D3 : D2, a3 = r4 ? D4 : D3,
+                               a4 = r4 ? D5 : D4;
+                const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
+                const uint32_t w1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
+                const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sh);
+                const uint32_t w3 = __builtin_amdgcn_alignbyte(a4, a3, sh);
+                // keep the first len bytes (1 <= len <= 16), branch-free
+                const uint32_t lc = min(len, 16u);
+                const uint32_t l0 = min(lc, 8u), l1 = lc - l0;
+                const uint64_t m0 = ~0ull >> (64u - 8u * l0);  // l0 >= 1
+                const uint64_t m1 = l1 ? ~0ull >> (64u - 8u * l1) : 0ull;
+                k0[u] = (((uint64_t)w1 << 32) | w0) & m0;
+                k1[u] = (((uint64_t)w3 << 32) | w2) & m1;
+                hh[u] = fold32((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
+            }
+            // words of more than 16 bytes: resolved by wc_long_kernel from the input (rare)
+            if (__ballot(lng[0] || lng[1] || lng[2])) {
+#pragma unroll
+                for (int u = 0; u < kBatch; u++)
+                    if (lng[u]) list_append(t, cs + (e[u] & 0x3FFu));
+            }
+            if constexpr ((mode & 4) != 0) {
+#pragma unroll
+                for (int u = 0; u < kBatch; u++) acc += ok[u] ? hh[u] : 0u;
+                continue;
+            }
+            bool hit[kBatch];
+            if (use_dict) {
+                u32x4 A[kBatch], B[kBatch];
+                uint32_t s1[kBatch], s2[kBatch];
+#pragma unroll
+                for (int u = 0; u < kBatch; u++) {
+                    dict_sets(hh[u], k1[u] != 0, s1[u], s2[u]);
+                    A[u] = dset[s1[u]];
+                    B[u] = dset[s2[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < kBatch; u++) {
+                    // short key: any of the 4 ways of its two sets; mid key: the single
+                    // 16-byte way of either set (kk = the word compared with each set's
+                    // second 8 bytes)
+                    const bool mid = k1[u] != 0;
+                    const uint64_t kk = mid ? k1[u] : k0[u];
+                    const uint64_t alo = ((uint64_t)A[u].y << 32) | A[u].x, ahi = ((uint64_t)A[u].w << 32) | A[u].z;
+                    const uint64_t blo = ((uint64_t)B[u].y << 32) | B[u].x, bhi = ((uint64_t)B[u].w << 32) | B[u].z;
+                    const bool a0 = alo == k0[u], a1 = ahi == kk, b0 = blo == k0[u], b1 = bhi == kk;
+                    const bool ha = mid ? (a0 && a1) : (a0 || a1);
+                    const bool hb = mid ? (b0 && b1) : (b0 || b1);
+                    hit[u] = ok[u] && (ha || hb);
+                    const uint32_t slot = ha ? 2 * s1[u] + (!mid && !a0) : 2 * s2[u] + (!mid && !b0);
+                    const uint32_t ci = hit[u] ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
+                    __hip_atomic_fetch_add(&dcnt[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < kBatch; u++) hit[u] = false;
+            }
+            if constexpr ((mode & 16) != 0) {
+#pragma unroll
+                for (int u = 0; u < kBatch; u++) acc += hit[u];
+                continue;
+            }
+            // misses: append to this workgroup's stream of the key's bucket
+            uint32_t pos[kBatch];
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                const bool miss = ok[u] && !hit[u];
+                const uint32_t b = spill_bucket(hh[u]);
+                const uint32_t ci = miss ? (k1[u] == 0 ? b : (uint32_t)kSpillBuckets + b) : 2u * kSpillBuckets + lane;
+                pos[u] = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            bool over = false;
+#pragma unroll
+            for (int u = 0; u < kBatch; u++) {
+                const bool miss = ok[u] && !hit[u];
+                const uint32_t b = spill_bucket(hh[u]);
+                const bool small = k1[u] == 0;  // key of at most 8 bytes: 8-byte record
+                if (miss && small && pos[u] < sub8) my_pool8[(uint64_t)b * sub8 + pos[u]] = k0[u];
+                if (miss && !small && pos[u] < sub)
+                    const_cast<uint4*>(my_pool)[(uint64_t)b * sub + pos[u]] =
+                        make_uint4((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
+                over |= miss && pos[u] >= (small ? sub8 : sub);
+            }
+            if (__ballot(over)) {  // a stream is full: count in the HBM table; the bucket then merges through it
+#pragma unroll
+                for (int u = 0; u < kBatch; u++) {
+                    const bool miss = ok[u] && !hit[u];
+                    if (miss && pos[u] >= (k1[u] == 0 ? sub8 : sub)) {
+                        short_insert(t, k0[u], k1[u], 1);
+                        t.bflag[spill_bucket(hh[u])] = 1u;
+                        ovf++;
+                    }
+                }
+            }
+        }
+        wave_sync();
+        cr = n1;
+        n1 = n2;
+    }
+
+    __syncthreads();
+    unsigned long long spilled = 0, hits = 0;
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
+        const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[kSpillBuckets + b], sub);
+        t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x] = k;
+        t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x] = k8;
+        spilled += k + k8;
+    }
+    if (use_dict)
+        for (uint32_t i = tid; i < (uint32_t)kDictSlots; i += kThreads) {
+            const uint32_t v = dcnt[i];
+            t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i] = v;
+            hits += v;
+        }
+    if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
+    block_add4<kWavesPerWG>(&t.ctr->spilled, &t.ctr->dict_hits, &t.ctr->spill_ovf, &t.ctr->chunks_utf8, spilled, hits,
+                            ovf, lane == 0 ? utf8_chunks : 0, L.red);
+    if (t.dbg && tid == 0) t.dbg[2 * (kSpillBuckets + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ------------------------------------------------------------ LDS hash table
+// 4-way set-associative table: the 4 k0 of a set are 32 contiguous bytes (two
+// ds_read_b128).  A way is claimed by CAS on its k0 (0 -> key), then k1 is
+// published (k1 == kUnwritten until then; 0xFF bytes never occur in UTF-8).
+template <int NSETS>
+struct alignas(16) STable {
+    unsigned long long k0[NSETS * 4];
+    unsigned long long k1[NSETS * 4];
+    uint32_t cnt[NSETS * 4];
+};
+
+// Count `add` occurrences of (k0,k1).  One probe, no loop: the key is looked up
+// in the first way of its set whose k0 matches.  Returns false (a miss: the
+// caller forwards the key, where it is still counted exactly) when that way
+// holds a different k1, is claimed but not yet published, when the key is
+// absent and its set is full, or when a claim CAS races — the table never waits
+// on another lane (see short_try).
+template <int NSETS>
+__device__ __forceinline__ bool st_lookup_add(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add,
+                                              uint32_t& base, uint32_t& empty, uint32_t& m_out) {
+    base = __umulhi(h, NSETS) * 4;
+    const u64x2 a = *(lds_u64x2*)(&T.k0[base]);
+    const u64x2 b = *(lds_u64x2*)(&T.k0[base + 2]);
+    const uint32_t m = (a.x == k0 ? 1u : 0u) | (a.y == k0 ? 2u : 0u) | (b.x == k0 ? 4u : 0u) | (b.y == k0 ? 8u : 0u);
+    const uint32_t z = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u) | (b.x == 0 ? 4u : 0u) | (b.y == 0 ? 8u : 0u);
+    const uint32_t slot = base + (__builtin_ctz(m | 16u) & 3u);
+    const uint64_t v = *(lds_u64*)(&T.k1[slot]);  // read unconditionally (way 0 when m == 0)
+    const bool hit = (m != 0) & (v == k1);
+    empty = m != 0 ? 0u : z;  // claimable ways, only when the key's k0 is absent from the set
+    m_out = m | (z << 4);     // 0: the key's k0 is absent and the set is full
+    if (hit) __hip_atomic_fetch_add((lds_u32*)&T.cnt[slot], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return hit;
+}
+
+template <int NSETS>
+__device__ __forceinline__ bool st_claim(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t base, uint32_t empty,
+                                         uint32_t add) {
+    const uint32_t es = base + __builtin_ctz(empty);
+    if (atomicCAS(&T.k0[es], 0ull, (unsigned long long)k0) != 0ull) return false;
+    __hip_atomic_store(&T.k1[es], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    atomicAdd(&T.cnt[es], add);
+    return true;
+}
+
+// Two-choice insert (a key whose first set is full and does not hold its k0
+// lives in a second set).  Ways are never freed, so once the first set is full
+// a key absent from it can never appear there later — lookups and claims agree
+// on the key's set.
+// A lost claim CAS (another lane took the way first, often for the same key)
+// is retried once: the winner of this wave published its k1 in program order.
+__device__ __forceinline__ uint32_t second_hash(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 16) * 0xC2B2AE3Du; }
+
+template <int NSETS>
+__device__ __forceinline__ bool st_insert2(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
+    bool ok = false;
+    for (int attempt = 0; attempt < 2 && !ok; attempt++) {
+        uint32_t base, empty, m;
+        ok = st_lookup_add(T, k0, k1, h, add, base, empty, m);
+        if (empty != 0) {
+            ok = st_claim(T, k0, k1, base, empty, add);
+        } else if (m == 0) {  // first set full, key absent
+            ok = st_lookup_add(T, k0, k1, second_hash(h), add, base, empty, m);
+            if (empty != 0) ok = st_claim(T, k0, k1, base, empty, add);
+            else break;
+        } else {
+            break;  // k0 present with another k1 (or unpublished): a miss, no retry
+        }
+    }
+    return ok;
+}
+
+// Exact lookup in a table no lane is claiming in any more (every way of both
+// candidate sets); -1 if absent.
+template <int NSETS>
+__device__ __forceinline__ int st_find_exact(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h) {
+    for (int c = 0; c < 2; c++) {
+        const uint32_t base = __umulhi(c == 0 ? h : second_hash(h), NSETS) * 4;
+        for (uint32_t w = 0; w < 4; w++)
+            if (T.k0[base + w] == k0 && T.k1[base + w] == k1) return (int)(base + w);
+    }
+    return -1;
+}
+
+template <int NSETS>
+__device__ __forceinline__ void st_init(STable<NSETS>& T, uint32_t tid, uint32_t nthreads) {
+    for (uint32_t i = tid; i < (uint32_t)NSETS * 4; i += nthreads) {
+        T.k0[i] = 0;
+        T.k1[i] = kUnwritten;
+        T.cnt[i] = 0;
+    }
+}
+
+struct alignas(16) AggLds {
+    STable<kAggSets> T;
+    unsigned long long red[4 * (kAggThreads / 64) + 4];  // block_add4 / block_alloc scratch
+    uint32_t spre[kMaxMapWGs + 4];  // exclusive prefix of the stream lengths of the pool being walked
+    uint32_t nmiss;               // keys appended to the bucket's miss list
+};
+static_assert(2 * sizeof(AggLds) <= 160 * 1024, "two aggregator workgroups per CU");
+
+// Write record o (distinct short key with its total) of t.out.
+__device__ __forceinline__ void put_short(const Tables& t, unsigned long long o, uint64_t k0, uint64_t k1, uint64_t cnt,
+                                          bool strict) {
+    if (o >= t.out_cap) {
+        if (strict) set_status(t.ctr, kStRecFull);
+        return;
+    }
+    const uint32_t len = key_len_short(k0, k1);
+    t.out.k0[o] = k0;
+    t.out.k1[o] = k1;
+    t.out.len[o] = len;
+    t.out.cnt[o] = cnt;
+    t.out.part[o] = short_partition(k0, k1, len, t.nreduce);
+    t.out.koff[o] = ~0ull;
+}
+
+// ------------------------------------------------------------ bucket aggregation
+// The bucket's nwg streams (one per map workgroup) are walked as one sequence
+// of kAggGroup-record groups with the next group's loads in flight while the
+// current one is inserted.
+constexpr uint32_t kAggUnroll = 4;
+constexpr uint32_t kAggGroup = kAggUnroll * kAggThreads;
+
+__device__ __forceinline__ void agg_load(const uint4* blk, uint32_t i, uint32_t f, uint4& r) {
+    r = i < f ? blk[i] : make_uint4(0, 0, 0, 0);
+}
+__device__ __forceinline__ void agg_load(const uint64_t* blk, uint32_t i, uint32_t f, uint4& r) {
+    const uint64_t k = i < f ? blk[i] : 0;
+    r = make_uint4((uint32_t)k, (uint32_t)(k >> 32), 0, 0);
+}
+
+template <uint32_t amode, typename Rec>
+__device__ __forceinline__ void agg_streams(AggLds& A, const Tables& t, const Rec* pool, const uint32_t* gcounts,
+                                            uint64_t gstride, bool keep_miss, uint64_t& miss) {
+    const uint32_t nwg = t.sp.nwg, tid = threadIdx.x;
+    // Exclusive prefix of the stream lengths in LDS: record v of the bucket's
+    // virtual concatenation of streams lives in stream g, pre[g] <= v < pre[g+1],
+    // so a group of kAggGroup records may span many short streams.
+    __syncthreads();
+    if (tid < 64) {
+        constexpr int kPer = kMaxMapWGs / 64;
+        uint32_t c[kPer], sum = 0;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            const uint32_t idx = tid * kPer + k;
+            c[k] = idx < nwg ? gcounts[idx] : 0u;
+            sum += c[k];
+        }
+        uint32_t incl = sum;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t y = __shfl_up(incl, off);
+            if (tid >= (uint32_t)off) incl += y;
+        }
+        uint32_t run = incl - sum;
+#pragma unroll
+        for (int k = 0; k < kPer; k++) {
+            A.spre[tid * kPer + k] = run;
+            run += c[k];
+        }
+        if (tid == 63) A.spre[kMaxMapWGs] = incl;
+    }
+    __syncthreads();
+    const uint32_t total = A.spre[kMaxMapWGs];
+    uint32_t gc = 0;  // this thread's stream cursor (its record indices only grow)
+    auto load = [&](uint32_t v, uint4& r) {
+        if (v < total) {
+            while (A.spre[gc + 1] <= v) gc++;
+            agg_load(pool + (uint64_t)gc * gstride, v - A.spre[gc], 0xFFFFFFFFu, r);
+        } else {
+            r = make_uint4(0, 0, 0, 0);
+        }
+    };
+    uint4 cur[kAggUnroll], nxt[kAggUnroll];
+#pragma unroll
+    for (uint32_t u = 0; u < kAggUnroll; u++) load(u * kAggThreads + tid, cur[u]);
+    for (uint32_t G = 0; G < total; G += kAggGroup) {
+#pragma unroll
+        for (uint32_t u = 0; u < kAggUnroll; u++) load(G + kAggGroup + u * kAggThreads + tid, nxt[u]);
+#pragma unroll
+        for (uint32_t u = 0; u < kAggUnroll; u++) {
+            const uint4 k = cur[u];
+            if ((k.x | k.y) != 0) {  // else past the end (keys have k0 != 0)
+                const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
+                const uint32_t h = fold32(k.x, k.y, k.z, k.w);
+                if constexpr ((amode & 128) != 0) {
+                    miss += h;
+                } else if (!st_insert2(A.T, k0, k1, h, 1)) {
+                    const uint32_t pos = atomicAdd(&A.nmiss, 1u);  // defer: no HBM round trip in the loop
+                    if (keep_miss) {
+                        if (pos < t.sp.amiss_cap)
+                            t.sp.amiss[(uint64_t)blockIdx.x * t.sp.amiss_cap + pos] =
+                                make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                        else
+                            short_insert(t, k0, k1, 1);
+                    }
+                    miss++;
+                }
+            }
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < kAggUnroll; u++) cur[u] = nxt[u];
+    }
+}
+
+// amode (benchmark ablation only, compile-time; results are wrong unless 0):
+// 128 = read + hash the records only.  emit: see launch_wc_agg.
+template <uint32_t amode>
+__global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit) {
+    __shared__ AggLds A;
+    const uint32_t tid = threadIdx.x;
+    if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
+    st_init(A.T, tid, kAggThreads);
+    if (tid == 0) A.nmiss = 0;
+    __syncthreads();
+    const uint64_t b = blockIdx.x;
+    const bool keep_miss = emit != 2;
+    uint64_t miss = 0;
+    // bucket b's stream of workgroup g: pool[(g * kSpillBuckets + b) * sub]
+    agg_streams<amode>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg, (uint64_t)kSpillBuckets * t.sp.sub8,
+                       keep_miss, miss);
+    agg_streams<amode>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
+                       (uint64_t)kSpillBuckets * t.sp.sub_keys, keep_miss, miss);
+    __syncthreads();
+    const uint32_t nm = min(A.nmiss, t.sp.amiss_cap);
+    // merge: a key of this bucket went to the HBM table from the map kernel
+    // (stream overflow) or a deferred miss did not fit the miss list, so the same
+    // key may be on both sides: merge the whole bucket through the HBM table.
+    const bool merge = emit == 0 || (emit == 1 && (t.bflag[b] != 0 || A.nmiss > t.sp.amiss_cap));
+    if (merge) {
+        for (uint32_t i = tid; i < (uint32_t)kAggSets * 4; i += kAggThreads) {
+            const uint64_t k0 = A.T.k0[i];
+            if (k0 != 0) short_insert(t, k0, A.T.k1[i], A.T.cnt[i]);
+        }
+        for (uint32_t i = tid; i < nm; i += kAggThreads) {  // deferred misses, all lanes in flight
+            const uint4 k = t.sp.amiss[b * t.sp.amiss_cap + i];
+            short_insert(t, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, 1);
+        }
+        if (tid == 0) atomicAdd(&t.ctr->bflush, 1ull);
+    } else {
+        // Deferred misses: counted in the (now stable) table when their key is
+        // there, otherwise in the HBM table — so the table's keys and the HBM
+        // table's keys of this bucket are disjoint and the table is emitted as is.
+        if (emit == 1)
+            for (uint32_t i = tid; i < nm; i += kAggThreads) {
+                const uint4 k = t.sp.amiss[b * t.sp.amiss_cap + i];
+                const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
+                const int slot = st_find_exact(A.T, k0, k1, fold32(k.x, k.y, k.z, k.w));
+                if (slot >= 0) atomicAdd(&A.T.cnt[slot], 1u);
+                else short_insert(t, k0, k1, 1);
+            }
+        __syncthreads();
+        // one cursor allocation per workgroup, then each thread writes its keys
+        uint32_t mine = 0;
+        for (uint32_t i = tid; i < (uint32_t)kAggSets * 4; i += kAggThreads) mine += A.T.k0[i] != 0;
+        unsigned long long o = block_alloc<kAggThreads / 64>(&t.ctr->nrec, mine, A.red);
+        for (uint32_t i = tid; i < (uint32_t)kAggSets * 4; i += kAggThreads) {
+            const uint64_t k0 = A.T.k0[i];
+            if (k0 != 0) put_short(t, o++, k0, A.T.k1[i], A.T.cnt[i], emit == 1);
+        }
+    }
+    if (amode != 0 && miss == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // no DCE in ablation builds
+    block_add4<kAggThreads / 64>(&t.ctr->agg_miss, nullptr, nullptr, nullptr, amode == 0 ? miss : 0, 0, 0, 0, A.red);
+    if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
+// ------------------------------------------------------------ dictionary
+// Records of the dictionary keys: per slot, the sum over map workgroups.  A
+// block owns 64 slots; its 16 waves each sum every 16th workgroup's row
+// (coalesced 256 B per wave), then the partial sums meet in LDS.
+constexpr int kEmitSlots = 64;
+__global__ void __launch_bounds__(1024) dict_emit_kernel(Tables t, uint32_t nwg) {
+    __shared__ unsigned long long part[16][kEmitSlots];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t i = blockIdx.x * kEmitSlots + lane;
+    unsigned long long sum = 0;
+    if (i < (uint32_t)kDictSlots)
+        for (uint32_t g = wv; g < nwg; g += 16) sum += t.dict_cnt[(uint64_t)g * kDictSlots + i];
+    part[wv][lane] = sum;
+    __syncthreads();
+    if (wv != 0) return;
+    sum = 0;
+    for (int w = 0; w < 16; w++) sum += part[w][lane];
+    uint64_t k0 = 0, k1 = 0;
+    if (i < (uint32_t)kDictSlots) {
+        const uint32_t set = i >> 1, way = i & 1;
+        const uint4 sv = t.dict[set];
+        if (set >= (uint32_t)kDictShortSets) {
+            k0 = way ? 0 : ((uint64_t)sv.y << 32) | sv.x;
+            k1 = ((uint64_t)sv.w << 32) | sv.z;
+        } else {
+            k0 = way ? (((uint64_t)sv.w << 32) | sv.z) : (((uint64_t)sv.y << 32) | sv.x);
+        }
+    }
+    const bool valid = k0 != 0 && sum != 0;
+    const unsigned long long o = wave_alloc(&t.ctr->nrec, valid);  // one wave per block
+    if (valid) put_short(t, o, k0, k1, sum, true);
+}
+
+// Copy sample windows: window w = in[w*stride, w*stride + win) -> dst[w*(win+16)],
+// followed by 16 '\n' bytes (a separator, so no word spans two windows).
+__global__ void sample_gather_kernel(const uint8_t* __restrict__ in, uint64_t win, uint64_t stride, uint32_t nwin,
+                                     uint8_t* __restrict__ dst) {
+    const uint64_t per = win / 16 + 1;  // uint4 units per window incl. the separator
+    const uint64_t total = per * nwin;
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += gs) {
+        const uint64_t w = i / per, k = i - w * per;
+        uint4 v;
+        if (k + 1 == per) v = make_uint4(0x0A0A0A0Au, 0x0A0A0A0Au, 0x0A0A0A0Au, 0x0A0A0A0Au);
+        else v = reinterpret_cast<const uint4*>(in + w * stride)[k];
+        reinterpret_cast<uint4*>(dst)[i] = v;
+    }
+}
+
+__global__ void dict_keys_kernel(Recs r, uint32_t* keys, uint32_t* idx) {
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += gs) {
+        const uint64_t c = r.cnt[i];
+        keys[i] = ~(uint32_t)(c > 0xFFFFFFFFull ? 0xFFFFFFFFull : c);  // ascending sort = descending count
+        idx[i] = (uint32_t)i;
+    }
+}
+
+// One workgroup places the sample's keys in descending-count order, 1024 at a
+// time, each into the first of its two sets with a free way; a key whose two
+// sets are full stays out (it is then counted through the spill path).
+__global__ void __launch_bounds__(1024) dict_build_kernel(Recs r, const uint32_t* order, uint64_t n, uint4* dict) {
+    __shared__ uint4 S[kDictSets];
+    __shared__ uint32_t fill[kDictSets];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < (uint32_t)kDictSets; i += 1024) {
+        S[i] = make_uint4(0, 0, 0, 0);
+        fill[i] = 0;
+    }
+    __syncthreads();
+    const uint64_t lim = n < (uint64_t)4 * kDictSlots ? n : (uint64_t)4 * kDictSlots;
+    for (uint64_t base = 0; base < lim; base += 1024) {
+        const uint64_t i = base + tid;
+        if (i < lim) {
+            const uint32_t j = order[i];
+            const uint64_t k0 = r.k0[j], k1 = r.k1[j];
+            if (r.koff[j] == ~0ull && k0 != 0) {
+                const bool mid = k1 != 0;
+                const uint32_t h = fold32((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                uint32_t s1, s2;
+                dict_sets(h, mid, s1, s2);
+                const uint32_t ways = mid ? 1u : 2u;
+                uint32_t s = s1, w = atomicAdd(&fill[s1], 1u);
+                if (w >= ways) { s = s2; w = atomicAdd(&fill[s2], 1u); }
+                if (w < ways) {
+                    if (mid) S[s] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+                    else if (w == 0) { S[s].x = (uint32_t)k0; S[s].y = (uint32_t)(k0 >> 32); }
+                    else { S[s].z = (uint32_t)k0; S[s].w = (uint32_t)(k0 >> 32); }
+                }
+            }
+        }
+        __syncthreads();
+    }
+    for (uint32_t i = tid; i < (uint32_t)kDictSets; i += 1024) dict[i] = S[i];
+}
+
+// ------------------------------------------------------------ launchers
+uint32_t wc_map_grid(uint64_t n, int grid) {
+    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
+    if (g > (uint64_t)grid) g = (uint64_t)grid;
+    if (g > (uint64_t)kMaxMapWGs) g = kMaxMapWGs;
+    return (uint32_t)(g ? g : 1);
+}
+
+void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode, hipStream_t s) {
+    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    if (nchunks == 0) return;
+    const uint64_t g = wc_map_grid(n, grid);
+    switch (mode) {
+#define MRG_MAP_MODE(M) \
+    case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
+        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16)
+#undef MRG_MAP_MODE
+        default: wc_map_kernel<0><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
+    }
+}
+
+void launch_wc_agg(const Tables& t, int mode, int emit, hipStream_t s) {
+    // mode 512 (diagnostic only, wrong results): a read-only pass first, so the
+    // timed pass runs with warm caches and address translations
+    if (mode & 512) wc_agg_kernel<128><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
+    if (mode & 128) wc_agg_kernel<128><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
+    else wc_agg_kernel<0><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
+}
+
+void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s) {
+    dict_emit_kernel<<<(kDictSlots + kEmitSlots - 1) / kEmitSlots, 1024, 0, s>>>(t, nwg);
+}
+
+void launch_sample_gather(const uint8_t* in, uint64_t /*n*/, uint64_t win, uint64_t stride, uint32_t nwin, uint8_t* dst,
+                          hipStream_t s) {
+    sample_gather_kernel<<<1024, 256, 0, s>>>(in, win, stride, nwin, dst);
+}
+
+void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t s) {
+    if (r.n) dict_keys_kernel<<<512, 256, 0, s>>>(r, keys, idx);
+}
+
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* dict, hipStream_t s) {
+    dict_build_kernel<<<1, 1024, 0, s>>>(r, order, n, dict);
+}
+
+}  // namespace mrg

@@ -63,6 +63,9 @@ class Stats(ctypes.Structure):
         ("agg_ms", ctypes.c_double),
         ("long_ms", ctypes.c_double),
         ("collect_ms", ctypes.c_double),
+        ("dict_ms", ctypes.c_double),
+        ("dict_keys", c_uint64),
+        ("dict_hits", c_uint64),
     ]
 
     def as_dict(self):

@@ -1,7 +1,7 @@
 """Summarize rocprofv3 --pmc CSVs per kernel (sum over dimensions per dispatch,
 then mean over dispatches of the same kernel).
 
-usage: python tools/pmc_summary.py <dir with *_counter_collection.csv> [kernel-substring ...]
+usage: python tools/pmc_summary.py [--each] <dir with *_counter_collection.csv> [kernel-substring ...]
 FETCH_SIZE / WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reports half the bytes of
 wide coalesced streaming reads (MI355X_MICROARCH.md §HBM), so `hbm_read_bytes_x2`
 doubles it.
@@ -14,7 +14,7 @@ import os
 import sys
 
 
-def load(d):
+def load(d, separate=False):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
     for f in glob.glob(os.path.join(d, "*_counter_collection.csv")):
@@ -23,17 +23,25 @@ def load(d):
             names[key] = r["Kernel_Name"].split("(")[0]
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
     out = collections.defaultdict(lambda: collections.defaultdict(list))
-    for key, ctrs in per.items():
-        for c, v in ctrs.items():
-            out[names[key]][c].append(v)
+    seen = collections.Counter()
+    for key in sorted(per, key=lambda k: (k[0], int(k[1]))):
+        nm = names[key]
+        if separate:
+            nm = f"{nm}#{seen[nm]}"
+            seen[names[key]] += 1
+        for c, v in per[key].items():
+            out[nm][c].append(v)
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in out.items()}
 
 
 def main():
-    d = sys.argv[1]
-    want = sys.argv[2:] or ["wc_map_kernel", "wc_agg_kernel"]
+    args = sys.argv[1:]
+    separate = "--each" in args  # one entry per dispatch (name#k) instead of the mean per kernel name
+    args = [a for a in args if a != "--each"]
+    d = args[0]
+    want = args[1:] or ["wc_map_kernel", "wc_agg_kernel"]
     res = {}
-    for k, cs in load(d).items():
+    for k, cs in load(d, separate).items():
         if any(w in k for w in want):
             if "FETCH_SIZE" in cs:
                 cs["hbm_read_bytes_x2"] = cs["FETCH_SIZE"] * 1024 * 2

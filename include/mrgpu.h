@@ -83,6 +83,9 @@ typedef struct {
     double agg_ms;            /* wc: per-bucket aggregation kernel */
     double long_ms;           /* long-word / grep-line resolution, incl. its host round trip */
     double collect_ms;        /* distinct keys -> records (partition = ihash % nReduce) */
+    double dict_ms;           /* wc: sample + hot-key dictionary build */
+    uint64_t dict_keys;       /* wc: sample keys offered to the dictionary */
+    uint64_t dict_hits;       /* wc: occurrences counted by the dictionary in LDS */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);

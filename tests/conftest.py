@@ -20,3 +20,21 @@ def ctx():
     c = Context(0)
     yield c
     c.close()
+
+
+@pytest.fixture(scope="session")
+def ctx_dict():
+    """A context that builds the wc hot-key dictionary even for small splits
+    (default: only splits >= 32 MiB get one), so parity covers the dictionary path."""
+    from mrgpu import Context
+
+    c = Context(0)
+    c.set_option("dict_min_bytes", 1)
+    yield c
+    c.close()
+
+
+@pytest.fixture(params=["nodict", "dict"])
+def wctx(request):
+    """wc parity runs on both paths: no dictionary (every word spills) and dictionary."""
+    return request.getfixturevalue("ctx" if request.param == "nodict" else "ctx_dict")

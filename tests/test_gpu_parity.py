@@ -55,8 +55,8 @@ def check(ctx, app, files, nreduces=(1, 10, 64)):
 
 
 @pytest.mark.parametrize("name", sorted(cases.edge_cases()))
-def test_wc_edge_cases(ctx, name):
-    check(ctx, "wc", cases.edge_cases()[name])
+def test_wc_edge_cases(wctx, name):
+    check(wctx, "wc", cases.edge_cases()[name])
 
 
 @pytest.mark.parametrize("name", sorted(cases.grep_edge_cases()))
@@ -67,9 +67,11 @@ def test_grep_edge_cases(ctx, name):
 
 @pytest.mark.parametrize("kind,V,seed,inv", [(C.KIND_ASCII, 5000, 1, 0.0), (C.KIND_ASCII, 200000, 2, 0.0),
                                              (C.KIND_UTF8, 20000, 3, 0.0), (C.KIND_UTF8, 20000, 4, 0.001)])
-def test_wc_synthetic(ctx, kind, V, seed, inv):
+def test_wc_synthetic(wctx, kind, V, seed, inv):
     files = cases.synthetic(kind, V, [1_000_003, 2_500_000, 777_777], seed, inv)
-    check(ctx, "wc", files, nreduces=(1, 10, 64))
+    check(wctx, "wc", files, nreduces=(1, 10, 64))
+    if wctx.stats()["dict_keys"]:
+        assert wctx.stats()["dict_hits"] > 0
 
 
 def test_grep_synthetic(ctx):
@@ -90,15 +92,26 @@ def test_wc_lds_overflow_and_table_growth(ctx):
         ctx.set_option("short_table_log2", 0)
 
 
-def test_wc_spill_region_full(ctx):
-    """Tiny spill streams: they overflow and the rest of their keys take the HBM-table path."""
+def test_wc_spill_region_full(wctx):
+    """Tiny spill streams: they overflow and the rest of their keys take the HBM-table path
+    (those buckets then merge through the HBM table instead of emitting directly)."""
     files = cases.synthetic(C.KIND_ASCII, 1_000_000, [6_000_000], 15)
-    ctx.set_option("spill_stream_keys", 8)
+    wctx.set_option("spill_stream_keys", 8)
     try:
-        check(ctx, "wc", files, nreduces=(10,))
-        assert ctx.stats()["spill_ovf"] > 0
+        check(wctx, "wc", files, nreduces=(10,))
+        assert wctx.stats()["spill_ovf"] > 0
     finally:
-        ctx.set_option("spill_stream_keys", 0)
+        wctx.set_option("spill_stream_keys", 0)
+
+
+def test_wc_record_buffer_growth(wctx):
+    """A record buffer far too small for the distinct keys: the map grows it and re-runs."""
+    files = cases.synthetic(C.KIND_ASCII, 200_000, [3_000_000], 17)
+    wctx.set_option("rec_cap", 64)
+    try:
+        check(wctx, "wc", files, nreduces=(10,))
+    finally:
+        wctx.set_option("rec_cap", 0)
 
 
 def test_wc_bucket_aggregator_overflow(ctx):
@@ -109,11 +122,11 @@ def test_wc_bucket_aggregator_overflow(ctx):
     assert ctx.stats()["agg_miss"] > 0
 
 
-def test_wc_large_vs_oracle(ctx):
+def test_wc_large_vs_oracle(wctx):
     """64 MB C2-style corpus: full bytes vs the C oracle."""
     voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
     files = [bytes(f) for f in voc.fill_files([16_000_000] * 4, [2000 + i for i in range(4)], C.wc_params())]
-    check(ctx, "wc", files, nreduces=(10,))
+    check(wctx, "wc", files, nreduces=(10,))
 
 
 def test_run_job_device_resident(ctx):
