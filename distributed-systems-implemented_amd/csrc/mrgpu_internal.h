@@ -89,7 +89,7 @@ struct Spill {
 // (two-choice), so a lookup is two aligned 16-byte LDS reads.  Count slot of
 // (set s, way w) = 2*s + w.  Zero = empty (letters are never 0x00).
 constexpr int kDictShortSets = 4096;
-constexpr int kDictMidSets = 512;
+constexpr int kDictMidSets = 256;
 constexpr int kDictSets = kDictShortSets + kDictMidSets;
 constexpr int kDictSlots = 2 * kDictSets;
 

@@ -36,24 +36,34 @@ constexpr int kBatchWords = kBatch * kWave;   // 192 words of a chunk per pass
 constexpr int kAggThreads = 512;
 constexpr int kAggSets = 960;                 // bucket aggregator (half the LDS: 2 workgroups per CU)
 
-struct alignas(16) WaveBuf {
-    uint8_t buf[kBuf];        // staged chunk with halos
-    uint16_t list[kListCap];  // word starts (10 bits) | min(len, 31) << 10
-};
+// A chunk owns kOwn input bytes; its LDS slot is one 1 KiB DMA of the bytes
+// [start - 16, start + 1008): 16 bytes of look-back (lane 0), the 944 owned
+// bytes (lanes 1-59) and 64 bytes of look-ahead (lanes 60-63).  Neighbouring
+// slots overlap by 80 bytes (re-read from L2, not HBM).
+constexpr int kSlotBytes = 1024;
+constexpr int kOwnLanes = 59;
+constexpr uint64_t kOwn = 16 * kOwnLanes;  // 944
+constexpr int kRing = 3;                    // LDS slots per wave: current, in flight, free (the word list)
+static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot");
 
 struct alignas(16) MapLds {
-    uint4 dset[kDictSets];               // dictionary image
-    uint32_t dcnt[kDictSlots + kWave];   // dictionary counts of this workgroup (+ per-lane miss dummies)
-    WaveBuf w[kWavesPerWG];
+    uint4 dset[kDictSets];                      // dictionary image
+    uint32_t dcnt[kDictSlots + kWave];          // dictionary counts of this workgroup (+ per-lane miss dummies)
+    uint8_t ring[kWavesPerWG][kRing][kSlotBytes];
     // spill cursors: [0, 512) 8-byte streams, [512, 1024) 16-byte streams, then per-lane dummies for hits
     uint32_t curs[2 * kSpillBuckets + kWave];
-    unsigned long long red[4 * kWavesPerWG];  // block_add4 scratch
+    unsigned long long red[4 * kWavesPerWG];    // block_add4 scratch
 };
 static_assert(sizeof(MapLds) <= 160 * 1024, "map LDS budget");
 
+__device__ __forceinline__ uint32_t lds_addr(const void* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+
 // The two candidate dictionary sets of a key (hash h; mid = key of 9-16 bytes).
 __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, uint32_t& s2) {
-    const uint32_t sh = mid ? 23u : 20u;
+    static_assert(kDictShortSets == 4096 && kDictMidSets == 256, "set index = top 12 / 8 bits");
+    const uint32_t sh = mid ? 24u : 20u;
     const uint32_t m = mid ? (uint32_t)(kDictMidSets - 1) : (uint32_t)(kDictShortSets - 1);
     const uint32_t off = mid ? (uint32_t)kDictShortSets : 0u;
     const uint32_t a = h >> sh;
@@ -69,23 +79,70 @@ __device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
 }
 
 // ------------------------------------------------------------ wc map kernel
+// One wave per 944-byte chunk at a time, every wave independent.  The input is
+// streamed into a private ring of three 1 KiB LDS slots with one
+// buffer_load_dwordx4...lds per chunk (lane l: bytes [start-16+16l, +16): lane 0
+// = look-back, lanes 1-59 = the 944 owned bytes, lanes 60-63 = look-ahead; the
+// descriptor's range check zero-fills before/after the split), issued two
+// chunks ahead.  gfx9 counts loads and stores on one in-order vmcnt, and hipcc
+// waits vmcnt(0) as soon as a loop's VMEM count is not static, so the loop's
+// VMEM instructions are fixed: the DMA is inline asm (invisible to hipcc's
+// waitcnt pass) and the spill appends are exactly 2 * kBatch range-checked
+// buffer stores per chunk (lanes with nothing to store use an out-of-range
+// offset).  The wait for chunk c's DMA is then vmcnt(kVmemPerIter): only the
+// previous iteration's stores and DMA may still be in flight.  Rare paths with
+// other memory operations (words > 16 bytes, chunks of more than kBatchWords
+// words, HBM-table overflow, UTF-8 table lookups) drain with vmcnt(0).
+constexpr uint32_t kOutOfRange = 0xFFFFFFF0u;
+constexpr int kVmemPerIter = 2 * kBatch + 1;
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ i32x4 raw_rsrc(const void* base, uint32_t nrec) {
+    const uint64_t b = (uint64_t)base;
+    return (i32x4){(int)(uint32_t)b, (int)((uint32_t)(b >> 32) & 0xFFFFu), (int)nrec, 0x00020000};
+}
+// 64 lanes x 16 B: lane l's bytes at rsrc + voff -> LDS [lds_base + 16 l]
+__device__ __forceinline__ void dma_chunk(i32x4 rsrc, uint32_t voff, uint32_t lds_base) {
+    // operands are wave-uniform; readfirstlane puts them in SGPRs for the asm "s" constraints
+    rsrc = (i32x4){__builtin_amdgcn_readfirstlane(rsrc.x), __builtin_amdgcn_readfirstlane(rsrc.y),
+                   __builtin_amdgcn_readfirstlane(rsrc.z), __builtin_amdgcn_readfirstlane(rsrc.w)};
+    lds_base = __builtin_amdgcn_readfirstlane(lds_base);
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
+                 : "memory", "m0");
+}
+__device__ __forceinline__ void wait_vmem_iter() {
+    static_assert(kVmemPerIter == 7, "update the immediate");
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+}
+__device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// Issue the DMA of chunk c (any c: chunks past the split read as zeros).
+__device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uint64_t c, uint32_t lane, uint32_t lds_base) {
+    const uint64_t cs = c * kOwn;
+    const uint64_t bo = cs >= 16 ? cs - 16 : 0;    // descriptor base (input offset)
+    const uint32_t e = (uint32_t)(bo + 16 - cs);   // 16 for the split's first chunk, else 0
+    const uint64_t rem = n > bo ? n - bo : 0;
+    const uint32_t nrec = rem > 0x7FFFFF00ull ? 0x7FFFFF00u : (uint32_t)rem;
+    dma_chunk(raw_rsrc(in + (n > bo ? bo : 0), nrec), 16u * lane - e, lds_base);
+}
+
 template <uint32_t mode>
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
                                                           Tables t, LetterTables lt) {
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
-    // 1 = read input only, 2 = tokenize only (no per-word work), 4 = per-word key
-    // extraction without the dictionary, 16 = no spill append (misses dropped)
+    // 1 = stream input only, 2 = tokenize only (no per-word work), 4 = per-word
+    // key extraction without the dictionary, 16 = no spill append (misses dropped)
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
-    const uint32_t wv = tid >> 6;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the DMA operands
     lds_uint4* dset = (lds_uint4*)L.dset;
     lds_u32* dcnt = (lds_u32*)L.dcnt;
-    lds_u8* buf = (lds_u8*)L.w[wv].buf;
-    lds_u16* list = (lds_u16*)L.w[wv].list;
     lds_u32* curs = (lds_u32*)L.curs;
-
     if (t.dbg && tid == 0) t.dbg[2 * (kSpillBuckets + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
+
     const bool use_dict = t.dict != nullptr;
     for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kThreads) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
     for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kThreads) dcnt[i] = 0;
@@ -94,206 +151,228 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
     const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
-    // this workgroup's streams: [g][bucket][sub] (a workgroup's stores stay within
-    // a few MiB, so they hit few TLB pages; mrgpu_internal.h Spill)
-    const uint4* const my_pool = t.sp.pool + (uint64_t)blockIdx.x * kSpillBuckets * t.sp.sub_keys;
-    uint64_t* const my_pool8 = t.sp.pool8 + (uint64_t)blockIdx.x * kSpillBuckets * t.sp.sub8;
     const uint32_t sub = (uint32_t)t.sp.sub_keys, sub8 = (uint32_t)t.sp.sub8;
+    // this workgroup's spill streams: [g][bucket][sub] (a workgroup's stores stay
+    // within a few MiB, so they hit few TLB pages; mrgpu_internal.h Spill)
+    const __amdgpu_buffer_rsrc_t rs8 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(t.sp.pool8 + (uint64_t)blockIdx.x * kSpillBuckets * sub8), (short)0, (int)(kSpillBuckets * sub8 * 8u),
+        0x00020000);
+    const __amdgpu_buffer_rsrc_t rs16 = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)(t.sp.pool + (uint64_t)blockIdx.x * kSpillBuckets * sub), (short)0, (int)(kSpillBuckets * sub * 16u),
+        0x00020000);
     uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
-    // two chunks in flight per wave while a third is processed (1 KiB per wave
-    // in flight leaves the loop bound by HBM latency, not bandwidth)
-    ChunkRegs cr, n1, n2;
-    if (c0 < nchunks) load_chunk(in, n, c0 * kChunk, lane, cr);
-    if (c0 + stride < nchunks) load_chunk(in, n, (c0 + stride) * kChunk, lane, n1);
+    const uint32_t ring0 = lds_addr(L.ring[wv][0]);
 
-    for (uint64_t c = c0; c < nchunks; c += stride) {
-        const uint64_t cs = c * kChunk;
-        if (c + 2 * stride < nchunks) load_chunk(in, n, (c + 2 * stride) * kChunk, lane, n2);
-        if constexpr ((mode & 1) != 0) {
-            acc ^= cr.a.x ^ cr.a.y ^ cr.a.z ^ cr.a.w ^ cr.h.x;
-            cr = n1;
-            n1 = n2;
-            continue;
-        }
-
-        stage_chunk((lds_uint4*)buf, cr, lane);
-        const uint32_t hi = (cr.a.x | cr.a.y | cr.a.z | cr.a.w | cr.h.x | cr.h.y | cr.h.z | cr.h.w) & 0x80808080u;
-        const bool ascii = __ballot(hi != 0) == 0;
-        uint32_t mA, mH = 0;
-        if (ascii) {
-            mA = ascii_mask16(cr.a);
-            if (lane < 5) mH = ascii_mask16(cr.h);
-        } else {
-            utf8_chunks++;
+    // prologue: chunk c0 landed before the loop, chunk c0 + stride in flight
+    dma_for_chunk(in, n, c0, lane, ring0);
+    wait_vmem_all();
+    dma_for_chunk(in, n, c0 + stride, lane, ring0 + kSlotBytes);
+    uint32_t k = 0;  // ring slot of the current chunk
+    for (uint64_t c = c0; c < nchunks; c += stride, k = k == kRing - 1 ? 0 : k + 1) {
+        wait_vmem_iter();  // chunk c's DMA (issued two iterations ago) has landed
+        const uint64_t cs = c * kOwn;  // the chunk's first own byte = slot byte 16 (slot byte i = input cs - 16 + i)
+        lds_u8* buf = (lds_u8*)L.ring[wv][k];
+        lds_uint4* b4 = (lds_uint4*)buf;
+        const uint32_t kf = k == 0 ? kRing - 1 : k - 1;  // free slot: the word list now, chunk c + 2*stride next
+        lds_u16* list = (lds_u16*)L.ring[wv][kf];
+        if ((n & 3) && (int64_t)cs - kBack + kSlotBytes > (int64_t)(n & ~3ull)) {
+            // the split's last n % 4 bytes sit in a dword the range check zero-filled
+            const int64_t p = (int64_t)(n & ~3ull) + lane - ((int64_t)cs - kBack);
+            if (lane < (uint32_t)(n & 3) && p >= 0 && p < kSlotBytes) buf[p] = in[(n & ~3ull) + lane];
+            wait_vmem_all();
             wave_sync();
-            mA = utf8_letter_mask<16>(buf, kBack + 16 * lane, lt);
-            if (lane < 2) mH = utf8_letter_mask<16>(buf, kBack + kChunk + 16 * lane, lt);
-            else if (lane == 4) mH = utf8_letter_mask<8>(buf, 8, lt) << 8;  // look-back bits 8..15
         }
-        // Word starts (a letter byte whose predecessor is not one) and lengths
-        // (ctz over this lane's mask and the next two lanes'), packed into the
-        // list as start | min(len, 31) << 10.  Neighbour masks by DPP; the
-        // chunk's edges come from the halo masks of lanes 0, 1 (ahead) and 4 (back).
-        const uint32_t mh0 = __builtin_amdgcn_readlane(mH, 0);
-        const uint32_t mh1 = __builtin_amdgcn_readlane(mH, 1);
-        const uint32_t back = __builtin_amdgcn_readlane(mH, 4);
-        const uint32_t x1 = wave_shl1(mA, mh0);
-        const uint32_t x2 = wave_shl1(x1, mh1);
-        const uint32_t pv = wave_shr1(mA, back);
-        const uint64_t win = (uint64_t)mA | ((uint64_t)x1 << 16) | ((uint64_t)x2 << 32);
-        uint32_t SA = mA & ~((mA << 1) | ((pv >> 15) & 1u)) & 0xFFFFu;
-        uint32_t total;
-        uint32_t j = wave_excl_scan<4>(__popc(SA), &total);
-        while (SA) {
-            const uint32_t bit = __builtin_ctz(SA);
-            const uint32_t len = min((uint32_t)__builtin_ctzll(~(win >> bit)), 31u);
-            list[j++] = (uint16_t)((16 * lane + bit) | (len << 10));
-            SA &= SA - 1;
-        }
-        wave_sync();
-        if constexpr ((mode & 2) != 0) {
-            acc += total;
-            cr = n1;
-            n1 = n2;
-            continue;
-        }
-
-        for (uint32_t base = 0; base < total; base += kBatchWords) {
-            // The batch runs in phases so that every LDS round trip of the
-            // kBatch words is in flight at once (list entries -> key bytes ->
-            // dictionary sets -> counters / spill cursors), with no branches
-            // on per-lane outcomes: misses add to a per-lane dummy counter and
-            // hits bump a per-lane dummy cursor.
-            uint32_t e[kBatch];
-#pragma unroll
-            for (int u = 0; u < kBatch; u++) {
-                const uint32_t w = base + lane + 64u * u;
-                e[u] = list[w < total ? w : 0u];
-            }
-            uint64_t d0[kBatch], d1[kBatch], d2[kBatch];
-#pragma unroll
-            for (int u = 0; u < kBatch; u++) {
-                const uint32_t q = kBack + (e[u] & 0x3FFu);
-                const lds_u64* p8 = (const lds_u64*)(buf + (q & ~7u));
-                d0[u] = p8[0];
-                d1[u] = p8[1];
-                d2[u] = p8[2];
-            }
-            uint64_t k0[kBatch], k1[kBatch];
-            uint32_t hh[kBatch];
-            bool ok[kBatch], lng[kBatch];
-#pragma unroll
-            for (int u = 0; u < kBatch; u++) {
-                const uint32_t w = base + lane + 64u * u;
-                const bool valid = w < total;
-                const uint32_t s = e[u] & 0x3FFu, len = e[u] >> 10;
-                ok[u] = valid && len <= 16;
-                lng[u] = valid && len > 16;
-                // 16 key bytes at [q, q+16) from the three aligned 8-byte reads
-                const uint32_t q = kBack + s;
-                const bool r4 = (q & 4u) != 0;
-                const uint32_t sh = q & 3u;
-                const uint32_t D0 = (uint32_t)d0[u], D1 = (uint32_t)(d0[u] >> 32), D2 = (uint32_t)d1[u],
-                               D3 = (uint32_t)(d1[u] >> 32), D4 = (uint32_t)d2[u], D5 = (uint32_t)(d2[u] >> 32);
-                const uint32_t a0 = r4 ? D1 : D0, a1 = r4 ? D2 : D1, a2 = r4 ? D3 : D2, a3 = r4 ? D4 : D3,
-                               a4 = r4 ? D5 : D4;
-                const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
-                const uint32_t w1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
-                const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sh);
-                const uint32_t w3 = __builtin_amdgcn_alignbyte(a4, a3, sh);
-                // keep the first len bytes (1 <= len <= 16), branch-free
-                const uint32_t lc = min(len, 16u);
-                const uint32_t l0 = min(lc, 8u), l1 = lc - l0;
-                const uint64_t m0 = ~0ull >> (64u - 8u * l0);  // l0 >= 1
-                const uint64_t m1 = l1 ? ~0ull >> (64u - 8u * l1) : 0ull;
-                k0[u] = (((uint64_t)w1 << 32) | w0) & m0;
-                k1[u] = (((uint64_t)w3 << 32) | w2) & m1;
-                hh[u] = fold32((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
-            }
-            // words of more than 16 bytes: resolved by wc_long_kernel from the input (rare)
-            if (__ballot(lng[0] || lng[1] || lng[2])) {
-#pragma unroll
-                for (int u = 0; u < kBatch; u++)
-                    if (lng[u]) list_append(t, cs + (e[u] & 0x3FFu));
-            }
-            if constexpr ((mode & 4) != 0) {
-#pragma unroll
-                for (int u = 0; u < kBatch; u++) acc += ok[u] ? hh[u] : 0u;
-                continue;
-            }
-            bool hit[kBatch];
-            if (use_dict) {
-                u32x4 A[kBatch], B[kBatch];
-                uint32_t s1[kBatch], s2[kBatch];
-#pragma unroll
-                for (int u = 0; u < kBatch; u++) {
-                    dict_sets(hh[u], k1[u] != 0, s1[u], s2[u]);
-                    A[u] = dset[s1[u]];
-                    B[u] = dset[s2[u]];
-                }
-#pragma unroll
-                for (int u = 0; u < kBatch; u++) {
-                    // short key: any of the 4 ways of its two sets; mid key: the single
-                    // 16-byte way of either set (kk = the word compared with each set's
-                    // second 8 bytes)
-                    const bool mid = k1[u] != 0;
-                    const uint64_t kk = mid ? k1[u] : k0[u];
-                    const uint64_t alo = ((uint64_t)A[u].y << 32) | A[u].x, ahi = ((uint64_t)A[u].w << 32) | A[u].z;
-                    const uint64_t blo = ((uint64_t)B[u].y << 32) | B[u].x, bhi = ((uint64_t)B[u].w << 32) | B[u].z;
-                    const bool a0 = alo == k0[u], a1 = ahi == kk, b0 = blo == k0[u], b1 = bhi == kk;
-                    const bool ha = mid ? (a0 && a1) : (a0 || a1);
-                    const bool hb = mid ? (b0 && b1) : (b0 || b1);
-                    hit[u] = ok[u] && (ha || hb);
-                    const uint32_t slot = ha ? 2 * s1[u] + (!mid && !a0) : 2 * s2[u] + (!mid && !b0);
-                    const uint32_t ci = hit[u] ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
-                    __hip_atomic_fetch_add(&dcnt[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                }
+        if constexpr ((mode & 1) != 0) {
+            acc += buf[16 + lane];
+        } else {
+            // lane l holds slot bytes [16l, 16l+16): lane 0 = look-back, lanes 1-59 the
+            // chunk's own 944 bytes, lanes 60-63 = look-ahead
+            const uint4 ca = from_v4(b4[lane]);
+            const uint32_t hi = (ca.x | ca.y | ca.z | ca.w) & 0x80808080u;
+            const bool ascii = __ballot(hi != 0) == 0;
+            uint32_t mA;
+            if (ascii) {
+                mA = ascii_mask16(ca);
             } else {
-#pragma unroll
-                for (int u = 0; u < kBatch; u++) hit[u] = false;
+                utf8_chunks++;
+                if (lane == 0) mA = utf8_letter_mask<8>(buf, 8, lt) << 8;  // bytes 8-15 (rune starts need 3 back)
+                else if (lane < 62) mA = utf8_letter_mask<16>(buf, 16 * lane, lt);
+                else mA = 0;  // lanes 62-63: never needed (lengths look two lanes past lane 59)
+                wait_vmem_all();
             }
-            if constexpr ((mode & 16) != 0) {
-#pragma unroll
-                for (int u = 0; u < kBatch; u++) acc += hit[u];
-                continue;
+            // Word starts (a letter byte whose predecessor is not one) in the owned lanes
+            // and lengths (ctz over this lane's mask and the next two lanes'), packed into
+            // the list as slot position | min(len, 31) << 10.  Neighbour masks by DPP.
+            const uint32_t x1 = wave_shl1(mA, 0u);
+            const uint32_t x2 = wave_shl1(x1, 0u);
+            const uint32_t pv = wave_shr1(mA, 0u);
+            const uint64_t win = (uint64_t)mA | ((uint64_t)x1 << 16) | ((uint64_t)x2 << 32);
+            const bool owned = lane >= 1 && lane <= (uint32_t)kOwnLanes;
+            uint32_t SA = owned ? (mA & ~((mA << 1) | ((pv >> 15) & 1u)) & 0xFFFFu) : 0u;
+            uint32_t total;
+            uint32_t j = wave_excl_scan<4>(__popc(SA), &total);
+            while (SA) {
+                const uint32_t bit = __builtin_ctz(SA);
+                const uint32_t len = min((uint32_t)__builtin_ctzll(~(win >> bit)), 31u);
+                list[j++] = (uint16_t)((16 * lane + bit) | (len << 10));
+                SA &= SA - 1;
             }
-            // misses: append to this workgroup's stream of the key's bucket
-            uint32_t pos[kBatch];
-#pragma unroll
-            for (int u = 0; u < kBatch; u++) {
-                const bool miss = ok[u] && !hit[u];
-                const uint32_t b = spill_bucket(hh[u]);
-                const uint32_t ci = miss ? (k1[u] == 0 ? b : (uint32_t)kSpillBuckets + b) : 2u * kSpillBuckets + lane;
-                pos[u] = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            bool over = false;
-#pragma unroll
-            for (int u = 0; u < kBatch; u++) {
-                const bool miss = ok[u] && !hit[u];
-                const uint32_t b = spill_bucket(hh[u]);
-                const bool small = k1[u] == 0;  // key of at most 8 bytes: 8-byte record
-                if (miss && small && pos[u] < sub8) my_pool8[(uint64_t)b * sub8 + pos[u]] = k0[u];
-                if (miss && !small && pos[u] < sub)
-                    const_cast<uint4*>(my_pool)[(uint64_t)b * sub + pos[u]] =
-                        make_uint4((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
-                over |= miss && pos[u] >= (small ? sub8 : sub);
-            }
-            if (__ballot(over)) {  // a stream is full: count in the HBM table; the bucket then merges through it
-#pragma unroll
-                for (int u = 0; u < kBatch; u++) {
-                    const bool miss = ok[u] && !hit[u];
-                    if (miss && pos[u] >= (k1[u] == 0 ? sub8 : sub)) {
-                        short_insert(t, k0[u], k1[u], 1);
-                        t.bflag[spill_bucket(hh[u])] = 1u;
-                        ovf++;
+            wave_sync();
+            if constexpr ((mode & 2) != 0) {
+                acc += total;
+            } else {
+                // passes of kBatchWords words: a 944-byte chunk of text has ~160; a chunk
+                // with more words drains after each extra pass (its VMEM count differs)
+                const uint32_t passes = total == 0 ? 1u : (total + kBatchWords - 1) / kBatchWords;
+                for (uint32_t pass = 0; pass < passes; pass++) {
+                    const uint32_t base = pass * kBatchWords;
+                    // The batch runs in phases so that every LDS round trip of the
+                    // kBatch words is in flight at once (list entries -> key bytes ->
+                    // dictionary sets -> counters / spill cursors), with no branches
+                    // on per-lane outcomes: misses add to a per-lane dummy counter and
+                    // hits bump a per-lane dummy cursor.
+                    uint32_t e[kBatch];
+        #pragma unroll
+                    for (int u = 0; u < kBatch; u++) {
+                        const uint32_t w = base + lane + 64u * u;
+                        e[u] = list[w < total ? w : 0u];
                     }
+                    uint64_t d0[kBatch], d1[kBatch], d2[kBatch];
+        #pragma unroll
+                    for (int u = 0; u < kBatch; u++) {
+                        const uint32_t q = e[u] & 0x3FFu;
+                        const lds_u64* p8 = (const lds_u64*)(buf + (q & ~7u));
+                        d0[u] = p8[0];
+                        d1[u] = p8[1];
+                        d2[u] = p8[2];
+                    }
+                    uint64_t k0[kBatch], k1[kBatch];
+                    uint32_t hh[kBatch];
+                    bool ok[kBatch], lng[kBatch];
+        #pragma unroll
+                    for (int u = 0; u < kBatch; u++) {
+                        const uint32_t w = base + lane + 64u * u;
+                        const bool valid = w < total;
+                        const uint32_t s = e[u] & 0x3FFu, len = e[u] >> 10;
+                        ok[u] = valid && len <= 16;
+                        lng[u] = valid && len > 16;
+                        // 16 key bytes at [q, q+16) from the three aligned 8-byte reads
+                        const uint32_t q = s;
+                        const bool r4 = (q & 4u) != 0;
+                        const uint32_t sh = q & 3u;
+                        const uint32_t D0 = (uint32_t)d0[u], D1 = (uint32_t)(d0[u] >> 32), D2 = (uint32_t)d1[u],
+                                       D3 = (uint32_t)(d1[u] >> 32), D4 = (uint32_t)d2[u], D5 = (uint32_t)(d2[u] >> 32);
+                        const uint32_t a0 = r4 ? D1 : D0, a1 = r4 ? D2 : D1, a2 = r4 ? D3 : D2, a3 = r4 ? D4 : D3,
+                                       a4 = r4 ? D5 : D4;
+                        const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
+                        const uint32_t w1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
+                        const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sh);
+                        const uint32_t w3 = __builtin_amdgcn_alignbyte(a4, a3, sh);
+                        // keep the first len bytes (1 <= len <= 16), branch-free
+                        const uint32_t lc = min(len, 16u);
+                        const uint32_t l0 = min(lc, 8u), l1 = lc - l0;
+                        const uint64_t m0 = ~0ull >> (64u - 8u * l0);  // l0 >= 1
+                        const uint64_t m1 = l1 ? ~0ull >> (64u - 8u * l1) : 0ull;
+                        k0[u] = (((uint64_t)w1 << 32) | w0) & m0;
+                        k1[u] = (((uint64_t)w3 << 32) | w2) & m1;
+                        hh[u] = fold32((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
+                    }
+                    // words of more than 16 bytes: resolved by wc_long_kernel from the input (rare)
+                    if (__ballot(lng[0] || lng[1] || lng[2])) {  // rare: a global atomic, then drain
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++)
+                            if (lng[u]) list_append(t, cs - kBack + (e[u] & 0x3FFu));
+                        wait_vmem_all();
+                    }
+                    if constexpr ((mode & 4) != 0) {
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++) acc += ok[u] ? hh[u] : 0u;
+                        continue;
+                    }
+                    bool hit[kBatch];
+                    if (use_dict) {
+                        u32x4 A[kBatch], B[kBatch];
+                        uint32_t s1[kBatch], s2[kBatch];
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++) {
+                            dict_sets(hh[u], k1[u] != 0, s1[u], s2[u]);
+                            A[u] = dset[s1[u]];
+                            B[u] = dset[s2[u]];
+                        }
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++) {
+                            // short key: any of the 4 ways of its two sets; mid key: the single
+                            // 16-byte way of either set (kk = the word compared with each set's
+                            // second 8 bytes)
+                            const bool mid = k1[u] != 0;
+                            const uint64_t kk = mid ? k1[u] : k0[u];
+                            const uint64_t alo = ((uint64_t)A[u].y << 32) | A[u].x, ahi = ((uint64_t)A[u].w << 32) | A[u].z;
+                            const uint64_t blo = ((uint64_t)B[u].y << 32) | B[u].x, bhi = ((uint64_t)B[u].w << 32) | B[u].z;
+                            const bool a0 = alo == k0[u], a1 = ahi == kk, b0 = blo == k0[u], b1 = bhi == kk;
+                            const bool ha = mid ? (a0 && a1) : (a0 || a1);
+                            const bool hb = mid ? (b0 && b1) : (b0 || b1);
+                            hit[u] = ok[u] && (ha || hb);
+                            const uint32_t slot = ha ? 2 * s1[u] + (!mid && !a0) : 2 * s2[u] + (!mid && !b0);
+                            const uint32_t ci = hit[u] ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
+                            __hip_atomic_fetch_add(&dcnt[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    } else {
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++) hit[u] = false;
+                    }
+                    if constexpr ((mode & 16) != 0) {
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++) acc += hit[u];
+                        continue;
+                    }
+                    // misses: append to this workgroup's stream of the key's bucket
+                    uint32_t pos[kBatch];
+        #pragma unroll
+                    for (int u = 0; u < kBatch; u++) {
+                        const bool miss = ok[u] && !hit[u];
+                        const uint32_t b = spill_bucket(hh[u]);
+                        const uint32_t ci = miss ? (k1[u] == 0 ? b : (uint32_t)kSpillBuckets + b) : 2u * kSpillBuckets + lane;
+                        pos[u] = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                    bool over = false;
+#pragma unroll
+                    for (int u = 0; u < kBatch; u++) {
+                        // exactly two store instructions per word slot, every pass: lanes with
+                        // nothing to store get an out-of-range offset, which the range check
+                        // drops (the loop's VMEM count stays fixed, so its DMA waits are counted)
+                        const bool miss = ok[u] && !hit[u];
+                        const uint32_t b = spill_bucket(hh[u]);
+                        const bool small = k1[u] == 0;  // key of at most 8 bytes: 8-byte record
+                        const bool put8 = miss && small && pos[u] < sub8, put16 = miss && !small && pos[u] < sub;
+                        __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32)}, rs8,
+                                                              put8 ? (b * sub8 + pos[u]) * 8u : kOutOfRange, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(
+                            (u32x4){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32)},
+                            rs16, put16 ? (b * sub + pos[u]) * 16u : kOutOfRange, 0, 0);
+                        over |= miss && pos[u] >= (small ? sub8 : sub);
+                    }
+                    if (__ballot(over)) {  // a stream is full: count in the HBM table; the bucket then merges through it
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++) {
+                            const bool miss = ok[u] && !hit[u];
+                            if (miss && pos[u] >= (k1[u] == 0 ? sub8 : sub)) {
+                                short_insert(t, k0[u], k1[u], 1);
+                                t.bflag[spill_bucket(hh[u])] = 1u;
+                                ovf++;
+                            }
+                        }
+                        wait_vmem_all();
+                    }
+        
+                    if (pass != 0) wait_vmem_all();
                 }
             }
         }
         wave_sync();
-        cr = n1;
-        n1 = n2;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
+        dma_for_chunk(in, n, c + 2 * stride, lane, ring0 + kf * kSlotBytes);
     }
+    wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
 
     __syncthreads();
     unsigned long long spilled = 0, hits = 0;
@@ -679,7 +758,7 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(Recs r, const uint32_t
 
 // ------------------------------------------------------------ launchers
 uint32_t wc_map_grid(uint64_t n, int grid) {
-    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    const uint64_t nchunks = (n + kOwn - 1) / kOwn;
     uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
     if (g > (uint64_t)grid) g = (uint64_t)grid;
     if (g > (uint64_t)kMaxMapWGs) g = kMaxMapWGs;
@@ -687,7 +766,7 @@ uint32_t wc_map_grid(uint64_t n, int grid) {
 }
 
 void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode, hipStream_t s) {
-    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    const uint64_t nchunks = (n + kOwn - 1) / kOwn;
     if (nchunks == 0) return;
     const uint64_t g = wc_map_grid(n, grid);
     switch (mode) {

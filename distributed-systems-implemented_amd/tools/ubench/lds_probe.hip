@@ -2,6 +2,8 @@
 //  1. DPP wave_shr:1 / wave_shl:1 move a value one lane across the whole wave64.
 //  2. ds_read_b128 / ds_read_b64 at byte-unaligned LDS addresses return the
 //     right bytes, and what they cost relative to aligned reads.
+//  3. buffer_load_dwordx4 ... lds (LDS-DMA) with a range-checked descriptor:
+//     what a dword that straddles num_records returns.
 // Build: hipcc -O3 --offload-arch=gfx950 lds_probe.hip -o lds_probe
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -57,6 +59,17 @@ __global__ void __launch_bounds__(1024) lds_bw(unsigned* out, int iters, int shi
     if (acc == 0x12345) out[0] = acc;
 }
 
+__global__ void oob_test(const unsigned char* in, int nrec, unsigned* o) {
+    __shared__ unsigned char buf[1024];
+    for (int i = threadIdx.x; i < 1024; i += 64) buf[i] = 0xEE;
+    __syncthreads();
+    __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)in, (short)0, nrec, 0x00020000);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)buf, 16, threadIdx.x * 16, 0, 0, 0);
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    for (int i = threadIdx.x; i < 64; i += 64) o[i] = ((unsigned*)buf)[i];
+}
+
 int main() {
     unsigned* d;
     hipMalloc(&d, 1 << 20);
@@ -85,6 +98,21 @@ int main() {
     }
     printf("unaligned ds_read_b128/b64: %s\n", ok ? "OK" : "FAIL");
 
+    {
+        unsigned char* src;
+        hipMalloc(&src, 4096);
+        unsigned char hb[256];
+        for (int i = 0; i < 256; i++) hb[i] = (unsigned char)(i + 1);
+        hipMemcpy(src, hb, 256, hipMemcpyHostToDevice);
+        for (int nrec : {5, 6, 8, 17}) {
+            oob_test<<<1, 64>>>(src, nrec, d);
+            unsigned ho[64];
+            hipMemcpy(ho, d, sizeof(ho), hipMemcpyDeviceToHost);
+            printf("buffer-lds nrec=%d: bytes 0..23 =", nrec);
+            for (int i = 0; i < 24; i++) printf(" %02x", ((unsigned char*)ho)[i]);
+            printf("\n");
+        }
+    }
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);

@@ -33,7 +33,26 @@ def edge_cases() -> dict[str, list[bytes]]:
         "truncated_at_eof": [b"word \xe2\x82", b"x\xf0\x9f\x98"],
         "multi_file": [b"one two three\n", b"two three\n", b"three"],
         "apostrophes": [b"don't can't won't it's O'Neil rock'n'roll"],
+        # splits whose last bytes are a word, for every n % 4 (the map streams the
+        # split with range-checked 16-byte loads and patches its last n % 4 bytes)
+        "tail_bytes": [b"a", b"ab", b"abc", b"abcd", b"abcde", b"xy z", b"q r st", b"  uvw"],
+        # words of 1..20 letters at every offset around 944-byte chunk seams, 16-byte
+        # lanes and the 1 KiB windows, split lengths of every residue mod 4
+        "mixed_lengths": [mixed_words(n, seed) for seed, n in enumerate([12345, 7777, 2002, 945, 944, 943, 1889, 5000])],
     }
+
+
+def mixed_words(n: int, seed: int) -> bytes:
+    """Deterministic text of exactly n bytes ending in a letter: words of 1-20
+    letters (some longer than the 16-byte inline key) and 1-3 byte separators."""
+    rnd = random.Random(1000 + seed)
+    out = bytearray()
+    while len(out) < n:
+        out += bytes(rnd.choice(b"abcdefghijklmnopqrstuvwxyzABC") for _ in range(rnd.randint(1, 20)))
+        out += bytes(rnd.choice(b" \n,.;0") for _ in range(rnd.randint(1, 3)))
+    out = out[:n]
+    out[-1] = ord("z")
+    return bytes(out)
 
 
 def grep_edge_cases() -> dict[str, tuple[list[bytes], bytes]]:
