@@ -62,7 +62,8 @@ void reduce_ws_free(ReduceWs* w) {
     delete w;
 }
 
-// flags[0]: any long record, flags[1]: any k1 != 0, flags[2]: tied runs found
+// flags[0]: any long record, flags[1]: any k1 != 0, flags[2]: tied runs found.
+// One atomic per block at most (same-address atomics serialize).
 __global__ void rec_flags_kernel(Recs r, unsigned long long* flags) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     bool lng = false, k1 = false;
@@ -70,8 +71,10 @@ __global__ void rec_flags_kernel(Recs r, unsigned long long* flags) {
         lng |= r.len[i] > 16;
         k1 |= r.k1[i] != 0;
     }
-    if (__ballot(lng) && (threadIdx.x & 63) == 0) atomicOr(&flags[0], 1ull);
-    if (__ballot(k1) && (threadIdx.x & 63) == 0) atomicOr(&flags[1], 1ull);
+    lng = __syncthreads_or(lng);
+    k1 = __syncthreads_or(k1);
+    if (threadIdx.x == 0 && lng) atomicOr(&flags[0], 1ull);
+    if (threadIdx.x == 1 && k1) atomicOr(&flags[1], 1ull);
 }
 
 __global__ void iota_kernel(uint32_t* p, uint64_t n) {
@@ -125,7 +128,7 @@ __global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8
         uint8_t t = 0;
         if (i > 0 && same_prefix(r, perm[i - 1], perm[i])) t = 1;
         tie[i] = t;
-        if (t) atomicOr(&flags[2], 1ull);
+        if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
     }
 }
 
@@ -228,13 +231,19 @@ static inline unsigned grid_for(uint64_t n) {
         if (_e != hipSuccess) return (int)_e;     \
     } while (0)
 
+// rocPRIM's default radix sort runs a block sort + ~30 merge launches per sort
+// below 1 Mi items (its merge_sort_limit), which is exactly our size range
+// (~1e6 distinct keys); onesweep is several times faster there.
+using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config,
+                                               (size_t)64 * 1024>;
+
 template <class K>
 static int sort_pass(ReduceWs* ws, K* keys_in, K* keys_out, uint32_t* v_in, uint32_t* v_out, uint64_t n, unsigned bits,
                      hipStream_t s) {
     size_t tb = 0;
-    RCHK(rocprim::radix_sort_pairs(nullptr, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
+    RCHK(rocprim::radix_sort_pairs<OnesweepCfg>(nullptr, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
     RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::radix_sort_pairs(ws->tmp.p, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
+    RCHK(rocprim::radix_sort_pairs<OnesweepCfg>(ws->tmp.p, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
     return 0;
 }
 
@@ -294,7 +303,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     RCHK(ws->flags.ensure(64));
     unsigned long long* flags = ws->flags.as<unsigned long long>();
     RCHK(hipMemsetAsync(flags, 0, 64, s));
-    rec_flags_kernel<<<grid_for(n), 256, 0, s>>>(r, flags);
+    rec_flags_kernel<<<grid_for(n) < 512 ? grid_for(n) : 512, 256, 0, s>>>(r, flags);
     RCHK(hipMemcpyAsync(ws->h_pinned, flags, 24, hipMemcpyDeviceToHost, s));
     RCHK(ws->perm_a.ensure(n * 4));
     RCHK(ws->perm_b.ensure(n * 4));

@@ -34,7 +34,6 @@ namespace mrg {
 constexpr int kBatch = 3;                     // words per lane in flight
 constexpr int kBatchWords = kBatch * kWave;   // 192 words of a chunk per pass
 constexpr int kAggThreads = 512;
-constexpr int kAggSets = 960;                 // bucket aggregator (half the LDS: 2 workgroups per CU)
 
 // A chunk owns kOwn input bytes; its LDS slot is one 1 KiB DMA of the bytes
 // [start - 16, start + 1008): 16 bytes of look-back (lane 0), the 944 owned
@@ -128,12 +127,13 @@ __device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uin
     dma_chunk(raw_rsrc(in + (n > bo ? bo : 0), nrec), 16u * lane - e, lds_base);
 }
 
-template <uint32_t mode>
+template <uint32_t mode, int NW = kWavesPerWG>
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
                                                           Tables t, LetterTables lt) {
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
     // 1 = stream input only, 2 = tokenize only (no per-word work), 4 = per-word
-    // key extraction without the dictionary, 16 = no spill append (misses dropped)
+    // key extraction without the dictionary, 16 = no spill append (misses dropped),
+    // 32 = spill cursors but no stores
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -144,13 +144,15 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     if (t.dbg && tid == 0) t.dbg[2 * (kSpillBuckets + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
 
     const bool use_dict = t.dict != nullptr;
-    for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kThreads) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
-    for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kThreads) dcnt[i] = 0;
-    for (uint32_t b = tid; b < 2u * kSpillBuckets + kWave; b += kThreads) curs[b] = 0;
+    // NW (waves per workgroup) < kWavesPerWG only for the occupancy benchmark (map_mode 0x1000 / 0x2000)
+    constexpr uint32_t kT = NW * kWave;
+    for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kT) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
+    for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kT) dcnt[i] = 0;
+    for (uint32_t b = tid; b < 2u * kSpillBuckets + kWave; b += kT) curs[b] = 0;
     __syncthreads();
 
-    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
-    const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
+    const uint64_t stride = (uint64_t)gridDim.x * NW;
+    const uint64_t c0 = (uint64_t)blockIdx.x * NW + wv;
     const uint32_t sub = (uint32_t)t.sp.sub_keys, sub8 = (uint32_t)t.sp.sub8;
     // this workgroup's spill streams: [g][bucket][sub] (a workgroup's stores stay
     // within a few MiB, so they hit few TLB pages; mrgpu_internal.h Spill)
@@ -237,14 +239,13 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint32_t w = base + lane + 64u * u;
                         e[u] = list[w < total ? w : 0u];
                     }
-                    uint64_t d0[kBatch], d1[kBatch], d2[kBatch];
+                    // the 20 bytes [s & ~3, +20) of each key: five dword reads (the same LDS
+                    // cycles as three aligned 8-byte reads, without their 8-byte-phase selects)
+                    uint32_t g0[kBatch], g1[kBatch], g2[kBatch], g3[kBatch], g4[kBatch];
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        const uint32_t q = e[u] & 0x3FFu;
-                        const lds_u64* p8 = (const lds_u64*)(buf + (q & ~7u));
-                        d0[u] = p8[0];
-                        d1[u] = p8[1];
-                        d2[u] = p8[2];
+                        const lds_u32* p4 = (const lds_u32*)(buf + ((e[u] & 0x3FFu) & ~3u));
+                        g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
                     }
                     uint64_t k0[kBatch], k1[kBatch];
                     uint32_t hh[kBatch];
@@ -256,14 +257,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint32_t s = e[u] & 0x3FFu, len = e[u] >> 10;
                         ok[u] = valid && len <= 16;
                         lng[u] = valid && len > 16;
-                        // 16 key bytes at [q, q+16) from the three aligned 8-byte reads
-                        const uint32_t q = s;
-                        const bool r4 = (q & 4u) != 0;
-                        const uint32_t sh = q & 3u;
-                        const uint32_t D0 = (uint32_t)d0[u], D1 = (uint32_t)(d0[u] >> 32), D2 = (uint32_t)d1[u],
-                                       D3 = (uint32_t)(d1[u] >> 32), D4 = (uint32_t)d2[u], D5 = (uint32_t)(d2[u] >> 32);
-                        const uint32_t a0 = r4 ? D1 : D0, a1 = r4 ? D2 : D1, a2 = r4 ? D3 : D2, a3 = r4 ? D4 : D3,
-                                       a4 = r4 ? D5 : D4;
+                        // 16 key bytes at [s, s+16)
+                        const uint32_t sh = s & 3u;
+                        const uint32_t a0 = g0[u], a1 = g1[u], a2 = g2[u], a3 = g3[u], a4 = g4[u];
                         const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
                         const uint32_t w1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
                         const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sh);
@@ -334,6 +330,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint32_t ci = miss ? (k1[u] == 0 ? b : (uint32_t)kSpillBuckets + b) : 2u * kSpillBuckets + lane;
                         pos[u] = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
+                    if constexpr ((mode & 32) != 0) {
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++) acc += pos[u];
+                        continue;
+                    }
                     bool over = false;
 #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
@@ -376,123 +377,145 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 
     __syncthreads();
     unsigned long long spilled = 0, hits = 0;
-    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kThreads) {
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kT) {
         const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[kSpillBuckets + b], sub);
         t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x] = k;
         t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x] = k8;
         spilled += k + k8;
     }
     if (use_dict)
-        for (uint32_t i = tid; i < (uint32_t)kDictSlots; i += kThreads) {
+        for (uint32_t i = tid; i < (uint32_t)kDictSlots; i += kT) {
             const uint32_t v = dcnt[i];
             t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i] = v;
             hits += v;
         }
     if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
-    block_add4<kWavesPerWG>(&t.ctr->spilled, &t.ctr->dict_hits, &t.ctr->spill_ovf, &t.ctr->chunks_utf8, spilled, hits,
+    block_add4<NW>(&t.ctr->spilled, &t.ctr->dict_hits, &t.ctr->spill_ovf, &t.ctr->chunks_utf8, spilled, hits,
                             ovf, lane == 0 ? utf8_chunks : 0, L.red);
     if (t.dbg && tid == 0) t.dbg[2 * (kSpillBuckets + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
-// ------------------------------------------------------------ LDS hash table
-// 4-way set-associative table: the 4 k0 of a set are 32 contiguous bytes (two
-// ds_read_b128).  A way is claimed by CAS on its k0 (0 -> key), then k1 is
-// published (k1 == kUnwritten until then; 0xFF bytes never occur in UTF-8).
-template <int NSETS>
-struct alignas(16) STable {
-    unsigned long long k0[NSETS * 4];
-    unsigned long long k1[NSETS * 4];
-    uint32_t cnt[NSETS * 4];
+// ------------------------------------------------------------ bucket aggregator tables
+// Two LDS tables per bucket, both 4-way set-associative with two-choice sets:
+//   short keys (<= 8 bytes, k1 == 0): the 4 keys of a set are 32 contiguous
+//     bytes (two ds_read_b128); a way is claimed by CAS 0 -> key, which also
+//     publishes it, so a lookup is one LDS round trip;
+//   mid keys (9-16 bytes): a way is 16 bytes (k0, k1), a set 64 bytes (four
+//     ds_read_b128, one round trip); a way is claimed by CAS on k0, then k1 is
+//     published (kUnwritten until then; 0xFF bytes never occur in UTF-8).
+// Ways are never freed, so once a key's first set is full a key absent from it
+// can never appear there later: lookups and claims agree on the key's set.
+constexpr int kAggShortSets = 1024;  // 4096 short keys (a bucket holds ~1/512 of the split's distinct keys)
+constexpr int kAggMidSets = 256;     // 1024 mid keys
+constexpr uint32_t kAggWaves = kAggThreads / kWave;
+
+struct alignas(16) AggLds {
+    unsigned long long sk[kAggShortSets * 4];
+    unsigned long long mk[kAggMidSets * 4 * 2];  // way w of set s: mk[2(4s+w)] = k0, mk[2(4s+w)+1] = k1
+    uint32_t sc[kAggShortSets * 4 + kWave];      // counts (+ per-lane dummies for branch-free adds)
+    uint32_t mc[kAggMidSets * 4];
+    unsigned long long red[4 * kAggWaves + 4];   // block_add4 / block_alloc scratch
+    uint32_t nmiss;                              // keys appended to the bucket's miss list
 };
+static_assert(2 * sizeof(AggLds) <= 160 * 1024, "two aggregator workgroups per CU");
 
-// Count `add` occurrences of (k0,k1).  One probe, no loop: the key is looked up
-// in the first way of its set whose k0 matches.  Returns false (a miss: the
-// caller forwards the key, where it is still counted exactly) when that way
-// holds a different k1, is claimed but not yet published, when the key is
-// absent and its set is full, or when a claim CAS races — the table never waits
-// on another lane (see short_try).
-template <int NSETS>
-__device__ __forceinline__ bool st_lookup_add(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add,
-                                              uint32_t& base, uint32_t& empty, uint32_t& m_out) {
-    base = __umulhi(h, NSETS) * 4;
-    const u64x2 a = *(lds_u64x2*)(&T.k0[base]);
-    const u64x2 b = *(lds_u64x2*)(&T.k0[base + 2]);
-    const uint32_t m = (a.x == k0 ? 1u : 0u) | (a.y == k0 ? 2u : 0u) | (b.x == k0 ? 4u : 0u) | (b.y == k0 ? 8u : 0u);
-    const uint32_t z = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u) | (b.x == 0 ? 4u : 0u) | (b.y == 0 ? 8u : 0u);
-    const uint32_t slot = base + (__builtin_ctz(m | 16u) & 3u);
-    const uint64_t v = *(lds_u64*)(&T.k1[slot]);  // read unconditionally (way 0 when m == 0)
-    const bool hit = (m != 0) & (v == k1);
-    empty = m != 0 ? 0u : z;  // claimable ways, only when the key's k0 is absent from the set
-    m_out = m | (z << 4);     // 0: the key's k0 is absent and the set is full
-    if (hit) __hip_atomic_fetch_add((lds_u32*)&T.cnt[slot], add, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    return hit;
-}
-
-template <int NSETS>
-__device__ __forceinline__ bool st_claim(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t base, uint32_t empty,
-                                         uint32_t add) {
-    const uint32_t es = base + __builtin_ctz(empty);
-    if (atomicCAS(&T.k0[es], 0ull, (unsigned long long)k0) != 0ull) return false;
-    __hip_atomic_store(&T.k1[es], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    atomicAdd(&T.cnt[es], add);
-    return true;
-}
-
-// Two-choice insert (a key whose first set is full and does not hold its k0
-// lives in a second set).  Ways are never freed, so once the first set is full
-// a key absent from it can never appear there later — lookups and claims agree
-// on the key's set.
-// A lost claim CAS (another lane took the way first, often for the same key)
-// is retried once: the winner of this wave published its k1 in program order.
 __device__ __forceinline__ uint32_t second_hash(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 16) * 0xC2B2AE3Du; }
-
 template <int NSETS>
-__device__ __forceinline__ bool st_insert2(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
-    bool ok = false;
-    for (int attempt = 0; attempt < 2 && !ok; attempt++) {
-        uint32_t base, empty, m;
-        ok = st_lookup_add(T, k0, k1, h, add, base, empty, m);
-        if (empty != 0) {
-            ok = st_claim(T, k0, k1, base, empty, add);
-        } else if (m == 0) {  // first set full, key absent
-            ok = st_lookup_add(T, k0, k1, second_hash(h), add, base, empty, m);
-            if (empty != 0) ok = st_claim(T, k0, k1, base, empty, add);
-            else break;
-        } else {
-            break;  // k0 present with another k1 (or unpublished): a miss, no retry
+__device__ __forceinline__ uint32_t set_base(uint32_t h) { return __umulhi(h, NSETS) * 4; }
+
+// 4-bit masks of the ways of a short set holding k / holding 0
+__device__ __forceinline__ void short_set_masks(const AggLds& A, uint32_t base, uint64_t k, uint32_t& m, uint32_t& z) {
+    const u64x2 a = *(const lds_u64x2*)(&A.sk[base]);
+    const u64x2 b = *(const lds_u64x2*)(&A.sk[base + 2]);
+    m = (a.x == k ? 1u : 0u) | (a.y == k ? 2u : 0u) | (b.x == k ? 4u : 0u) | (b.y == k ? 8u : 0u);
+    z = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u) | (b.x == 0 ? 4u : 0u) | (b.y == 0 ? 8u : 0u);
+}
+
+// Slow path of a short key absent from the first read of its first set:
+// claim in the first set, else find/claim in the second.  A lost claim is
+// retried once (the winner, often the same key, published it with its CAS).
+// Returns false (a miss: the caller defers the key, where it is still counted
+// exactly) when both sets are full without the key or claims keep racing.
+__device__ bool short_insert_slow(AggLds& A, uint64_t k, uint32_t h, uint32_t add) {
+    for (int attempt = 0; attempt < 2; attempt++) {
+        for (int c = 0; c < 2; c++) {
+            const uint32_t base = set_base<kAggShortSets>(c == 0 ? h : second_hash(h));
+            uint32_t m, z;
+            short_set_masks(A, base, k, m, z);
+            if (m) {
+                atomicAdd(&A.sc[base + __builtin_ctz(m)], add);
+                return true;
+            }
+            if (z) {
+                const uint32_t w = base + __builtin_ctz(z);
+                const unsigned long long old = atomicCAS(&A.sk[w], 0ull, (unsigned long long)k);
+                if (old == 0ull || old == k) {
+                    atomicAdd(&A.sc[w], add);
+                    return true;
+                }
+                break;  // lost the way to another key: re-read from the first set
+            }
+            // set full without the key: the second set (after the first)
         }
     }
-    return ok;
+    return false;
 }
 
-// Exact lookup in a table no lane is claiming in any more (every way of both
-// candidate sets); -1 if absent.
-template <int NSETS>
-__device__ __forceinline__ int st_find_exact(STable<NSETS>& T, uint64_t k0, uint64_t k1, uint32_t h) {
+// Mid keys: way masks of a set (64 bytes, four b128 reads)
+__device__ __forceinline__ void mid_set_masks(const AggLds& A, uint32_t base, uint64_t k0, uint64_t k1, uint32_t& m,
+                                              uint32_t& z, uint32_t& pend) {
+    m = z = pend = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; w++) {
+        const u64x2 e = *(const lds_u64x2*)(&A.mk[2 * (base + w)]);
+        m |= (e.x == k0 && e.y == k1) ? 1u << w : 0u;
+        z |= e.x == 0 ? 1u << w : 0u;
+        pend |= (e.x == k0 && e.y == kUnwritten) ? 1u << w : 0u;  // claimed by this key's k0, k1 not yet visible
+    }
+}
+
+__device__ bool mid_insert(AggLds& A, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
+    for (int attempt = 0; attempt < 2; attempt++) {
+        for (int c = 0; c < 2; c++) {
+            const uint32_t base = set_base<kAggMidSets>(c == 0 ? h : second_hash(h));
+            uint32_t m, z, pend;
+            mid_set_masks(A, base, k0, k1, m, z, pend);
+            if (m) {
+                atomicAdd(&A.mc[base + __builtin_ctz(m)], add);
+                return true;
+            }
+            if (pend) break;  // a way of this k0 is being published: retry (or defer)
+            if (z) {
+                const uint32_t w = base + __builtin_ctz(z);
+                if (atomicCAS(&A.mk[2 * w], 0ull, (unsigned long long)k0) == 0ull) {
+                    __hip_atomic_store(&A.mk[2 * w + 1], (unsigned long long)k1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    atomicAdd(&A.mc[w], add);
+                    return true;
+                }
+                break;
+            }
+        }
+    }
+    return false;
+}
+
+// Exact lookups in tables no lane is claiming in any more; -1 if absent.
+__device__ __forceinline__ int short_find_exact(const AggLds& A, uint64_t k, uint32_t h) {
     for (int c = 0; c < 2; c++) {
-        const uint32_t base = __umulhi(c == 0 ? h : second_hash(h), NSETS) * 4;
+        const uint32_t base = set_base<kAggShortSets>(c == 0 ? h : second_hash(h));
         for (uint32_t w = 0; w < 4; w++)
-            if (T.k0[base + w] == k0 && T.k1[base + w] == k1) return (int)(base + w);
+            if (A.sk[base + w] == k) return (int)(base + w);
     }
     return -1;
 }
-
-template <int NSETS>
-__device__ __forceinline__ void st_init(STable<NSETS>& T, uint32_t tid, uint32_t nthreads) {
-    for (uint32_t i = tid; i < (uint32_t)NSETS * 4; i += nthreads) {
-        T.k0[i] = 0;
-        T.k1[i] = kUnwritten;
-        T.cnt[i] = 0;
+__device__ __forceinline__ int mid_find_exact(const AggLds& A, uint64_t k0, uint64_t k1, uint32_t h) {
+    for (int c = 0; c < 2; c++) {
+        const uint32_t base = set_base<kAggMidSets>(c == 0 ? h : second_hash(h));
+        for (uint32_t w = 0; w < 4; w++)
+            if (A.mk[2 * (base + w)] == k0 && A.mk[2 * (base + w) + 1] == k1) return (int)(base + w);
     }
+    return -1;
 }
-
-struct alignas(16) AggLds {
-    STable<kAggSets> T;
-    unsigned long long red[4 * (kAggThreads / 64) + 4];  // block_add4 / block_alloc scratch
-    uint32_t spre[kMaxMapWGs + 4];  // exclusive prefix of the stream lengths of the pool being walked
-    uint32_t nmiss;               // keys appended to the bucket's miss list
-};
-static_assert(2 * sizeof(AggLds) <= 160 * 1024, "two aggregator workgroups per CU");
 
 // Write record o (distinct short key with its total) of t.out.
 __device__ __forceinline__ void put_short(const Tables& t, unsigned long long o, uint64_t k0, uint64_t k1, uint64_t cnt,
@@ -511,91 +534,113 @@ __device__ __forceinline__ void put_short(const Tables& t, unsigned long long o,
 }
 
 // ------------------------------------------------------------ bucket aggregation
-// The bucket's nwg streams (one per map workgroup) are walked as one sequence
-// of kAggGroup-record groups with the next group's loads in flight while the
-// current one is inserted.
+// Wave w walks streams w, w + kAggWaves, ... of the bucket (one stream per map
+// workgroup), each contiguously: blocks of kAggUnroll * 64 records, the next
+// block's loads in flight while the current one is counted.  Every record of a
+// block is looked up in one LDS round trip (all the block's set reads issued
+// together); hits add (a per-lane dummy counter for lanes without one), and
+// only first occurrences and collisions take the claim path.
 constexpr uint32_t kAggUnroll = 4;
-constexpr uint32_t kAggGroup = kAggUnroll * kAggThreads;
+constexpr uint32_t kAggBlock = kAggUnroll * kWave;
 
-__device__ __forceinline__ void agg_load(const uint4* blk, uint32_t i, uint32_t f, uint4& r) {
-    r = i < f ? blk[i] : make_uint4(0, 0, 0, 0);
-}
-__device__ __forceinline__ void agg_load(const uint64_t* blk, uint32_t i, uint32_t f, uint4& r) {
-    const uint64_t k = i < f ? blk[i] : 0;
-    r = make_uint4((uint32_t)k, (uint32_t)(k >> 32), 0, 0);
-}
-
-template <uint32_t amode, typename Rec>
-__device__ __forceinline__ void agg_streams(AggLds& A, const Tables& t, const Rec* pool, const uint32_t* gcounts,
-                                            uint64_t gstride, bool keep_miss, uint64_t& miss) {
-    const uint32_t nwg = t.sp.nwg, tid = threadIdx.x;
-    // Exclusive prefix of the stream lengths in LDS: record v of the bucket's
-    // virtual concatenation of streams lives in stream g, pre[g] <= v < pre[g+1],
-    // so a group of kAggGroup records may span many short streams.
-    __syncthreads();
-    if (tid < 64) {
-        constexpr int kPer = kMaxMapWGs / 64;
-        uint32_t c[kPer], sum = 0;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            const uint32_t idx = tid * kPer + k;
-            c[k] = idx < nwg ? gcounts[idx] : 0u;
-            sum += c[k];
-        }
-        uint32_t incl = sum;
-#pragma unroll
-        for (int off = 1; off < 64; off <<= 1) {
-            const uint32_t y = __shfl_up(incl, off);
-            if (tid >= (uint32_t)off) incl += y;
-        }
-        uint32_t run = incl - sum;
-#pragma unroll
-        for (int k = 0; k < kPer; k++) {
-            A.spre[tid * kPer + k] = run;
-            run += c[k];
-        }
-        if (tid == 63) A.spre[kMaxMapWGs] = incl;
+__device__ __forceinline__ void defer_miss(AggLds& A, const Tables& t, uint64_t k0, uint64_t k1, bool keep_miss,
+                                           uint64_t& miss) {
+    const uint32_t pos = atomicAdd(&A.nmiss, 1u);  // no HBM round trip in the loop
+    if (keep_miss) {
+        if (pos < t.sp.amiss_cap)
+            t.sp.amiss[(uint64_t)blockIdx.x * t.sp.amiss_cap + pos] =
+                make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+        else
+            short_insert(t, k0, k1, 1);
     }
-    __syncthreads();
-    const uint32_t total = A.spre[kMaxMapWGs];
-    uint32_t gc = 0;  // this thread's stream cursor (its record indices only grow)
-    auto load = [&](uint32_t v, uint4& r) {
-        if (v < total) {
-            while (A.spre[gc + 1] <= v) gc++;
-            agg_load(pool + (uint64_t)gc * gstride, v - A.spre[gc], 0xFFFFFFFFu, r);
-        } else {
-            r = make_uint4(0, 0, 0, 0);
+    miss++;
+}
+
+template <uint32_t amode, bool kMid>
+__device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void* pool_b, const uint32_t* gcounts,
+                                         uint64_t gstride, bool keep_miss, uint64_t& miss) {
+    const uint32_t nwg = t.sp.nwg, lane = threadIdx.x & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // wave-uniform cursor: stream g, record offset off within it (cnt records)
+    uint32_t g = wv, off = 0, cnt = g < nwg ? gcounts[g] : 0u;
+    auto skip_empty = [&]() {
+        while (g < nwg && off >= cnt) {
+            g += kAggWaves;
+            off = 0;
+            cnt = g < nwg ? gcounts[g] : 0u;
         }
     };
+    skip_empty();
     uint4 cur[kAggUnroll], nxt[kAggUnroll];
-#pragma unroll
-    for (uint32_t u = 0; u < kAggUnroll; u++) load(u * kAggThreads + tid, cur[u]);
-    for (uint32_t G = 0; G < total; G += kAggGroup) {
-#pragma unroll
-        for (uint32_t u = 0; u < kAggUnroll; u++) load(G + kAggGroup + u * kAggThreads + tid, nxt[u]);
+    auto load = [&](uint32_t gg, uint32_t o, uint32_t c, uint4* r) {
 #pragma unroll
         for (uint32_t u = 0; u < kAggUnroll; u++) {
-            const uint4 k = cur[u];
-            if ((k.x | k.y) != 0) {  // else past the end (keys have k0 != 0)
-                const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
-                const uint32_t h = fold32(k.x, k.y, k.z, k.w);
-                if constexpr ((amode & 128) != 0) {
-                    miss += h;
-                } else if (!st_insert2(A.T, k0, k1, h, 1)) {
-                    const uint32_t pos = atomicAdd(&A.nmiss, 1u);  // defer: no HBM round trip in the loop
-                    if (keep_miss) {
-                        if (pos < t.sp.amiss_cap)
-                            t.sp.amiss[(uint64_t)blockIdx.x * t.sp.amiss_cap + pos] =
-                                make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-                        else
-                            short_insert(t, k0, k1, 1);
-                    }
-                    miss++;
+            const uint32_t i = o + u * kWave + lane;
+            if (gg < nwg && i < c) {
+                if constexpr (kMid) {
+                    r[u] = ((const uint4*)pool_b)[(uint64_t)gg * gstride + i];
+                } else {
+                    const uint64_t k = ((const uint64_t*)pool_b)[(uint64_t)gg * gstride + i];
+                    r[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), 0, 0);
+                }
+            } else {
+                r[u] = make_uint4(0, 0, 0, 0);
+            }
+        }
+    };
+    load(g, off, cnt, cur);
+    while (g < nwg) {
+        // next block's position and loads
+        uint32_t g2 = g, off2 = off + kAggBlock, cnt2 = cnt;
+        while (g2 < nwg && off2 >= cnt2) {
+            g2 += kAggWaves;
+            off2 = 0;
+            cnt2 = g2 < nwg ? gcounts[g2] : 0u;
+        }
+        load(g2, off2, cnt2, nxt);
+        uint32_t h[kAggUnroll];
+#pragma unroll
+        for (uint32_t u = 0; u < kAggUnroll; u++) h[u] = fold32(cur[u].x, cur[u].y, cur[u].z, cur[u].w);
+        if constexpr ((amode & 128) != 0) {
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) miss += h[u];
+        } else if constexpr (!kMid) {
+            uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                base[u] = set_base<kAggShortSets>(h[u]);
+                short_set_masks(A, base[u], ((uint64_t)cur[u].y << 32) | cur[u].x, m[u], z[u]);
+            }
+            bool slow[kAggUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
+                const bool hit = valid && m[u] != 0;
+                slow[u] = valid && m[u] == 0;
+                const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)kAggShortSets * 4 + lane;
+                __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                if (slow[u]) {
+                    const uint64_t k = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                    if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, miss);
+                }
+            }
+        } else {
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                if ((cur[u].x | cur[u].y) != 0) {
+                    const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                    if (!mid_insert(A, k0, k1, h[u], 1)) defer_miss(A, t, k0, k1, keep_miss, miss);
                 }
             }
         }
 #pragma unroll
         for (uint32_t u = 0; u < kAggUnroll; u++) cur[u] = nxt[u];
+        g = g2;
+        off = off2;
+        cnt = cnt2;
     }
 }
 
@@ -606,17 +651,23 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
     __shared__ AggLds A;
     const uint32_t tid = threadIdx.x;
     if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    st_init(A.T, tid, kAggThreads);
+    for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4 + kWave; i += kAggThreads) A.sc[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) A.sk[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kAggThreads) {
+        A.mk[2 * i] = 0;
+        A.mk[2 * i + 1] = kUnwritten;
+        A.mc[i] = 0;
+    }
     if (tid == 0) A.nmiss = 0;
     __syncthreads();
     const uint64_t b = blockIdx.x;
     const bool keep_miss = emit != 2;
     uint64_t miss = 0;
     // bucket b's stream of workgroup g: pool[(g * kSpillBuckets + b) * sub]
-    agg_streams<amode>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg, (uint64_t)kSpillBuckets * t.sp.sub8,
-                       keep_miss, miss);
-    agg_streams<amode>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
-                       (uint64_t)kSpillBuckets * t.sp.sub_keys, keep_miss, miss);
+    agg_pool<amode, false>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg,
+                           (uint64_t)kSpillBuckets * t.sp.sub8, keep_miss, miss);
+    agg_pool<amode, true>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
+                          (uint64_t)kSpillBuckets * t.sp.sub_keys, keep_miss, miss);
     __syncthreads();
     const uint32_t nm = min(A.nmiss, t.sp.amiss_cap);
     // merge: a key of this bucket went to the HBM table from the map kernel
@@ -624,9 +675,13 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
     // key may be on both sides: merge the whole bucket through the HBM table.
     const bool merge = emit == 0 || (emit == 1 && (t.bflag[b] != 0 || A.nmiss > t.sp.amiss_cap));
     if (merge) {
-        for (uint32_t i = tid; i < (uint32_t)kAggSets * 4; i += kAggThreads) {
-            const uint64_t k0 = A.T.k0[i];
-            if (k0 != 0) short_insert(t, k0, A.T.k1[i], A.T.cnt[i]);
+        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) {
+            const uint64_t k0 = A.sk[i];
+            if (k0 != 0) short_insert(t, k0, 0, A.sc[i]);
+        }
+        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kAggThreads) {
+            const uint64_t k0 = A.mk[2 * i];
+            if (k0 != 0) short_insert(t, k0, A.mk[2 * i + 1], A.mc[i]);
         }
         for (uint32_t i = tid; i < nm; i += kAggThreads) {  // deferred misses, all lanes in flight
             const uint4 k = t.sp.amiss[b * t.sp.amiss_cap + i];
@@ -634,29 +689,41 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
         }
         if (tid == 0) atomicAdd(&t.ctr->bflush, 1ull);
     } else {
-        // Deferred misses: counted in the (now stable) table when their key is
-        // there, otherwise in the HBM table — so the table's keys and the HBM
-        // table's keys of this bucket are disjoint and the table is emitted as is.
+        // Deferred misses: counted in the (now stable) tables when their key is
+        // there, otherwise in the HBM table — so the tables' keys and the HBM
+        // table's keys of this bucket are disjoint and the tables are emitted as is.
         if (emit == 1)
             for (uint32_t i = tid; i < nm; i += kAggThreads) {
                 const uint4 k = t.sp.amiss[b * t.sp.amiss_cap + i];
                 const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
-                const int slot = st_find_exact(A.T, k0, k1, fold32(k.x, k.y, k.z, k.w));
-                if (slot >= 0) atomicAdd(&A.T.cnt[slot], 1u);
-                else short_insert(t, k0, k1, 1);
+                const uint32_t h = fold32(k.x, k.y, k.z, k.w);
+                if (k1 == 0) {
+                    const int slot = short_find_exact(A, k0, h);
+                    if (slot >= 0) atomicAdd(&A.sc[slot], 1u);
+                    else short_insert(t, k0, k1, 1);
+                } else {
+                    const int slot = mid_find_exact(A, k0, k1, h);
+                    if (slot >= 0) atomicAdd(&A.mc[slot], 1u);
+                    else short_insert(t, k0, k1, 1);
+                }
             }
         __syncthreads();
         // one cursor allocation per workgroup, then each thread writes its keys
         uint32_t mine = 0;
-        for (uint32_t i = tid; i < (uint32_t)kAggSets * 4; i += kAggThreads) mine += A.T.k0[i] != 0;
-        unsigned long long o = block_alloc<kAggThreads / 64>(&t.ctr->nrec, mine, A.red);
-        for (uint32_t i = tid; i < (uint32_t)kAggSets * 4; i += kAggThreads) {
-            const uint64_t k0 = A.T.k0[i];
-            if (k0 != 0) put_short(t, o++, k0, A.T.k1[i], A.T.cnt[i], emit == 1);
+        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) mine += A.sk[i] != 0;
+        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kAggThreads) mine += A.mk[2 * i] != 0;
+        unsigned long long o = block_alloc<kAggWaves>(&t.ctr->nrec, mine, A.red);
+        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) {
+            const uint64_t k0 = A.sk[i];
+            if (k0 != 0) put_short(t, o++, k0, 0, A.sc[i], emit == 1);
+        }
+        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kAggThreads) {
+            const uint64_t k0 = A.mk[2 * i];
+            if (k0 != 0) put_short(t, o++, k0, A.mk[2 * i + 1], A.mc[i], emit == 1);
         }
     }
     if (amode != 0 && miss == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // no DCE in ablation builds
-    block_add4<kAggThreads / 64>(&t.ctr->agg_miss, nullptr, nullptr, nullptr, amode == 0 ? miss : 0, 0, 0, 0, A.red);
+    block_add4<kAggWaves>(&t.ctr->agg_miss, nullptr, nullptr, nullptr, amode == 0 ? miss : 0, 0, 0, 0, A.red);
     if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -772,8 +839,11 @@ void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     switch (mode) {
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
-        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16)
+        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32)
 #undef MRG_MAP_MODE
+        // occupancy benchmark: 8 or 12 waves per workgroup (results stay exact)
+        case 0x1000: wc_map_kernel<0, 8><<<(unsigned)g, 8 * kWave, 0, s>>>(in, n, nchunks, t, lt); break;
+        case 0x2000: wc_map_kernel<0, 12><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, nchunks, t, lt); break;
         default: wc_map_kernel<0><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
     }
 }

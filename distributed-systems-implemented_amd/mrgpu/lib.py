@@ -23,7 +23,8 @@ except Exception:  # pragma: no cover - torch is optional for the C ABI itself
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD_DIR = os.path.join(PKG_DIR, "build")
-LIB_PATH = os.path.join(BUILD_DIR, "libmrgpu.so")
+# MRGPU_LIB: another build of the same library (A/B timing of kernel variants)
+LIB_PATH = os.environ.get("MRGPU_LIB") or os.path.join(BUILD_DIR, "libmrgpu.so")
 
 MRG_OK = 0
 MRG_APP_WC = 1
