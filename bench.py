@@ -180,6 +180,7 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    log("map kernel ms per timed step: " + " ".join(f"{k:.2f}" for k in kern_ms))
 
     t_max = elapsed
     if world > 1:

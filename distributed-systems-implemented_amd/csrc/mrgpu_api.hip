@@ -17,6 +17,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -28,9 +29,78 @@ using namespace mrg;
 
 namespace {
 
+// Freed device blocks kept for reuse (parts record arrays and arenas): a map
+// task's parts adopt the context's record buffer instead of copying it, and the
+// next task takes a cached block instead of hipMalloc — hipFree would also
+// synchronize the device.  Process-wide (contexts may live on several threads).
+namespace {
+struct CachedBlock {
+    int dev;
+    void* p;
+    size_t bytes;
+};
+std::mutex g_cache_mu;
+std::vector<CachedBlock> g_cache;
+constexpr size_t kCacheBlocks = 8;
+}  // namespace
+
+// A cached block of `dev` with at least `bytes` (the smallest such), or nullptr.
+static void* cache_take(int dev, size_t bytes, size_t* got) {
+    std::lock_guard<std::mutex> g(g_cache_mu);
+    size_t best = g_cache.size();
+    for (size_t i = 0; i < g_cache.size(); i++)
+        if (g_cache[i].dev == dev && g_cache[i].bytes >= bytes && (best == g_cache.size() || g_cache[i].bytes < g_cache[best].bytes))
+            best = i;
+    if (best == g_cache.size()) return nullptr;
+    void* p = g_cache[best].p;
+    *got = g_cache[best].bytes;
+    g_cache.erase(g_cache.begin() + best);
+    return p;
+}
+
+static void cache_put(int dev, void* p, size_t bytes) {
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> g(g_cache_mu);
+        if (g_cache.size() < kCacheBlocks) {
+            g_cache.push_back({dev, p, bytes});
+            return;
+        }
+    }
+    hipFree(p);
+}
+
+// Cached block or a fresh allocation (the caller has bound `dev`).
+static hipError_t block_alloc(int dev, size_t bytes, void** p, size_t* got) {
+    if ((*p = cache_take(dev, bytes, got))) return hipSuccess;
+    *got = bytes;
+    return hipMalloc(p, bytes);
+}
+
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    // Like ensure(), but a missing buffer comes from the block cache (buffers
+    // that are handed over to parts objects: recbuf, recarena).
+    hipError_t ensure_cached(size_t n, int dev) {
+        if (n <= cap) return hipSuccess;
+        if (p) cache_put(dev, p, cap);
+        p = nullptr;
+        cap = 0;
+        size_t got = 0;
+        hipError_t e = block_alloc(dev, n < 4096 ? 4096 : n, &p, &got);
+        if (e == hipSuccess) cap = got;
+        else p = nullptr;
+        return e;
+    }
+    // The buffer changes owner (a parts object): this one is empty afterwards.
+    void* adopt(size_t* bytes) {
+        void* q = p;
+        *bytes = cap;
+        p = nullptr;
+        cap = 0;
+        return q;
+    }
     hipError_t ensure(size_t n) {
         if (n <= cap) return hipSuccess;
         if (p) hipFree(p);
@@ -94,6 +164,7 @@ struct mrg_parts {
     Recs r{};
     void* block = nullptr;  // record arrays
     uint8_t* arena = nullptr;
+    size_t block_bytes = 0, arena_bytes = 0;  // returned to the block cache on free
 };
 
 static int fail(mrg_ctx* c, int code, const char* fmt, ...) {
@@ -231,10 +302,14 @@ static int parts_alloc(mrg_ctx* c, uint64_t n, uint64_t arena_n, int app, uint32
     p->device = c->device;
     uint64_t cap = n ? n : 1;
     size_t bytes = cap * (8 + 8 + 4 + 8 + 4 + 8) + 256;
-    hipError_t e = hipMalloc(&p->block, bytes);
+    hipError_t e = block_alloc(c->device, bytes, &p->block, &p->block_bytes);
     if (e != hipSuccess) { delete p; return fail(c, MRG_ENOMEM, "hipMalloc(%zu) for parts failed", bytes); }
-    e = hipMalloc((void**)&p->arena, arena_n ? arena_n : 16);
-    if (e != hipSuccess) { hipFree(p->block); delete p; return fail(c, MRG_ENOMEM, "hipMalloc arena failed"); }
+    e = block_alloc(c->device, arena_n ? arena_n : 16, (void**)&p->arena, &p->arena_bytes);
+    if (e != hipSuccess) {
+        cache_put(c->device, p->block, p->block_bytes);
+        delete p;
+        return fail(c, MRG_ENOMEM, "hipMalloc arena failed");
+    }
     char* b = (char*)p->block;
     p->r.k0 = (uint64_t*)b; b += cap * 8;
     p->r.k1 = (uint64_t*)b; b += cap * 8;
@@ -290,7 +365,8 @@ static int grow_on_overflow(mrg_ctx* c, uint32_t st) {
 }
 
 static int ensure_recbuf(mrg_ctx* c) {
-    HCHK(c, c->recbuf.ensure(c->rec_cap * 40));
+    HCHK(c, c->recbuf.ensure_cached(c->rec_cap * 40, c->device));
+    HCHK(c, c->recarena.ensure_cached(16, c->device));
     return MRG_OK;
 }
 
@@ -434,36 +510,35 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         if ((rc = read_counters(c))) return rc;
         if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
         const uint64_t nlist = c->h_ctr->nlist;
-        launch_wc_long(in, len, t, lt, nlist, c->s);
-        HCHK(c, hipGetLastError());
+        if (nlist) {  // words > 16 bytes
+            launch_wc_long(in, len, t, lt, nlist, c->s);
+            HCHK(c, hipGetLastError());
+        }
         HCHK(c, hipEventRecord(c->ev[2], c->s));
-        if ((rc = read_counters(c))) return rc;
+        if (nlist && (rc = read_counters(c))) return rc;
         Counters h = *c->h_ctr;
         if (h.status & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", h.status);
         if (grow_on_overflow(c, h.status & (kStShortFull | kStLongFull | kStRecFull))) continue;
-        HCHK(c, c->recarena.ensure(h.long_bytes + 16));
-        t.out = rec_view(c);
+        if (h.long_bytes + 16 > c->recarena.cap) {  // the arena is written by collect below
+            HCHK(c, c->recarena.ensure_cached(h.long_bytes + 16, c->device));
+            t.out = rec_view(c);
+        }
         if ((h.short_used || h.long_used) && launch_collect(t, c->rws, h.nrec, h.short_used, h.long_used != 0, c->s))
             return fail(c, MRG_EDEVICE, "collect failed");
-        if ((rc = read_counters(c))) return rc;
+        if ((h.short_used || h.long_used) && (rc = read_counters(c))) return rc;
         h = *c->h_ctr;
         if (grow_on_overflow(c, h.status & kStRecFull)) continue;
-        const uint64_t n = h.nrec;
-        mrg_parts* p = nullptr;
-        if ((rc = parts_alloc(c, n, h.long_bytes, MRG_APP_WC, nreduce, &p))) return rc;
-        const Recs& s = t.out;
-        hipError_t e = hipSuccess;
-        auto cp = [&](void* d, const void* src, size_t b) {
-            if (e == hipSuccess && b) e = hipMemcpyAsync(d, src, b, hipMemcpyDeviceToDevice, c->s);
-        };
-        cp(p->r.k0, s.k0, n * 8);
-        cp(p->r.k1, s.k1, n * 8);
-        cp(p->r.cnt, s.cnt, n * 8);
-        cp(p->r.koff, s.koff, n * 8);
-        cp(p->r.len, s.len, n * 4);
-        cp(p->r.part, s.part, n * 4);
-        cp(p->r.arena, s.arena, h.long_bytes);
-        if (e != hipSuccess) { mrg_parts_free(p); return fail(c, MRG_EDEVICE, "record copy: %s", hipGetErrorString(e)); }
+        // the parts object takes over the record buffer and arena (no copy); the
+        // next map task gets cached blocks
+        mrg_parts* p = new mrg_parts();
+        p->app = MRG_APP_WC;
+        p->nreduce = nreduce;
+        p->device = c->device;
+        p->r = t.out;
+        p->r.n = h.nrec;
+        p->r.arena_n = h.long_bytes;
+        p->block = c->recbuf.adopt(&p->block_bytes);
+        p->arena = (uint8_t*)c->recarena.adopt(&p->arena_bytes);
         HCHK(c, hipEventRecord(c->ev[3], c->s));
         HCHK(c, hipEventSynchronize(c->ev[3]));
         c->stats.map_kernel_ms = ev_ms(c->ev[0], c->ev[1]);
@@ -476,7 +551,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         c->stats.spill_ovf = h.spill_ovf;
         c->stats.agg_miss = h.agg_miss;
         c->stats.dict_hits = h.dict_hits;
-        c->stats.distinct_keys = n;
+        c->stats.distinct_keys = h.nrec;
         c->stats.long_keys = h.nlong_rec;
         *out = p;
         return MRG_OK;
@@ -690,8 +765,8 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
 void mrg_parts_free(mrg_parts* p) {
     if (!p) return;
     hipSetDevice(p->device);
-    if (p->block) hipFree(p->block);
-    if (p->arena) hipFree(p->arena);
+    cache_put(p->device, p->block, p->block_bytes);
+    cache_put(p->device, p->arena, p->arena_bytes);
     delete p;
 }
 
@@ -732,10 +807,13 @@ int mrg_parts_merge(mrg_ctx* c, mrg_parts* into, const mrg_parts* from) {
     if ((rc = bind(c))) return rc;
     mrg_parts* m = nullptr;
     if ((rc = aggregate(c, {into->r, from->r}, into->app, into->nreduce, &m))) return rc;
-    hipFree(into->block);
-    hipFree(into->arena);
+    // aggregate() has synchronized the stream: into's old blocks are idle
+    cache_put(into->device, into->block, into->block_bytes);
+    cache_put(into->device, into->arena, into->arena_bytes);
     into->block = m->block;
+    into->block_bytes = m->block_bytes;
     into->arena = m->arena;
+    into->arena_bytes = m->arena_bytes;
     into->r = m->r;
     m->block = nullptr;
     m->arena = nullptr;
@@ -1005,10 +1083,8 @@ int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     HCHK(c, hipMemcpyAsync(rmeta.p, hsrc.data(), 16 * P, hipMemcpyHostToDevice, c->s));
     mrg_parts* tmp = nullptr;
     if ((rc = parts_alloc(c, rrec, 0, local->app, local->nreduce, &tmp))) return rc;
-    hipFree(tmp->arena);
-    tmp->arena = (uint8_t*)rar_b.p;  // adopt the received arena
-    rar_b.p = nullptr;
-    rar_b.cap = 0;
+    cache_put(c->device, tmp->arena, tmp->arena_bytes);  // nothing has used it yet
+    tmp->arena = (uint8_t*)rar_b.adopt(&tmp->arena_bytes);  // adopt the received arena
     tmp->r.arena = tmp->arena;
     tmp->r.arena_n = rar;
     if (rrec)

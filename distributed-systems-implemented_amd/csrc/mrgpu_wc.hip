@@ -535,13 +535,12 @@ __device__ __forceinline__ void put_short(const Tables& t, unsigned long long o,
 
 // ------------------------------------------------------------ bucket aggregation
 // Wave w walks streams w, w + kAggWaves, ... of the bucket (one stream per map
-// workgroup), each contiguously: blocks of kAggUnroll * 64 records, the next
+// workgroup), each contiguously: blocks of kAggUnroll * 64 records (8 per lane
+// for 8-byte records, 4 for 16-byte ones), the next
 // block's loads in flight while the current one is counted.  Every record of a
 // block is looked up in one LDS round trip (all the block's set reads issued
 // together); hits add (a per-lane dummy counter for lanes without one), and
 // only first occurrences and collisions take the claim path.
-constexpr uint32_t kAggUnroll = 4;
-constexpr uint32_t kAggBlock = kAggUnroll * kWave;
 
 __device__ __forceinline__ void defer_miss(AggLds& A, const Tables& t, uint64_t k0, uint64_t k1, bool keep_miss,
                                            uint64_t& miss) {
@@ -556,31 +555,34 @@ __device__ __forceinline__ void defer_miss(AggLds& A, const Tables& t, uint64_t 
     miss++;
 }
 
-template <uint32_t amode, bool kMid>
+template <uint32_t amode, bool kMid, uint32_t kAggUnroll>
 __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void* pool_b, const uint32_t* gcounts,
                                          uint64_t gstride, bool keep_miss, uint64_t& miss) {
+    constexpr uint32_t kAggBlock = kAggUnroll * kWave;
+    static_assert(kMaxMapWGs <= kAggWaves * kWave, "a wave's stream counts fit one VGPR");
     const uint32_t nwg = t.sp.nwg, lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // wave-uniform cursor: stream g, record offset off within it (cnt records)
-    uint32_t g = wv, off = 0, cnt = g < nwg ? gcounts[g] : 0u;
-    auto skip_empty = [&]() {
-        while (g < nwg && off >= cnt) {
-            g += kAggWaves;
-            off = 0;
-            cnt = g < nwg ? gcounts[g] : 0u;
-        }
-    };
-    skip_empty();
+    // The wave's streams are wv + kAggWaves * j, j < js; lane j holds stream j's
+    // record count, so moving to the next stream is a readlane, not a load.
+    const uint32_t js = nwg > wv ? (nwg - wv + kAggWaves - 1) / kAggWaves : 0u;
+    const uint32_t vcnt = lane < js ? gcounts[wv + kAggWaves * lane] : 0u;
+    // wave-uniform cursor: stream j, record offset off within it (cnt records)
+    uint32_t j = 0, off = 0, cnt = __builtin_amdgcn_readlane(vcnt, 0);
+    while (j < js && off >= cnt) {
+        j++;
+        cnt = j < js ? __builtin_amdgcn_readlane(vcnt, j) : 0u;
+    }
     uint4 cur[kAggUnroll], nxt[kAggUnroll];
-    auto load = [&](uint32_t gg, uint32_t o, uint32_t c, uint4* r) {
+    auto load = [&](uint32_t jj, uint32_t o, uint32_t c, uint4* r) {
+        const uint64_t row = (uint64_t)(wv + kAggWaves * jj) * gstride;
 #pragma unroll
         for (uint32_t u = 0; u < kAggUnroll; u++) {
             const uint32_t i = o + u * kWave + lane;
-            if (gg < nwg && i < c) {
+            if (jj < js && i < c) {
                 if constexpr (kMid) {
-                    r[u] = ((const uint4*)pool_b)[(uint64_t)gg * gstride + i];
+                    r[u] = ((const uint4*)pool_b)[row + i];
                 } else {
-                    const uint64_t k = ((const uint64_t*)pool_b)[(uint64_t)gg * gstride + i];
+                    const uint64_t k = ((const uint64_t*)pool_b)[row + i];
                     r[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), 0, 0);
                 }
             } else {
@@ -588,16 +590,16 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
             }
         }
     };
-    load(g, off, cnt, cur);
-    while (g < nwg) {
+    load(j, off, cnt, cur);
+    while (j < js) {
         // next block's position and loads
-        uint32_t g2 = g, off2 = off + kAggBlock, cnt2 = cnt;
-        while (g2 < nwg && off2 >= cnt2) {
-            g2 += kAggWaves;
+        uint32_t j2 = j, off2 = off + kAggBlock, cnt2 = cnt;
+        while (j2 < js && off2 >= cnt2) {
+            j2++;
             off2 = 0;
-            cnt2 = g2 < nwg ? gcounts[g2] : 0u;
+            cnt2 = j2 < js ? __builtin_amdgcn_readlane(vcnt, j2) : 0u;
         }
-        load(g2, off2, cnt2, nxt);
+        load(j2, off2, cnt2, nxt);
         uint32_t h[kAggUnroll];
 #pragma unroll
         for (uint32_t u = 0; u < kAggUnroll; u++) h[u] = fold32(cur[u].x, cur[u].y, cur[u].z, cur[u].w);
@@ -638,7 +640,7 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
         }
 #pragma unroll
         for (uint32_t u = 0; u < kAggUnroll; u++) cur[u] = nxt[u];
-        g = g2;
+        j = j2;
         off = off2;
         cnt = cnt2;
     }
@@ -664,9 +666,9 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
     const bool keep_miss = emit != 2;
     uint64_t miss = 0;
     // bucket b's stream of workgroup g: pool[(g * kSpillBuckets + b) * sub]
-    agg_pool<amode, false>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg,
+    agg_pool<amode, false, 8>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg,
                            (uint64_t)kSpillBuckets * t.sp.sub8, keep_miss, miss);
-    agg_pool<amode, true>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
+    agg_pool<amode, true, 4>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
                           (uint64_t)kSpillBuckets * t.sp.sub_keys, keep_miss, miss);
     __syncthreads();
     const uint32_t nm = min(A.nmiss, t.sp.amiss_cap);
