@@ -139,6 +139,10 @@ def main():
     if world > 1:
         dist.init_process_group("gloo")  # control plane only; the shuffle is RCCL inside libmrgpu
     torch.cuda.set_device(local)
+    # torch initializes its CUDA runtime lazily on first use; do it now, so it can
+    # never overlap a timed step (seen: one 57 ms map kernel in the first step)
+    torch.zeros(1, device=f"cuda:{local}").add_(1)
+    torch.cuda.synchronize()
 
     t0 = time.time()
     host = gen_corpus(rank, args.file_mb, args.files, seed_base=2)

@@ -144,7 +144,7 @@ void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s);
 void launch_sample_gather(const uint8_t* in, uint64_t n, uint64_t win, uint64_t stride, uint32_t nwin, uint8_t* dst,
                           hipStream_t s);
 // Build the dictionary image from sample records ordered by descending count.
-void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* dict, hipStream_t s);
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s);
 // Sort keys for the dictionary build: ~count (u32) of each record.
 void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t s);
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
@@ -173,7 +173,7 @@ int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64
                       uint32_t** d_count, hipStream_t s);
 // Stable radix sort of (u32 key, u32 value) pairs; result in k_out / v_out.
 int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, uint64_t n,
-                   hipStream_t s);
+                   unsigned bits, hipStream_t s);
 // Compact recs with part == p (or owner rank) into dst (device), returns count on host.
 int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst_host_desc, hipStream_t s);
 

@@ -115,30 +115,39 @@ __device__ int rec_cmp(const Recs& r, uint32_t a, uint32_t b) {
     return (la > lb) - (la < lb);
 }
 
-__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b) {
-    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && r.k1[a] == r.k1[b];
+__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b, bool with_k1) {
+    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && (!with_k1 || r.k1[a] == r.k1[b]);
 }
 
-// tie[i] = 1 when sorted position i has the same (part, 16-byte prefix) as i-1:
-// distinct keys with equal zero-padded prefixes (a key > 16 bytes, or a grep
-// line with NUL bytes) are only ordered by a full bytewise comparison.
-__global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8_t* tie, unsigned long long* flags) {
+// tie[i] = 1 when sorted position i has the same (part, prefix) as i-1, the
+// prefix being the first 8 key bytes (sorted without the k1 pass) or all 16:
+// distinct keys with equal zero-padded prefixes are only ordered by a full
+// bytewise comparison.
+__global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8_t* tie, unsigned long long* flags,
+                                 bool with_k1) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint8_t t = 0;
-        if (i > 0 && same_prefix(r, perm[i - 1], perm[i])) t = 1;
+        if (i > 0 && same_prefix(r, perm[i - 1], perm[i], with_k1)) t = 1;
         tie[i] = t;
         if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
     }
 }
 
-// Insertion sort of each tied run by full bytewise comparison (runs are tiny in practice).
-__global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_t* tie) {
+// Insertion sort of each tied run by full bytewise comparison.  A run longer
+// than max_run is left alone and flags[3] set: the caller then sorts with the
+// k1 pass (16-byte prefixes), whose ties are only keys > 16 bytes.
+__global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_t* tie, uint64_t max_run,
+                                unsigned long long* flags) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
         if (tie[i] || !tie[i + 1]) continue;
         uint64_t e = i + 1;
-        while (e < n && tie[e]) e++;
+        while (e < n && tie[e] && e - i <= max_run) e++;
+        if (e - i > max_run) {
+            atomicOr(&flags[3], 1ull);
+            continue;
+        }
         for (uint64_t a = i + 1; a < e; a++) {
             uint32_t v = perm[a];
             uint64_t b = a;
@@ -269,8 +278,8 @@ int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64
 }
 
 int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, uint64_t n,
-                   hipStream_t s) {
-    return sort_pass<uint32_t>(ws, k_in, k_out, v_in, v_out, n, 32, s);
+                   unsigned bits, hipStream_t s) {
+    return sort_pass<uint32_t>(ws, k_in, k_out, v_in, v_out, n, bits, s);
 }
 
 int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst, hipStream_t s) {
@@ -315,7 +324,6 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
 
     uint32_t* pa = ws->perm_a.as<uint32_t>();
     uint32_t* pb = ws->perm_b.as<uint32_t>();
-    iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
     auto pass32 = [&](int which, unsigned bits) -> int {
         gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, nullptr, ws->key_a.as<uint32_t>());
         int e = sort_pass<uint32_t>(ws, ws->key_a.as<uint32_t>(), ws->key_b.as<uint32_t>(), pa, pb, n, bits, s);
@@ -328,18 +336,39 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         std::swap(pa, pb);
         return e;
     };
-    int e;
-    if (has_k1 && (e = pass64(1))) return e;
-    if ((e = pass64(2))) return e;
-    if (all && nreduce > 1) {
-        unsigned bits = 1;
-        while ((1ull << bits) < nreduce) bits++;
-        if ((e = pass32(3, bits))) return e;
-    }
-    if (has_long || app != 1) {
+    // Stable LSD passes: (k1), k0, partition.  The k1 pass (bytes 8-15) is
+    // skipped at first: keys that share their first 8 bytes form short tied runs
+    // that fix_ties orders by full comparison; if a run is long (many keys with
+    // one 8-byte prefix), everything is sorted again with the k1 pass.
+    auto sort_all = [&](bool with_k1) -> int {
+        int e;
+        iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
+        if (with_k1 && (e = pass64(1))) return e;
+        if ((e = pass64(2))) return e;
+        if (all && nreduce > 1) {
+            unsigned bits = 1;
+            while ((1ull << bits) < nreduce) bits++;
+            if ((e = pass32(3, bits))) return e;
+        }
+        return 0;
+    };
+    auto fix_ties = [&](bool with_k1, uint64_t max_run) {
         uint8_t* tie = ws->key_a.as<uint8_t>();
-        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags);
-        fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie);
+        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1);
+        fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, max_run, flags);
+    };
+    int e;
+    if ((e = sort_all(false))) return e;
+    if (has_k1 || has_long || app != 1) {
+        fix_ties(false, has_k1 ? 64 : ~0ull);
+        if (has_k1) {
+            RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 3, 8, hipMemcpyDeviceToHost, s));
+            RCHK(hipStreamSynchronize(s));
+            if (ws->h_pinned[3]) {  // a long run of one 8-byte prefix: sort with the k1 pass
+                if ((e = sort_all(true))) return e;
+                fix_ties(true, ~0ull);
+            }
+        }
     }
     uint64_t* ll = ws->key_b.as<uint64_t>();
     uint64_t* off = ws->lineoff.as<uint64_t>();

@@ -103,13 +103,18 @@ __device__ __forceinline__ i32x4 raw_rsrc(const void* base, uint32_t nrec) {
     return (i32x4){(int)(uint32_t)b, (int)((uint32_t)(b >> 32) & 0xFFFFu), (int)nrec, 0x00020000};
 }
 // 64 lanes x 16 B: lane l's bytes at rsrc + voff -> LDS [lds_base + 16 l]
+template <bool kNT = false>
 __device__ __forceinline__ void dma_chunk(i32x4 rsrc, uint32_t voff, uint32_t lds_base) {
     // operands are wave-uniform; readfirstlane puts them in SGPRs for the asm "s" constraints
     rsrc = (i32x4){__builtin_amdgcn_readfirstlane(rsrc.x), __builtin_amdgcn_readfirstlane(rsrc.y),
                    __builtin_amdgcn_readfirstlane(rsrc.z), __builtin_amdgcn_readfirstlane(rsrc.w)};
     lds_base = __builtin_amdgcn_readfirstlane(lds_base);
-    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
-                 : "memory", "m0");
+    if constexpr (kNT)  // non-temporal: the input stream does not push spill lines out of L2
+        asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
+                     : "memory", "m0");
+    else
+        asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
+                     : "memory", "m0");
 }
 __device__ __forceinline__ void wait_vmem_iter() {
     static_assert(kVmemPerIter == 7, "update the immediate");
@@ -118,13 +123,14 @@ __device__ __forceinline__ void wait_vmem_iter() {
 __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Issue the DMA of chunk c (any c: chunks past the split read as zeros).
+template <bool kNT = false>
 __device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uint64_t c, uint32_t lane, uint32_t lds_base) {
     const uint64_t cs = c * kOwn;
     const uint64_t bo = cs >= 16 ? cs - 16 : 0;    // descriptor base (input offset)
     const uint32_t e = (uint32_t)(bo + 16 - cs);   // 16 for the split's first chunk, else 0
     const uint64_t rem = n > bo ? n - bo : 0;
     const uint32_t nrec = rem > 0x7FFFFF00ull ? 0x7FFFFF00u : (uint32_t)rem;
-    dma_chunk(raw_rsrc(in + (n > bo ? bo : 0), nrec), 16u * lane - e, lds_base);
+    dma_chunk<kNT>(raw_rsrc(in + (n > bo ? bo : 0), nrec), 16u * lane - e, lds_base);
 }
 
 template <uint32_t mode, int NW = kWavesPerWG>
@@ -133,7 +139,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
     // 1 = stream input only, 2 = tokenize only (no per-word work), 4 = per-word
     // key extraction without the dictionary, 16 = no spill append (misses dropped),
-    // 32 = spill cursors but no stores
+    // 32 = spill cursors but no stores; 0x100 (exact) = non-temporal input loads
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -166,9 +172,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     const uint32_t ring0 = lds_addr(L.ring[wv][0]);
 
     // prologue: chunk c0 landed before the loop, chunk c0 + stride in flight
-    dma_for_chunk(in, n, c0, lane, ring0);
+    dma_for_chunk<(mode & 0x100) != 0>(in, n, c0, lane, ring0);
     wait_vmem_all();
-    dma_for_chunk(in, n, c0 + stride, lane, ring0 + kSlotBytes);
+    dma_for_chunk<(mode & 0x100) != 0>(in, n, c0 + stride, lane, ring0 + kSlotBytes);
     uint32_t k = 0;  // ring slot of the current chunk
     for (uint64_t c = c0; c < nchunks; c += stride, k = k == kRing - 1 ? 0 : k + 1) {
         wait_vmem_iter();  // chunk c's DMA (issued two iterations ago) has landed
@@ -371,7 +377,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         }
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
-        dma_for_chunk(in, n, c + 2 * stride, lane, ring0 + kf * kSlotBytes);
+        dma_for_chunk<(mode & 0x100) != 0>(in, n, c + 2 * stride, lane, ring0 + kf * kSlotBytes);
     }
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
 
@@ -782,15 +788,31 @@ __global__ void dict_keys_kernel(Recs r, uint32_t* keys, uint32_t* idx) {
     const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += gs) {
         const uint64_t c = r.cnt[i];
-        keys[i] = ~(uint32_t)(c > 0xFFFFFFFFull ? 0xFFFFFFFFull : c);  // ascending sort = descending count
+        // 16-bit key, ascending = descending count (counts >= 65535 tie: the few
+        // hottest keys, placed first in any order); a 16-bit sort is 2 passes
+        keys[i] = 0xFFFFu - (uint32_t)(c > 0xFFFFull ? 0xFFFFull : c);
         idx[i] = (uint32_t)i;
     }
 }
 
-// One workgroup places the sample's keys in descending-count order, 1024 at a
-// time, each into the first of its two sets with a free way; a key whose two
-// sets are full stays out (it is then counted through the spill path).
-__global__ void __launch_bounds__(1024) dict_build_kernel(Recs r, const uint32_t* order, uint64_t n, uint4* dict) {
+// Candidates in descending-count order, gathered densely (the placement below is
+// one workgroup; here every gather is in flight at once): {k0, k1}, or zeros for
+// keys the dictionary cannot hold (long keys).
+constexpr uint64_t kDictCands = 4ull * kDictSlots;
+__global__ void dict_cands_kernel(Recs r, const uint32_t* order, uint64_t lim, uint4* cand) {
+    const uint64_t gs = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < lim; i += gs) {
+        const uint32_t j = order[i];
+        const uint64_t k0 = r.k0[j], k1 = r.k1[j];
+        cand[i] = r.koff[j] == ~0ull ? make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32))
+                                     : make_uint4(0, 0, 0, 0);
+    }
+}
+
+// One workgroup places the candidates in order, 1024 at a time, each into the
+// first of its two sets with a free way; a key whose two sets are full stays out
+// (it is then counted through the spill path).
+__global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uint64_t lim, uint4* dict) {
     __shared__ uint4 S[kDictSets];
     __shared__ uint32_t fill[kDictSets];
     const uint32_t tid = threadIdx.x;
@@ -799,25 +821,23 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(Recs r, const uint32_t
         fill[i] = 0;
     }
     __syncthreads();
-    const uint64_t lim = n < (uint64_t)4 * kDictSlots ? n : (uint64_t)4 * kDictSlots;
+    uint4 nx = tid < lim ? cand[tid] : make_uint4(0, 0, 0, 0);
     for (uint64_t base = 0; base < lim; base += 1024) {
-        const uint64_t i = base + tid;
-        if (i < lim) {
-            const uint32_t j = order[i];
-            const uint64_t k0 = r.k0[j], k1 = r.k1[j];
-            if (r.koff[j] == ~0ull && k0 != 0) {
-                const bool mid = k1 != 0;
-                const uint32_t h = fold32((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-                uint32_t s1, s2;
-                dict_sets(h, mid, s1, s2);
-                const uint32_t ways = mid ? 1u : 2u;
-                uint32_t s = s1, w = atomicAdd(&fill[s1], 1u);
-                if (w >= ways) { s = s2; w = atomicAdd(&fill[s2], 1u); }
-                if (w < ways) {
-                    if (mid) S[s] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-                    else if (w == 0) { S[s].x = (uint32_t)k0; S[s].y = (uint32_t)(k0 >> 32); }
-                    else { S[s].z = (uint32_t)k0; S[s].w = (uint32_t)(k0 >> 32); }
-                }
+        const uint4 c = nx;
+        const uint64_t i2 = base + 1024 + tid;  // next round's candidate, in flight during this one
+        nx = i2 < lim ? cand[i2] : make_uint4(0, 0, 0, 0);
+        const uint64_t k0 = ((uint64_t)c.y << 32) | c.x, k1 = ((uint64_t)c.w << 32) | c.z;
+        if (k0 != 0) {
+            const bool mid = k1 != 0;
+            uint32_t s1, s2;
+            dict_sets(fold32(c.x, c.y, c.z, c.w), mid, s1, s2);
+            const uint32_t ways = mid ? 1u : 2u;
+            uint32_t s = s1, w = atomicAdd(&fill[s1], 1u);
+            if (w >= ways) { s = s2; w = atomicAdd(&fill[s2], 1u); }
+            if (w < ways) {
+                if (mid) S[s] = c;
+                else if (w == 0) { S[s].x = c.x; S[s].y = c.y; }
+                else { S[s].z = c.x; S[s].w = c.y; }
             }
         }
         __syncthreads();
@@ -841,7 +861,7 @@ void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     switch (mode) {
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
-        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32)
+        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32) MRG_MAP_MODE(0x100)
 #undef MRG_MAP_MODE
         // occupancy benchmark: 8 or 12 waves per workgroup (results stay exact)
         case 0x1000: wc_map_kernel<0, 8><<<(unsigned)g, 8 * kWave, 0, s>>>(in, n, nchunks, t, lt); break;
@@ -871,8 +891,11 @@ void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t 
     if (r.n) dict_keys_kernel<<<512, 256, 0, s>>>(r, keys, idx);
 }
 
-void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* dict, hipStream_t s) {
-    dict_build_kernel<<<1, 1024, 0, s>>>(r, order, n, dict);
+// cand: scratch for kDictCands uint4
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s) {
+    const uint64_t lim = n < kDictCands ? n : kDictCands;
+    if (lim) dict_cands_kernel<<<(unsigned)((lim + 255) / 256), 256, 0, s>>>(r, order, lim, cand);
+    dict_build_kernel<<<1, 1024, 0, s>>>(cand, lim, dict);
 }
 
 }  // namespace mrg

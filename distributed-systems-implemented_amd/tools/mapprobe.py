@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--modes", default="1,2,4,0")
     ap.add_argument("--grids", default="0")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--opt", action="append", default=[], help="context option name=value (repeatable)")
     a = ap.parse_args()
     nfiles = max(1, int(a.gb * 4))
     voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
@@ -31,6 +32,9 @@ def main():
     buf = np.empty(sum(sizes), dtype=np.uint8)
     voc.fill_files(sizes, [2 + i for i in range(nfiles)], C.wc_params(), out=buf)
     ctx = Context(0)
+    for o in a.opt:
+        k, v = o.split("=")
+        ctx.set_option(k, int(v))
     d = ctx.device_alloc(buf.size)
     for off in range(0, buf.size, 1 << 30):
         n = min(1 << 30, buf.size - off)
@@ -48,7 +52,8 @@ def main():
                 p.free()
             r = {"grid": g, "mode": m, "map_kernel_ms": min(ts), "GBps": buf.size / min(ts) / 1e6,
                  "map_total_ms": st["map_total_ms"], "agg_ms": st["agg_ms"], "long_ms": st["long_ms"],
-                 "collect_ms": st["collect_ms"], "spilled": st["lds_overflow"], "agg_miss": st["agg_miss"]}
+                 "collect_ms": st["collect_ms"], "spilled": st["lds_overflow"], "agg_miss": st["agg_miss"],
+                 "dict_ms": st["dict_ms"], "dict_hits": st["dict_hits"]}
             print(json.dumps(r), flush=True)
             res.append(r)
     ctx.set_option("map_mode", 0)

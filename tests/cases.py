@@ -39,6 +39,10 @@ def edge_cases() -> dict[str, list[bytes]]:
         # words of 1..20 letters at every offset around 944-byte chunk seams, 16-byte
         # lanes and the 1 KiB windows, split lengths of every residue mod 4
         "mixed_lengths": [mixed_words(n, seed) for seed, n in enumerate([12345, 7777, 2002, 945, 944, 943, 1889, 5000])],
+        # > 64 distinct keys with one 8-byte prefix: the reduce's long tied run (sort
+        # falls back to the k1 pass), plus prefix-of-another-key orderings
+        "shared_prefix": [b" ".join(b"abcdefgh" + bytes([97 + i % 26, 97 + i // 26 % 26]) * (1 + i % 3)
+                                    for i in range(600)) + b" abcdefgh abcdefg abcdefghi"],
     }
 
 
