@@ -632,7 +632,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "spill_stream_keys")) c->spill_force_sub = v > 0 ? v : 0;
     else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
     else if (!strcmp(name, "dict_min_bytes")) c->dict_min_bytes = v > 0 ? (uint64_t)v : (32ull << 20);
-    else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (64ull << 20);
+    else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);
     else if (!strcmp(name, "rec_cap")) c->rec_cap = v > 0 ? (uint64_t)v : (1u << 21);
     else return fail(c, MRG_EINVAL, "unknown option %s", name);
     return MRG_OK;
