@@ -253,7 +253,9 @@ static int ensure_spill(mrg_ctx* c, uint64_t n) {
     sub = (sub + 63) & ~63ull;
     uint64_t sub8 = 2 * sub;
     if (c->spill_force_sub > 0) sub = sub8 = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
-    if (sub8 >= (1ull << 31)) sub = sub8 = (1ull << 31);  // in-stream positions are 32-bit
+    // stream offsets are 24-bit products in the map kernel (b * sub): 2^23 records per
+    // (workgroup, bucket) stream is a 1 TB split at 8 B per record and 512 streams
+    if (sub8 >= (1ull << 23)) return fail(c, MRG_EINVAL, "split too large for the spill layout (%llu bytes)", (unsigned long long)n);
     c->spill_nwg = nwg;
     c->spill_sub_keys = sub;
     c->spill_sub8 = sub8;
@@ -432,7 +434,7 @@ static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win
     clear_for_run(c, t);
     // the spill layout was sized for the split's workgroup count (ensure_spill): never launch more
     const uint32_t g = wc_map_grid(sn, (int)c->spill_nwg);
-    launch_wc_map((const uint8_t*)c->sample.p, sn, t, lt, (int)g, 0, c->s);
+    if (!launch_wc_map((const uint8_t*)c->sample.p, sn, t, lt, (int)g, 0, c->s)) return fail(c, MRG_EINVAL, "sample too large");
     launch_wc_agg(t, c->map_mode & 512, 2, c->s);
     if (with_dict) launch_dict_emit(t, g, c->s);
     HCHK(c, hipGetLastError());
@@ -502,7 +504,8 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         t.out_cap = c->rec_cap;
         clear_for_run(c, t);
         HCHK(c, hipEventRecord(c->ev[0], c->s));
-        launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s);
+        if (!launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s))
+            return fail(c, MRG_EINVAL, "split too large for 32-bit chunk indices (%llu bytes)", (unsigned long long)len);
         HCHK(c, hipEventRecord(c->ev[1], c->s));
         print_stamps(c, "map", nwg, kSpillBuckets);
         launch_wc_agg(t, c->map_mode, 1, c->s);

@@ -133,7 +133,7 @@ struct LetterTables {
 void clear_tables(const Tables& t, bool short_table, hipStream_t s);
 // ---- wc pipeline (mrgpu_wc.hip) ----
 uint32_t wc_map_grid(uint64_t n, int grid);
-void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode,
+bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode,
                    hipStream_t s);
 // emit: 0 = flush every bucket table into the HBM table (legacy),
 //       1 = emit records directly unless the bucket overflowed (then merge through HBM),

@@ -52,6 +52,7 @@ struct alignas(16) MapLds {
     // spill cursors: [0, 512) 8-byte streams, [512, 1024) 16-byte streams, then per-lane dummies for hits
     uint32_t curs[2 * kSpillBuckets + kWave];
     unsigned long long red[4 * kWavesPerWG];    // block_add4 scratch
+    uint4 kmask[17];                            // kmask[len]: the first len of 16 key bytes
 };
 static_assert(sizeof(MapLds) <= 160 * 1024, "map LDS budget");
 
@@ -123,19 +124,23 @@ __device__ __forceinline__ void wait_vmem_iter() {
 __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // Issue the DMA of chunk c (any c: chunks past the split read as zeros).
+// cs = the chunk's first owned byte (chunk index * kOwn)
 template <bool kNT = false>
-__device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uint64_t c, uint32_t lane, uint32_t lds_base) {
-    const uint64_t cs = c * kOwn;
-    const uint64_t bo = cs >= 16 ? cs - 16 : 0;    // descriptor base (input offset)
-    const uint32_t e = (uint32_t)(bo + 16 - cs);   // 16 for the split's first chunk, else 0
-    const uint64_t rem = n > bo ? n - bo : 0;
-    const uint32_t nrec = rem > 0x7FFFFF00ull ? 0x7FFFFF00u : (uint32_t)rem;
-    dma_chunk<kNT>(raw_rsrc(in + (n > bo ? bo : 0), nrec), 16u * lane - e, lds_base);
+// The descriptor base is the window start rounded down to 1 GiB (a chunk's
+// window never crosses its base's range), so this is 32-bit scalar arithmetic.
+// For the split's first chunk the base is 0 and lane 0's offset (-16) wraps past
+// the range: its look-back reads zeros, like everything at or past n.
+__device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uint64_t cs, uint32_t lane, uint32_t lds_base) {
+    const uint64_t base = cs == 0 ? 0 : ((cs - kBack) & ~((1ull << 30) - 1));
+    const uint64_t r = n - base;  // bytes from the base to the end of the split (wraps if base >= n)
+    const uint32_t rhi = (uint32_t)(r >> 32), rlo = (uint32_t)r;
+    const uint32_t nrec = (int32_t)rhi < 0 ? 0u : (rhi != 0 || rlo > 0xFFFFFF00u) ? 0xFFFFFF00u : rlo;
+    dma_chunk<kNT>(raw_rsrc(in + base, nrec), (uint32_t)(cs - base) - kBack + 16u * lane, lds_base);
 }
 
 template <uint32_t mode, int NW = kWavesPerWG>
-__global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
-                                                          Tables t, LetterTables lt) {
+__global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t nchunks,
+                                                          uint32_t ctail, Tables t, LetterTables lt) {
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
     // 1 = stream input only, 2 = tokenize only (no per-word work), 4 = per-word
     // key extraction without the dictionary, 16 = no spill append (misses dropped),
@@ -147,6 +152,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     lds_uint4* dset = (lds_uint4*)L.dset;
     lds_u32* dcnt = (lds_u32*)L.dcnt;
     lds_u32* curs = (lds_u32*)L.curs;
+    const lds_uint4* kmask4 = (const lds_uint4*)L.kmask;
     if (t.dbg && tid == 0) t.dbg[2 * (kSpillBuckets + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
 
     const bool use_dict = t.dict != nullptr;
@@ -155,10 +161,15 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kT) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
     for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kT) dcnt[i] = 0;
     for (uint32_t b = tid; b < 2u * kSpillBuckets + kWave; b += kT) curs[b] = 0;
+    if (tid < 17 * 4) {  // byte masks: dword d of kmask[len] keeps clamp(len - 4d, 0, 4) bytes
+        const int nb = min(max((int)(tid >> 2) - 4 * (int)(tid & 3), 0), 4);
+        ((uint32_t*)L.kmask)[tid] = nb == 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
+    }
     __syncthreads();
 
-    const uint64_t stride = (uint64_t)gridDim.x * NW;
-    const uint64_t c0 = (uint64_t)blockIdx.x * NW + wv;
+    // chunk indices are 32-bit (the launcher checks): scalar compares, no 64-bit VALU ones
+    const uint32_t stride = gridDim.x * NW;
+    const uint32_t c0 = blockIdx.x * NW + wv;
     const uint32_t sub = (uint32_t)t.sp.sub_keys, sub8 = (uint32_t)t.sp.sub8;
     // this workgroup's spill streams: [g][bucket][sub] (a workgroup's stores stay
     // within a few MiB, so they hit few TLB pages; mrgpu_internal.h Spill)
@@ -172,18 +183,20 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     const uint32_t ring0 = lds_addr(L.ring[wv][0]);
 
     // prologue: chunk c0 landed before the loop, chunk c0 + stride in flight
-    dma_for_chunk<(mode & 0x100) != 0>(in, n, c0, lane, ring0);
+    // byte offsets advance by addition (64-bit scalar multiplies per iteration are not free)
+    const uint64_t cstep = (uint64_t)stride * kOwn;
+    dma_for_chunk<(mode & 0x100) != 0>(in, n, (uint64_t)c0 * kOwn, lane, ring0);
     wait_vmem_all();
-    dma_for_chunk<(mode & 0x100) != 0>(in, n, c0 + stride, lane, ring0 + kSlotBytes);
+    dma_for_chunk<(mode & 0x100) != 0>(in, n, (uint64_t)c0 * kOwn + cstep, lane, ring0 + kSlotBytes);
     uint32_t k = 0;  // ring slot of the current chunk
-    for (uint64_t c = c0; c < nchunks; c += stride, k = k == kRing - 1 ? 0 : k + 1) {
+    uint64_t cs = (uint64_t)c0 * kOwn;  // the current chunk's first own byte = slot byte 16 (slot byte i = input cs - 16 + i)
+    for (uint32_t c = c0; c < nchunks; c += stride, cs += cstep, k = k == kRing - 1 ? 0 : k + 1) {
         wait_vmem_iter();  // chunk c's DMA (issued two iterations ago) has landed
-        const uint64_t cs = c * kOwn;  // the chunk's first own byte = slot byte 16 (slot byte i = input cs - 16 + i)
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
         lds_uint4* b4 = (lds_uint4*)buf;
         const uint32_t kf = k == 0 ? kRing - 1 : k - 1;  // free slot: the word list now, chunk c + 2*stride next
         lds_u16* list = (lds_u16*)L.ring[wv][kf];
-        if ((n & 3) && (int64_t)cs - kBack + kSlotBytes > (int64_t)(n & ~3ull)) {
+        if (c >= ctail) {  // the window reaches the split's last n % 4 bytes (ctail = ~0u: none)
             // the split's last n % 4 bytes sit in a dword the range check zero-filled
             const int64_t p = (int64_t)(n & ~3ull) + lane - ((int64_t)cs - kBack);
             if (lane < (uint32_t)(n & 3) && p >= 0 && p < kSlotBytes) buf[p] = in[(n & ~3ull) + lane];
@@ -248,10 +261,12 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     // the 20 bytes [s & ~3, +20) of each key: five dword reads (the same LDS
                     // cycles as three aligned 8-byte reads, without their 8-byte-phase selects)
                     uint32_t g0[kBatch], g1[kBatch], g2[kBatch], g3[kBatch], g4[kBatch];
+                    u32x4 km[kBatch];  // the key's byte mask, from the length (same round trip)
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         const lds_u32* p4 = (const lds_u32*)(buf + ((e[u] & 0x3FFu) & ~3u));
                         g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
+                        km[u] = kmask4[min(e[u] >> 10, 16u)];
                     }
                     uint64_t k0[kBatch], k1[kBatch];
                     uint32_t hh[kBatch];
@@ -261,8 +276,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint32_t w = base + lane + 64u * u;
                         const bool valid = w < total;
                         const uint32_t s = e[u] & 0x3FFu, len = e[u] >> 10;
-                        ok[u] = valid && len <= 16;
-                        lng[u] = valid && len > 16;
+                        ok[u] = valid & (len <= 16);
+                        lng[u] = valid & (len > 16);
                         // 16 key bytes at [s, s+16)
                         const uint32_t sh = s & 3u;
                         const uint32_t a0 = g0[u], a1 = g1[u], a2 = g2[u], a3 = g3[u], a4 = g4[u];
@@ -270,13 +285,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint32_t w1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
                         const uint32_t w2 = __builtin_amdgcn_alignbyte(a3, a2, sh);
                         const uint32_t w3 = __builtin_amdgcn_alignbyte(a4, a3, sh);
-                        // keep the first len bytes (1 <= len <= 16), branch-free
-                        const uint32_t lc = min(len, 16u);
-                        const uint32_t l0 = min(lc, 8u), l1 = lc - l0;
-                        const uint64_t m0 = ~0ull >> (64u - 8u * l0);  // l0 >= 1
-                        const uint64_t m1 = l1 ? ~0ull >> (64u - 8u * l1) : 0ull;
-                        k0[u] = (((uint64_t)w1 << 32) | w0) & m0;
-                        k1[u] = (((uint64_t)w3 << 32) | w2) & m1;
+                        // keep the first min(len, 16) bytes
+                        k0[u] = ((uint64_t)(w1 & km[u].y) << 32) | (w0 & km[u].x);
+                        k1[u] = ((uint64_t)(w3 & km[u].w) << 32) | (w2 & km[u].z);
                         hh[u] = fold32((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
                     }
                     // words of more than 16 bytes: resolved by wc_long_kernel from the input (rare)
@@ -292,6 +303,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         continue;
                     }
                     bool hit[kBatch];
+                    uint64_t mHit[kBatch], mOk[kBatch];  // lane masks of hit[], ok[]
                     if (use_dict) {
                         u32x4 A[kBatch], B[kBatch];
                         uint32_t s1[kBatch], s2[kBatch];
@@ -310,30 +322,51 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             const uint64_t kk = mid ? k1[u] : k0[u];
                             const uint64_t alo = ((uint64_t)A[u].y << 32) | A[u].x, ahi = ((uint64_t)A[u].w << 32) | A[u].z;
                             const uint64_t blo = ((uint64_t)B[u].y << 32) | B[u].x, bhi = ((uint64_t)B[u].w << 32) | B[u].z;
-                            const bool a0 = alo == k0[u], a1 = ahi == kk, b0 = blo == k0[u], b1 = bhi == kk;
-                            const bool ha = mid ? (a0 && a1) : (a0 || a1);
-                            const bool hb = mid ? (b0 && b1) : (b0 || b1);
-                            hit[u] = ok[u] && (ha || hb);
-                            const uint32_t slot = ha ? 2 * s1[u] + (!mid && !a0) : 2 * s2[u] + (!mid && !b0);
+                            // The hit logic runs on the wave's lane masks (uniform 64-bit values,
+                            // scalar ops): per-lane bool logic compiles to exec-masked branches
+                            // (&&, ||) or to 0/1 VALU arithmetic.  inverse_ballot reads this
+                            // lane's bit back as a condition at no cost.  The batch runs with
+                            // every lane active.
+                            const uint64_t mMid = __ballot(mid);
+                            mOk[u] = __ballot(ok[u]);
+                            const uint64_t mA0 = __ballot(alo == k0[u]), mA1 = __ballot(ahi == kk);
+                            const uint64_t mB0 = __ballot(blo == k0[u]), mB1 = __ballot(bhi == kk);
+                            const uint64_t mHa = (mA0 & mA1) | (~mMid & (mA0 | mA1));
+                            const uint64_t mHb = (mB0 & mB1) | (~mMid & (mB0 | mB1));
+                            mHit[u] = mOk[u] & (mHa | mHb);
+                            hit[u] = __builtin_amdgcn_inverse_ballot_w64(mHit[u]);
+                            const uint32_t wa = __builtin_amdgcn_inverse_ballot_w64(~mMid & ~mA0) ? 1u : 0u;
+                            const uint32_t wb = __builtin_amdgcn_inverse_ballot_w64(~mMid & ~mB0) ? 1u : 0u;
+                            const uint32_t slot = __builtin_amdgcn_inverse_ballot_w64(mHa) ? 2 * s1[u] + wa : 2 * s2[u] + wb;
                             const uint32_t ci = hit[u] ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
                             __hip_atomic_fetch_add(&dcnt[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     } else {
         #pragma unroll
-                        for (int u = 0; u < kBatch; u++) hit[u] = false;
+                        for (int u = 0; u < kBatch; u++) {
+                            hit[u] = false;
+                            mHit[u] = 0;
+                            mOk[u] = __ballot(ok[u]);
+                        }
                     }
                     if constexpr ((mode & 16) != 0) {
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) acc += hit[u];
                         continue;
                     }
-                    // misses: append to this workgroup's stream of the key's bucket
+                    // misses: append to this workgroup's stream of the key's bucket (lane-mask
+                    // logic as above; offsets by 24-bit multiplies, ensure_spill keeps
+                    // stream lengths below 2^24)
                     uint32_t pos[kBatch];
+                    uint64_t mMiss[kBatch], mBig[kBatch];
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        const bool miss = ok[u] && !hit[u];
+                        mMiss[u] = mOk[u] & ~mHit[u];
+                        mBig[u] = __ballot(k1[u] != 0);  // key of 9-16 bytes: 16-byte record
                         const uint32_t b = spill_bucket(hh[u]);
-                        const uint32_t ci = miss ? (k1[u] == 0 ? b : (uint32_t)kSpillBuckets + b) : 2u * kSpillBuckets + lane;
+                        const uint32_t ci = __builtin_amdgcn_inverse_ballot_w64(mMiss[u])
+                                                ? b + (__builtin_amdgcn_inverse_ballot_w64(mBig[u]) ? (uint32_t)kSpillBuckets : 0u)
+                                                : 2u * kSpillBuckets + lane;  // per-lane dummy cursor
                         pos[u] = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                     if constexpr ((mode & 32) != 0) {
@@ -341,24 +374,24 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         for (int u = 0; u < kBatch; u++) acc += pos[u];
                         continue;
                     }
-                    bool over = false;
+                    uint64_t mOver = 0;
 #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         // exactly two store instructions per word slot, every pass: lanes with
                         // nothing to store get an out-of-range offset, which the range check
                         // drops (the loop's VMEM count stays fixed, so its DMA waits are counted)
-                        const bool miss = ok[u] && !hit[u];
                         const uint32_t b = spill_bucket(hh[u]);
-                        const bool small = k1[u] == 0;  // key of at most 8 bytes: 8-byte record
-                        const bool put8 = miss && small && pos[u] < sub8, put16 = miss && !small && pos[u] < sub;
-                        __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32)}, rs8,
-                                                              put8 ? (b * sub8 + pos[u]) * 8u : kOutOfRange, 0, 0);
+                        const uint64_t mFit8 = __ballot(pos[u] < sub8), mFit16 = __ballot(pos[u] < sub);
+                        const uint64_t mPut8 = mMiss[u] & ~mBig[u] & mFit8, mPut16 = mMiss[u] & mBig[u] & mFit16;
+                        const uint32_t o8 = __builtin_amdgcn_inverse_ballot_w64(mPut8) ? (__umul24(b, sub8) + pos[u]) * 8u : kOutOfRange;
+                        const uint32_t o16 = __builtin_amdgcn_inverse_ballot_w64(mPut16) ? (__umul24(b, sub) + pos[u]) * 16u : kOutOfRange;
+                        __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32)}, rs8, o8, 0, 0);
                         __builtin_amdgcn_raw_buffer_store_b128(
                             (u32x4){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32)},
-                            rs16, put16 ? (b * sub + pos[u]) * 16u : kOutOfRange, 0, 0);
-                        over |= miss && pos[u] >= (small ? sub8 : sub);
+                            rs16, o16, 0, 0);
+                        mOver |= mMiss[u] & ((mBig[u] & ~mFit16) | (~mBig[u] & ~mFit8));
                     }
-                    if (__ballot(over)) {  // a stream is full: count in the HBM table; the bucket then merges through it
+                    if (mOver) {  // a stream is full: count in the HBM table; the bucket then merges through it
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
                             const bool miss = ok[u] && !hit[u];
@@ -377,7 +410,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         }
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
-        dma_for_chunk<(mode & 0x100) != 0>(in, n, c + 2 * stride, lane, ring0 + kf * kSlotBytes);
+        dma_for_chunk<(mode & 0x100) != 0>(in, n, cs + 2 * cstep, lane, ring0 + kf * kSlotBytes);
     }
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
 
@@ -854,20 +887,27 @@ uint32_t wc_map_grid(uint64_t n, int grid) {
     return (uint32_t)(g ? g : 1);
 }
 
-void launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode, hipStream_t s) {
-    const uint64_t nchunks = (n + kOwn - 1) / kOwn;
-    if (nchunks == 0) return;
+bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode, hipStream_t s) {
+    const uint64_t nch = (n + kOwn - 1) / kOwn;
+    if (nch == 0) return true;
+    if (nch + (uint64_t)kMaxMapWGs * kWavesPerWG * 3 >= (1ull << 32)) return false;  // 32-bit chunk indices
+    const uint32_t nchunks = (uint32_t)nch;
+    // first chunk whose window [cs - 16, cs + 1008) reaches the dword holding the
+    // split's last n % 4 bytes (the range check zero-fills that partial dword)
+    const uint64_t n4 = n & ~3ull, reach = kSlotBytes - kBack;
+    const uint32_t ctail = (n & 3) == 0 ? 0xFFFFFFFFu : n4 < reach ? 0u : (uint32_t)((n4 - reach) / kOwn + 1);
     const uint64_t g = wc_map_grid(n, grid);
     switch (mode) {
 #define MRG_MAP_MODE(M) \
-    case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
+    case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
         MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32) MRG_MAP_MODE(0x100)
 #undef MRG_MAP_MODE
         // occupancy benchmark: 8 or 12 waves per workgroup (results stay exact)
-        case 0x1000: wc_map_kernel<0, 8><<<(unsigned)g, 8 * kWave, 0, s>>>(in, n, nchunks, t, lt); break;
-        case 0x2000: wc_map_kernel<0, 12><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, nchunks, t, lt); break;
-        default: wc_map_kernel<0><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, t, lt); break;
+        case 0x1000: wc_map_kernel<0, 8><<<(unsigned)g, 8 * kWave, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
+        case 0x2000: wc_map_kernel<0, 12><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
+        default: wc_map_kernel<0><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
     }
+    return true;
 }
 
 void launch_wc_agg(const Tables& t, int mode, int emit, hipStream_t s) {
