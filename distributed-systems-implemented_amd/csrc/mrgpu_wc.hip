@@ -225,17 +225,21 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             // and lengths (ctz over this lane's mask and the next two lanes'), packed into
             // the list as slot position | min(len, 31) << 10.  Neighbour masks by DPP.
             const uint32_t x1 = wave_shl1(mA, 0u);
-            const uint32_t x2 = wave_shl1(x1, 0u);
             const uint32_t pv = wave_shr1(mA, 0u);
-            const uint64_t win = (uint64_t)mA | ((uint64_t)x1 << 16) | ((uint64_t)x2 << 32);
+            // Non-letters of this lane's 16 bytes and the next lane's.  A word starts at
+            // bit <= 15, so one of <= 16 bytes ends by bit 31; the length is the
+            // distance to the next non-letter, capped at 31 by a forced bit (a word
+            // without a terminator in the window has more than 16 bytes).
+            const uint32_t nl = ~(mA | (x1 << 16));
             const bool owned = lane >= 1 && lane <= (uint32_t)kOwnLanes;
             uint32_t SA = owned ? (mA & ~((mA << 1) | ((pv >> 15) & 1u)) & 0xFFFFu) : 0u;
             uint32_t total;
             uint32_t j = wave_excl_scan<4>(__popc(SA), &total);
+            const uint32_t pos0 = 16 * lane;
             while (SA) {
                 const uint32_t bit = __builtin_ctz(SA);
-                const uint32_t len = min((uint32_t)__builtin_ctzll(~(win >> bit)), 31u);
-                list[j++] = (uint16_t)((16 * lane + bit) | (len << 10));
+                const uint32_t len = __builtin_ctz((nl >> bit) | 0x80000000u);
+                list[j++] = (uint16_t)((pos0 + bit) | (len << 10));
                 SA &= SA - 1;
             }
             wave_sync();
@@ -313,6 +317,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             A[u] = dset[s1[u]];
                             B[u] = dset[s2[u]];
                         }
+                        __builtin_amdgcn_sched_barrier(0);  // all 2 * kBatch set reads in flight before the compares
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
                             // short key: any of the 4 ways of its two sets; mid key: the single
