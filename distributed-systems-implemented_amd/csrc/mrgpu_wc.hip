@@ -87,14 +87,14 @@ __device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
 // chunks ahead.  gfx9 counts loads and stores on one in-order vmcnt, and hipcc
 // waits vmcnt(0) as soon as a loop's VMEM count is not static, so the loop's
 // VMEM instructions are fixed: the DMA is inline asm (invisible to hipcc's
-// waitcnt pass) and the spill appends are exactly 2 * kBatch range-checked
-// buffer stores per chunk (lanes with nothing to store use an out-of-range
-// offset).  The wait for chunk c's DMA is then vmcnt(kVmemPerIter): only the
+// waitcnt pass) and the spill appends of a chunk are exactly two range-checked
+// buffer stores (its misses compacted in LDS first; lanes with nothing to store
+// use an out-of-range offset).  The wait for chunk c's DMA is then vmcnt(kVmemPerIter): only the
 // previous iteration's stores and DMA may still be in flight.  Rare paths with
 // other memory operations (words > 16 bytes, chunks of more than kBatchWords
 // words, HBM-table overflow, UTF-8 table lookups) drain with vmcnt(0).
 constexpr uint32_t kOutOfRange = 0xFFFFFFF0u;
-constexpr int kVmemPerIter = 2 * kBatch + 1;
+constexpr int kVmemPerIter = 3;  // per chunk: one 8-byte and one 16-byte spill store, one DMA
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -118,8 +118,8 @@ __device__ __forceinline__ void dma_chunk(i32x4 rsrc, uint32_t voff, uint32_t ld
                      : "memory", "m0");
 }
 __device__ __forceinline__ void wait_vmem_iter() {
-    static_assert(kVmemPerIter == 7, "update the immediate");
-    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+    static_assert(kVmemPerIter == 3, "update the immediate");
+    asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
 }
 __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -359,15 +359,64 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         for (int u = 0; u < kBatch; u++) acc += hit[u];
                         continue;
                     }
-                    // misses: append to this workgroup's stream of the key's bucket (lane-mask
-                    // logic as above; offsets by 24-bit multiplies, ensure_spill keeps
-                    // stream lengths below 2^24)
-                    uint32_t pos[kBatch];
+                    // Misses: append to this workgroup's stream of the key's bucket.  A spill
+                    // store costs per instruction (TA cycles per wave-instruction), so the
+                    // pass's misses are first compacted: staged as 16-byte (k0,k1) records in
+                    // the chunk's own ring slot (free once its key bytes are in registers)
+                    // at their rank, then lane i appends record i — one cursor add and
+                    // one 8-byte plus one 16-byte store per chunk instead of per word slot.
+                    // Chunks of several passes (slot still needed) or with more than 64
+                    // misses append from the word slots and drain (their VMEM count differs).
                     uint64_t mMiss[kBatch], mBig[kBatch];
+                    uint32_t nmu[kBatch + 1];
+                    nmu[0] = 0;
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         mMiss[u] = mOk[u] & ~mHit[u];
                         mBig[u] = __ballot(k1[u] != 0);  // key of 9-16 bytes: 16-byte record
+                        nmu[u + 1] = nmu[u] + (uint32_t)__popcll(mMiss[u]);
+                    }
+                    const uint32_t nm = nmu[kBatch];
+                    if (passes == 1 && nm <= (uint32_t)kWave) {
+                        lds_uint4* stage = (lds_uint4*)buf;
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++)
+                            if (__builtin_amdgcn_inverse_ballot_w64(mMiss[u]))
+                                stage[nmu[u] + mbcnt64(mMiss[u])] =
+                                    (u32x4){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32)};
+                        const u32x4 r = stage[lane];  // this wave's own writes, in order
+                        const bool valid = lane < nm;
+                        const uint32_t b = spill_bucket(fold32(r.x, r.y, r.z, r.w));
+                        const bool big = (r.z | r.w) != 0;
+                        const uint32_t ci = valid ? b + (big ? (uint32_t)kSpillBuckets : 0u) : 2u * kSpillBuckets + lane;
+                        const uint32_t pos = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if constexpr ((mode & 32) != 0) {
+                            acc += pos;
+                            continue;
+                        }
+                        // exactly two store instructions per chunk: lanes with nothing to store
+                        // get an out-of-range offset, which the range check drops (the loop's
+                        // VMEM count stays fixed, so its DMA waits are counted)
+                        const bool fit8 = pos < sub8, fit16 = pos < sub;
+                        const bool put8 = valid & !big & fit8, put16 = valid & big & fit16;
+                        __builtin_amdgcn_raw_buffer_store_b64((u32x2){r.x, r.y}, rs8,
+                                                              put8 ? (__umul24(b, sub8) + pos) * 8u : kOutOfRange, 0, 0);
+                        __builtin_amdgcn_raw_buffer_store_b128(r, rs16, put16 ? (__umul24(b, sub) + pos) * 16u : kOutOfRange,
+                                                               0, 0);
+                        const bool over = valid & (big ? !fit16 : !fit8);
+                        if (__ballot(over)) {  // a stream is full: count in the HBM table; the bucket then merges through it
+                            if (over) {
+                                short_insert(t, ((uint64_t)r.y << 32) | r.x, ((uint64_t)r.w << 32) | r.z, 1);
+                                t.bflag[b] = 1u;
+                                ovf++;
+                            }
+                            wait_vmem_all();
+                        }
+                        continue;  // passes == 1
+                    }
+                    uint32_t pos[kBatch];
+        #pragma unroll
+                    for (int u = 0; u < kBatch; u++) {
                         const uint32_t b = spill_bucket(hh[u]);
                         const uint32_t ci = __builtin_amdgcn_inverse_ballot_w64(mMiss[u])
                                                 ? b + (__builtin_amdgcn_inverse_ballot_w64(mBig[u]) ? (uint32_t)kSpillBuckets : 0u)
@@ -379,12 +428,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         for (int u = 0; u < kBatch; u++) acc += pos[u];
                         continue;
                     }
-                    uint64_t mOver = 0;
-#pragma unroll
+        #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        // exactly two store instructions per word slot, every pass: lanes with
-                        // nothing to store get an out-of-range offset, which the range check
-                        // drops (the loop's VMEM count stays fixed, so its DMA waits are counted)
                         const uint32_t b = spill_bucket(hh[u]);
                         const uint64_t mFit8 = __ballot(pos[u] < sub8), mFit16 = __ballot(pos[u] < sub);
                         const uint64_t mPut8 = mMiss[u] & ~mBig[u] & mFit8, mPut16 = mMiss[u] & mBig[u] & mFit16;
@@ -394,22 +439,14 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         __builtin_amdgcn_raw_buffer_store_b128(
                             (u32x4){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32)},
                             rs16, o16, 0, 0);
-                        mOver |= mMiss[u] & ((mBig[u] & ~mFit16) | (~mBig[u] & ~mFit8));
-                    }
-                    if (mOver) {  // a stream is full: count in the HBM table; the bucket then merges through it
-        #pragma unroll
-                        for (int u = 0; u < kBatch; u++) {
-                            const bool miss = ok[u] && !hit[u];
-                            if (miss && pos[u] >= (k1[u] == 0 ? sub8 : sub)) {
-                                short_insert(t, k0[u], k1[u], 1);
-                                t.bflag[spill_bucket(hh[u])] = 1u;
-                                ovf++;
-                            }
+                        const uint64_t mOver = mMiss[u] & ((mBig[u] & ~mFit16) | (~mBig[u] & ~mFit8));
+                        if (__builtin_amdgcn_inverse_ballot_w64(mOver)) {
+                            short_insert(t, k0[u], k1[u], 1);
+                            t.bflag[b] = 1u;
+                            ovf++;
                         }
-                        wait_vmem_all();
                     }
-        
-                    if (pass != 0) wait_vmem_all();
+                    wait_vmem_all();  // this pass issued a different number of VMEM instructions
                 }
             }
         }
