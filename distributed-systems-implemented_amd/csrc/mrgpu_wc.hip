@@ -104,14 +104,23 @@ __device__ __forceinline__ i32x4 raw_rsrc(const void* base, uint32_t nrec) {
     return (i32x4){(int)(uint32_t)b, (int)((uint32_t)(b >> 32) & 0xFFFFu), (int)nrec, 0x00020000};
 }
 // 64 lanes x 16 B: lane l's bytes at rsrc + voff -> LDS [lds_base + 16 l]
-template <bool kNT = false>
+// kPol (benchmark variants of the input loads' cache policy): 0 default, 1 nt,
+// 2 sc1, 3 sc0 sc1
+template <int kPol = 0>
 __device__ __forceinline__ void dma_chunk(i32x4 rsrc, uint32_t voff, uint32_t lds_base) {
     // operands are wave-uniform; readfirstlane puts them in SGPRs for the asm "s" constraints
     rsrc = (i32x4){__builtin_amdgcn_readfirstlane(rsrc.x), __builtin_amdgcn_readfirstlane(rsrc.y),
                    __builtin_amdgcn_readfirstlane(rsrc.z), __builtin_amdgcn_readfirstlane(rsrc.w)};
     lds_base = __builtin_amdgcn_readfirstlane(lds_base);
-    if constexpr (kNT)  // non-temporal: the input stream does not push spill lines out of L2
+    if constexpr (kPol == 1)
         asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen nt lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
+                     : "memory", "m0");
+    else if constexpr (kPol == 2)
+        asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc1 lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
+                     : "memory", "m0");
+    else if constexpr (kPol == 3)
+        asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen sc0 sc1 lds" ::"v"(voff), "s"(rsrc),
+                     "s"(lds_base)
                      : "memory", "m0");
     else
         asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
@@ -125,7 +134,7 @@ __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(
 
 // Issue the DMA of chunk c (any c: chunks past the split read as zeros).
 // cs = the chunk's first owned byte (chunk index * kOwn)
-template <bool kNT = false>
+template <int kPol = 0>
 // The descriptor base is the window start rounded down to 1 GiB (a chunk's
 // window never crosses its base's range), so this is 32-bit scalar arithmetic.
 // For the split's first chunk the base is 0 and lane 0's offset (-16) wraps past
@@ -135,8 +144,13 @@ __device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uin
     const uint64_t r = n - base;  // bytes from the base to the end of the split (wraps if base >= n)
     const uint32_t rhi = (uint32_t)(r >> 32), rlo = (uint32_t)r;
     const uint32_t nrec = (int32_t)rhi < 0 ? 0u : (rhi != 0 || rlo > 0xFFFFFF00u) ? 0xFFFFFF00u : rlo;
-    dma_chunk<kNT>(raw_rsrc(in + base, nrec), (uint32_t)(cs - base) - kBack + 16u * lane, lds_base);
+    dma_chunk<kPol>(raw_rsrc(in + base, nrec), (uint32_t)(cs - base) - kBack + 16u * lane, lds_base);
 }
+
+// input loads are non-temporal (measured ~2 % faster than the default policy);
+// the other policies are benchmark variants (map_mode 0x100 = default, 0x4000 =
+// sc1, 0x8000 = sc0 sc1)
+constexpr int dma_policy(uint32_t mode) { return (mode & 0x100) ? 0 : (mode & 0x4000) ? 2 : (mode & 0x8000) ? 3 : 1; }
 
 template <uint32_t mode, int NW = kWavesPerWG>
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t nchunks,
@@ -144,7 +158,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
     // 1 = stream input only, 2 = tokenize only (no per-word work), 4 = per-word
     // key extraction without the dictionary, 16 = no spill append (misses dropped),
-    // 32 = spill cursors but no stores; 0x100 (exact) = non-temporal input loads
+    // 32 = spill cursors but no stores; 0x100 / 0x4000 / 0x8000 (exact) = input
+    // loads with the default policy / sc1 / sc0 sc1 instead of nt
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -185,9 +200,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // prologue: chunk c0 landed before the loop, chunk c0 + stride in flight
     // byte offsets advance by addition (64-bit scalar multiplies per iteration are not free)
     const uint64_t cstep = (uint64_t)stride * kOwn;
-    dma_for_chunk<(mode & 0x100) != 0>(in, n, (uint64_t)c0 * kOwn, lane, ring0);
+    dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn, lane, ring0);
     wait_vmem_all();
-    dma_for_chunk<(mode & 0x100) != 0>(in, n, (uint64_t)c0 * kOwn + cstep, lane, ring0 + kSlotBytes);
+    dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn + cstep, lane, ring0 + kSlotBytes);
     uint32_t k = 0;  // ring slot of the current chunk
     uint64_t cs = (uint64_t)c0 * kOwn;  // the current chunk's first own byte = slot byte 16 (slot byte i = input cs - 16 + i)
     for (uint32_t c = c0; c < nchunks; c += stride, cs += cstep, k = k == kRing - 1 ? 0 : k + 1) {
@@ -452,7 +467,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         }
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
-        dma_for_chunk<(mode & 0x100) != 0>(in, n, cs + 2 * cstep, lane, ring0 + kf * kSlotBytes);
+        dma_for_chunk<dma_policy(mode)>(in, n, cs + 2 * cstep, lane, ring0 + kf * kSlotBytes);
     }
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
 
@@ -943,6 +958,7 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
         MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32) MRG_MAP_MODE(0x100)
+        MRG_MAP_MODE(0x4000) MRG_MAP_MODE(0x8000)
 #undef MRG_MAP_MODE
         // occupancy benchmark: 8 or 12 waves per workgroup (results stay exact)
         case 0x1000: wc_map_kernel<0, 8><<<(unsigned)g, 8 * kWave, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
