@@ -11,6 +11,12 @@ workload (configs[1] = SURVEY.md §8d C2): 10 GB synthetic Zipf(s=1.07, V=1e6)
          every rank maps its own 10 GB (seed per rank); value = all ranks' input
          bytes x steps / max-over-ranks time.
 
+Other §8d workloads (evidence runs; the default is C2):
+  --workload c3  grep "distributed" over 10 GB of valid mixed ASCII/UTF-8 lines
+  --workload c4  wc, 12.5 GB per GPU, nReduce = 64 (the 8-GPU 100 GB config)
+  --workload c5  wc, 25 GB per GPU, Zipf(s=0.8, V=1e7) with every vocabulary word
+                 once up front (>= 1e7 distinct keys), nReduce = 64
+
 Run:  python bench.py [--gpus N --steps K --warmup W]
       N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
              --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
@@ -35,10 +41,25 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402  (import before mrgpu: one shared HIP runtime)
 import torch.distributed as dist  # noqa: E402
 
-from mrgpu import MRG_APP_WC, Context, ihash  # noqa: E402
+from mrgpu import MRG_APP_GREP, MRG_APP_WC, Context, ihash  # noqa: E402
 from mrgpu import corpus as C  # noqa: E402
 
 METRIC = "word-count input GB/s (map+shuffle+reduce) at 1/2/4/8 MI355X; % HBM roofline"
+GREP_METRIC = "grep input GB/s (map+shuffle+reduce) at 1/2/4/8 MI355X; % HBM roofline"
+
+# SURVEY.md §8d workloads: app, corpus kind, Zipf s, vocabulary V, seed, files x MB, nReduce
+WORKLOADS = {
+    "c2": dict(app="wc", kind=C.KIND_ASCII, s=1.07, V=10**6, seed=2, files=40, file_mb=250, nreduce=10,
+               desc="C2: wc, Zipf s=1.07 over 1e6 ASCII words"),
+    "c3": dict(app="grep", kind=C.KIND_UTF8, s=1.07, V=10**6, seed=3, files=40, file_mb=250, nreduce=10,
+               desc="C3: grep 'distributed' (0.5 % of lines, 20 % of those repeated), valid UTF-8, "
+                    "~30 % non-ASCII words, lines 40-120 B"),
+    "c4": dict(app="wc", kind=C.KIND_ASCII, s=1.07, V=10**6, seed=4, files=50, file_mb=250, nreduce=64,
+               desc="C4: wc, Zipf s=1.07 over 1e6 ASCII words, 12.5 GB per GPU"),
+    "c5": dict(app="wc", kind=C.KIND_ASCII, s=0.8, V=10**7, seed=5, files=100, file_mb=250, nreduce=64,
+               desc="C5: wc, Zipf s=0.8 over 1e7 ASCII words, every word once up front"),
+}
+PATTERN = b"distributed"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
@@ -46,37 +67,69 @@ def log(msg):
     print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
 
 
-def gen_corpus(rank: int, file_mb: int, nfiles: int, seed_base: int):
+def file_params(w: dict, i: int, nfiles: int):
+    if w["app"] == "grep":
+        return C.grep_params(PATTERN)
+    if w["V"] > 10**6:  # C5: file i emits its share of the vocabulary once, up front
+        return C.wc_params(vocab_lo=w["V"] * i // nfiles, vocab_hi=w["V"] * (i + 1) // nfiles)
+    return C.wc_params()
+
+
+def gen_corpus(w: dict, rank: int, file_mb: int, nfiles: int):
     """nfiles generated files back to back in one buffer.  Every file ends with '\n',
-    so the concatenation is word-for-word the same input as separate wc splits."""
-    voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
-    sizes = [file_mb * 1_000_000] * nfiles
-    seeds = [seed_base + 1000 * rank + i for i in range(nfiles)]
-    buf = np.empty(sum(sizes), dtype=np.uint8)
-    voc.fill_files(sizes, seeds, C.wc_params(), threads=min(16, os.cpu_count() or 1), out=buf)
+    so the concatenation is word-for-word the same input as separate splits."""
+    voc = C.Vocab(w["kind"], w["s"], w["V"], w["seed"])
+    buf = np.empty(nfiles * file_mb * 1_000_000, dtype=np.uint8)
+    sz = file_mb * 1_000_000
+    uniform = w["app"] == "grep" or w["V"] <= 10**6
+    if uniform:
+        seeds = [w["seed"] + 1000 * rank + i for i in range(nfiles)]
+        voc.fill_files([sz] * nfiles, seeds, file_params(w, 0, nfiles), threads=min(16, os.cpu_count() or 1), out=buf)
+    else:
+        from concurrent.futures import ThreadPoolExecutor  # the C generator releases the GIL
+
+        def one(i):
+            voc.fill_files([sz], [w["seed"] + 1000 * rank + i], file_params(w, i, nfiles), threads=1,
+                           out=buf[i * sz:(i + 1) * sz])
+        with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+            list(ex.map(one, range(nfiles)))
     return buf
 
 
-def check_output(parts: list[bytes], nreduce: int, sample: int = 20000) -> dict:
+def check_output(parts: list[bytes], nreduce: int, app: str = "wc", sample: int = 20000) -> dict:
     """Size-independent properties of the full-size output: every partition sorted
-    bytewise with unique keys, every sampled key in the right partition, counts > 0."""
-    ok_sorted = ok_part = True
+    bytewise with unique keys, every sampled key in the right partition; wc: counts
+    sum to the word total; grep: every line is "L L" and L holds the pattern."""
+    ok_sorted = ok_part = ok_form = True
     total = 0
     rng = np.random.default_rng(0)
     for r, p in enumerate(parts):
         lines = p.split(b"\n")[:-1] if p else []
-        keys = [l.rsplit(b" ", 1)[0] for l in lines]
-        total += sum(int(l.rsplit(b" ", 1)[1]) for l in lines)
+        if app == "grep":
+            keys = [l[:(len(l) - 1) // 2] for l in lines]
+            total += len(lines)
+            for i in rng.integers(0, len(keys), size=min(sample // nreduce, len(keys))) if keys else []:
+                l, k = lines[i], keys[i]
+                if len(l) % 2 == 0 or l != k + b" " + k or PATTERN not in k:
+                    ok_form = False
+        else:
+            keys = [l.rsplit(b" ", 1)[0] for l in lines]
+            total += sum(int(l.rsplit(b" ", 1)[1]) for l in lines)
         if any(keys[i] >= keys[i + 1] for i in range(len(keys) - 1)):
             ok_sorted = False
         if keys:
             for i in rng.integers(0, len(keys), size=min(sample // nreduce, len(keys))):
                 if ihash(keys[i]) % nreduce != r:
                     ok_part = False
-    return {"sorted_unique": ok_sorted, "partition_ok": ok_part, "total_words": total}
+    out = {"sorted_unique": ok_sorted, "partition_ok": ok_part}
+    if app == "grep":
+        out.update(lines_format_ok=ok_form, matching_lines=total)
+    else:
+        out["total_words"] = total
+    return out
 
 
-def cpu_baseline(sample_files: int, sample_mb: int, nreduce: int, ctx: Context) -> dict | None:
+def cpu_baseline(w: dict, sample_files: int, sample_mb: int, nreduce: int, ctx: Context) -> dict | None:
     """The oracle's distributed restatement (oracle/_build/mrcpu: coordinator + N worker
     processes, JSON-lines intermediates — mr/coordinator.go + mr/worker.go) on a bounded
     sample of the same workload; its outputs are also compared with the GPU's."""
@@ -88,9 +141,10 @@ def cpu_baseline(sample_files: int, sample_mb: int, nreduce: int, ctx: Context) 
     base = "/dev/shm" if os.path.isdir("/dev/shm") else None
     tmp = tempfile.mkdtemp(prefix="mrcpu-", dir=base)
     try:
-        voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
+        voc = C.Vocab(w["kind"], w["s"], w["V"], w["seed"])
         sizes = [sample_mb * 1_000_000] * sample_files
-        files = voc.fill_files(sizes, [2 + i for i in range(sample_files)], C.wc_params())
+        files = [voc.fill_files([sizes[i]], [w["seed"] + i], file_params(w, i, w["files"]))[0]
+                 for i in range(sample_files)]
         paths = []
         for i, f in enumerate(files):
             p = os.path.join(tmp, f"pg-{i}.txt")
@@ -98,7 +152,8 @@ def cpu_baseline(sample_files: int, sample_mb: int, nreduce: int, ctx: Context) 
             paths.append(p)
         wdir = os.path.join(tmp, "work")
         os.makedirs(wdir)
-        res = subprocess.run([exe, "--app", "wc", "--nreduce", str(nreduce), "--workers", str(workers), "--dir", wdir]
+        app_args = ["--app", "grep", "--pattern", PATTERN.decode()] if w["app"] == "grep" else ["--app", "wc"]
+        res = subprocess.run([exe] + app_args + ["--nreduce", str(nreduce), "--workers", str(workers), "--dir", wdir]
                              + paths, capture_output=True, text=True, timeout=600)
         if res.returncode != 0:
             log(f"mrcpu failed: {res.stderr[-500:]}")
@@ -106,10 +161,13 @@ def cpu_baseline(sample_files: int, sample_mb: int, nreduce: int, ctx: Context) 
         info = json.loads(res.stdout.strip().splitlines()[-1])
         cpu_out = [open(os.path.join(wdir, f"mr-out-{r}"), "rb").read() for r in range(nreduce)]
         joined = b"\n".join(bytes(f) for f in files)
-        gpu_out = ctx.run_job(MRG_APP_WC, joined, nreduce=nreduce)
+        if w["app"] == "grep":
+            gpu_out = ctx.run_job(MRG_APP_GREP, joined, pattern=PATTERN, nreduce=nreduce)
+        else:
+            gpu_out = ctx.run_job(MRG_APP_WC, joined, nreduce=nreduce)
         return {"value": round(info["bytes"] / info["seconds"] / 1e9, 4), "unit": "GB/s", "cores": workers,
                 "kind": "port",
-                "sample": f"{sample_files} files x {sample_mb} MB of the same Zipf corpus "
+                "sample": f"{sample_files} files x {sample_mb} MB of the same corpus generator "
                           f"({info['bytes'] / 1e9:.2f} GB), mrcpu = restated mrcoordinator + {workers} mrworker "
                           f"processes with JSON-lines mr-X-Y shuffle, nReduce={nreduce}; "
                           f"{info['seconds']:.1f} s",
@@ -123,13 +181,19 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--file-mb", type=int, default=250)
-    ap.add_argument("--files", type=int, default=40)
-    ap.add_argument("--nreduce", type=int, default=10)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--file-mb", type=int, default=None, help="override the workload's file size (MB)")
+    ap.add_argument("--files", type=int, default=None, help="override the workload's file count")
+    ap.add_argument("--nreduce", type=int, default=None, help="override the workload's nReduce")
     ap.add_argument("--cpu-sample-files", type=int, default=16)
     ap.add_argument("--cpu-sample-mb", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
+    w = WORKLOADS[args.workload]
+    args.file_mb = args.file_mb or w["file_mb"]
+    args.files = args.files or w["files"]
+    args.nreduce = args.nreduce or w["nreduce"]
+    grep = w["app"] == "grep"
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -145,7 +209,7 @@ def main():
     torch.cuda.synchronize()
 
     t0 = time.time()
-    host = gen_corpus(rank, args.file_mb, args.files, seed_base=2)
+    host = gen_corpus(w, rank, args.file_mb, args.files)
     nbytes = int(host.size)
     log(f"generated {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
 
@@ -162,6 +226,9 @@ def main():
     ctx.sync()
 
     def run_step():
+        if grep:
+            return ctx.run_job(MRG_APP_GREP, pattern=PATTERN, device_ptr=dptr, nbytes=nbytes, nreduce=args.nreduce,
+                               copy_out=False)
         return ctx.run_job(MRG_APP_WC, device_ptr=dptr, nbytes=nbytes, nreduce=args.nreduce, copy_out=False)
 
     for _ in range(args.warmup):
@@ -197,13 +264,14 @@ def main():
     p, n, offs = run_step()
     out = ctypes.string_at(p, n) if n else b""
     parts = [out[offs[i]:offs[i + 1]] for i in range(args.nreduce)]
-    checks = check_output(parts, args.nreduce)
+    checks = check_output(parts, args.nreduce, w["app"])
     checks["deterministic"] = hashlib.sha256(out).hexdigest() == hashlib.sha256(
         ctypes.string_at(*run_step()[:2])).hexdigest()
     if world > 1:
-        tw = torch.tensor([checks["total_words"]], dtype=torch.int64)
+        key = "matching_lines" if grep else "total_words"
+        tw = torch.tensor([checks[key]], dtype=torch.int64)
         dist.all_reduce(tw)
-        checks["total_words"] = int(tw.item())
+        checks[key] = int(tw.item())
 
     total_bytes = nbytes * world * args.steps
     value = total_bytes / t_max / 1e9
@@ -216,18 +284,18 @@ def main():
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
-            if tj.get("input_bytes") == nbytes:
+            if tj.get("input_bytes") == nbytes and tj.get("workload", "c2") == args.workload:
                 traffic = tj.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.cpu_sample_files, args.cpu_sample_mb, args.nreduce, ctx)
+        cpu = cpu_baseline(w, args.cpu_sample_files, args.cpu_sample_mb, args.nreduce, ctx)
 
     if rank == 0:
         line = {
-            "metric": METRIC,
+            "metric": GREP_METRIC if grep else METRIC,
             "value": round(value, 3),
             "unit": "GB/s",
             "n_gpus": world,
@@ -239,15 +307,16 @@ def main():
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (deterministic Zipf corpus from csrc/corpus.c; reference pg-*.txt not bundled)",
-            "config": {"workload": f"C2: wc over {nbytes / 1e9:.2f} GB per GPU ({args.files} files x {args.file_mb} MB, "
-                                   "Zipf s=1.07 over 1e6 ASCII words), device-resident input",
+            "config": {"workload": f"{w['desc']}; {nbytes / 1e9:.2f} GB per GPU ({args.files} files x "
+                                   f"{args.file_mb} MB), device-resident input",
                        "nreduce": args.nreduce, "input_bytes_per_gpu": nbytes, "parallelism": f"dp{world}",
                        "shuffle": "RCCL all-to-all" if world > 1 else "none (single GPU)"},
-            "roofline": {"bound": "hbm", "kernel": "wc_map_kernel", "achieved": round(achieved, 1),
+            "roofline": {"bound": "hbm", "kernel": "grep_map_kernel" if grep else "wc_map_kernel",
+                         "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
-                         "note": "achieved = input bytes per launch / mean HIP-event duration of wc_map_kernel on "
-                                 "the library stream over the timed steps"},
+                         "note": "achieved = input bytes per launch / mean HIP-event duration of the map kernel "
+                                 "on the library stream over the timed steps"},
             "phases_ms": {"map_kernel": round(avg_kern, 3), "map_total": round(last["map_total_ms"], 3),
                           "dict": round(last["dict_ms"], 3), "agg": round(last["agg_ms"], 3),
                           "exchange": round(last["exchange_ms"], 3), "reduce": round(last["reduce_ms"], 3),

@@ -12,6 +12,7 @@
 // prefixes (keys > 16 bytes, or grep lines containing NUL bytes) are then
 // ordered by a full bytewise comparison inside each run.
 #include <cstring>
+#include <rocprim/device/device_merge_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
@@ -135,17 +136,20 @@ __global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8
 }
 
 // Insertion sort of each tied run by full bytewise comparison.  A run longer
-// than max_run is left alone and flags[3] set: the caller then sorts with the
-// k1 pass (16-byte prefixes), whose ties are only keys > 16 bytes.
+// than max_run is left alone, its members marked in `lng` and flags[3] set: the
+// caller then sorts with the k1 pass (16-byte prefixes), or merge-sorts the
+// marked members by full comparison (sort_long_runs).
 __global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_t* tie, uint64_t max_run,
-                                unsigned long long* flags) {
+                                unsigned long long* flags, uint8_t* lng) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i + 1 < n; i += stride) {
         if (tie[i] || !tie[i + 1]) continue;
         uint64_t e = i + 1;
         while (e < n && tie[e] && e - i <= max_run) e++;
         if (e - i > max_run) {
-            atomicOr(&flags[3], 1ull);
+            if (flags[3] == 0) atomicOr(&flags[3], 1ull);
+            lng[i] = 1;
+            for (uint64_t a = i + 1; a < n && tie[a]; a++) lng[a] = 1;
             continue;
         }
         for (uint64_t a = i + 1; a < e; a++) {
@@ -158,6 +162,24 @@ __global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_
             perm[b] = v;
         }
     }
+}
+
+// (partition, key) order of two records: the order the whole sort produces.
+struct FullLess {
+    Recs r;
+    __device__ bool operator()(const uint32_t& a, const uint32_t& b) const {
+        if (r.part[a] != r.part[b]) return r.part[a] < r.part[b];
+        return rec_cmp(r, a, b) < 0;
+    }
+};
+
+__global__ void gather_perm_kernel(const uint32_t* perm, const uint32_t* pos, const uint32_t* d_m, uint32_t* v) {
+    const uint32_t m = *d_m;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) v[i] = perm[pos[i]];
+}
+__global__ void scatter_perm_kernel(uint32_t* perm, const uint32_t* pos, const uint32_t* d_m, const uint32_t* v) {
+    const uint32_t m = *d_m;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) perm[pos[i]] = v[i];
 }
 
 __device__ __forceinline__ uint32_t ndigits(uint64_t v) {
@@ -282,6 +304,42 @@ int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in
     return sort_pass<uint32_t>(ws, k_in, k_out, v_in, v_out, n, bits, s);
 }
 
+struct MarkedPos {
+    const uint8_t* lng;
+    __host__ __device__ bool operator()(const uint32_t& i) const { return lng[i] != 0; }
+};
+
+// The members of long tied runs (lng[i] != 0): compacted in order, merge-sorted
+// by full (partition, key) comparison, written back to the same positions.  The
+// runs are contiguous and already in (partition, prefix) order, which the full
+// order refines, so sorting all marked members together keeps every run in its
+// own positions.  Scratch: sel (positions), key_b (values, two halves).
+static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t n, const uint8_t* lng, hipStream_t s) {
+    RCHK(ws->sel.ensure(n * 4 + 1024));
+    RCHK(ws->offs.ensure(64));
+    uint32_t* pos = ws->sel.as<uint32_t>();
+    uint32_t* d_m = ws->offs.as<uint32_t>();
+    rocprim::counting_iterator<uint32_t> first(0);
+    size_t tb = 0;
+    RCHK(rocprim::select(nullptr, tb, first, pos, d_m, (size_t)n, MarkedPos{lng}, s));
+    RCHK(ws->tmp.ensure(tb));
+    RCHK(rocprim::select(ws->tmp.p, tb, first, pos, d_m, (size_t)n, MarkedPos{lng}, s));
+    RCHK(hipMemcpyAsync(ws->h_pinned + 8, d_m, 4, hipMemcpyDeviceToHost, s));
+    RCHK(hipStreamSynchronize(s));
+    const uint32_t m = (uint32_t)(ws->h_pinned[8] & 0xFFFFFFFFu);
+    if (m == 0) return 0;
+    uint32_t* va = ws->key_b.as<uint32_t>();
+    uint32_t* vb = va + n;
+    const unsigned g = (unsigned)((m + 255) / 256 < 4096 ? (m + 255) / 256 : 4096);
+    gather_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, va);
+    tb = 0;
+    RCHK(rocprim::merge_sort(nullptr, tb, va, vb, (size_t)m, FullLess{r}, s));
+    RCHK(ws->tmp.ensure(tb));
+    RCHK(rocprim::merge_sort(ws->tmp.p, tb, va, vb, (size_t)m, FullLess{r}, s));
+    scatter_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, vb);
+    return 0;
+}
+
 int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst, hipStream_t s) {
     // dst arrays must be preallocated by the caller with src.n capacity; arena shared with src.
     unsigned long long* cnt = nullptr;
@@ -352,22 +410,34 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         }
         return 0;
     };
-    auto fix_ties = [&](bool with_k1, uint64_t max_run) {
+    // Tied runs of up to kMaxRun are insertion-sorted in place (one thread per
+    // run); longer ones are marked.  Returns whether any run was long; with
+    // `merge`, the long runs are then merge-sorted by full comparison.
+    constexpr uint64_t kMaxRun = 64;
+    auto fix_ties = [&](bool with_k1, bool merge, bool* any_long) -> int {
         uint8_t* tie = ws->key_a.as<uint8_t>();
+        uint8_t* lng = tie + n;
+        RCHK(hipMemsetAsync(lng, 0, n, s));
+        RCHK(hipMemsetAsync(flags + 3, 0, 8, s));
         mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1);
-        fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, max_run, flags);
+        fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, kMaxRun, flags, lng);
+        RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 3, 8, hipMemcpyDeviceToHost, s));
+        RCHK(hipStreamSynchronize(s));
+        *any_long = ws->h_pinned[3] != 0;
+        if (*any_long && merge) return sort_long_runs(ws, r, pa, n, lng, s);
+        return 0;
     };
     int e;
     if ((e = sort_all(false))) return e;
     if (has_k1 || has_long || app != 1) {
-        fix_ties(false, has_k1 ? 64 : ~0ull);
-        if (has_k1) {
-            RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 3, 8, hipMemcpyDeviceToHost, s));
-            RCHK(hipStreamSynchronize(s));
-            if (ws->h_pinned[3]) {  // a long run of one 8-byte prefix: sort with the k1 pass
-                if ((e = sort_all(true))) return e;
-                fix_ties(true, ~0ull);
-            }
+        // keys of 9-16 bytes sharing an 8-byte prefix in a long run: sort again with
+        // the k1 pass (cheaper than a comparison sort); any other long run (keys
+        // > 16 bytes, grep lines): comparison merge sort of the run members
+        bool any_long = false;
+        if ((e = fix_ties(false, !has_k1, &any_long))) return e;
+        if (has_k1 && any_long) {
+            if ((e = sort_all(true))) return e;
+            if ((e = fix_ties(true, true, &any_long))) return e;
         }
     }
     uint64_t* ll = ws->key_b.as<uint64_t>();

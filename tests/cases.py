@@ -43,6 +43,10 @@ def edge_cases() -> dict[str, list[bytes]]:
         # falls back to the k1 pass), plus prefix-of-another-key orderings
         "shared_prefix": [b" ".join(b"abcdefgh" + bytes([97 + i % 26, 97 + i // 26 % 26]) * (1 + i % 3)
                                     for i in range(600)) + b" abcdefgh abcdefg abcdefghi"],
+        # > 64 distinct keys longer than 16 bytes sharing their first 16: a long tied
+        # run even after the k1 pass (the reduce merge-sorts it by full comparison)
+        "long_shared_prefix": [b"\n".join(b"abcdefghijklmnopq" + bytes([97 + (i * 7) % 26, 97 + (i * 11) % 26]) * (i % 4)
+                                           for i in range(700)) + b" abcdefghijklmnop abcdefghijklmnopq"],
     }
 
 
@@ -72,6 +76,11 @@ def grep_edge_cases() -> dict[str, tuple[list[bytes], bytes]]:
         "newline_pattern": ([b"a\nb\n"], b"a\nb"),
         "multi_file": ([b"distributed one\n", b"distributed two\ndistributed one\n"], b"distributed"),
         "long_lines": ([(b"w" * 5000 + b" distributed " + b"v" * 3000 + b"\n") * 3], b"distributed"),
+        # > 64 distinct matching lines with one 16-byte prefix, in scrambled order,
+        # and lines that are prefixes of others: the reduce's long tied run
+        "tied_lines": ([b"".join(b"the distributed system " + str((i * 7919) % 1000).encode() * (1 + i % 3) + b"\n"
+                                 for i in range(1000)) + b"the distributed system \nthe distributed system\n"],
+                       b"distributed"),
     }
 
 
