@@ -1033,6 +1033,96 @@ __global__ void unpack_kernel(const WireRec* wrec, uint64_t n, const uint64_t* s
     }
 }
 
+// Host-side layout of one rank's exchange: byte counts / displacements of its
+// send segments (per owner rank) and of its receive segments (per source rank).
+struct ExchPlan {
+    std::vector<size_t> sc, sd, rc, rd, asc, asd, arc, ard;  // records (bytes) and arena bytes
+    std::vector<uint64_t> hbase;                             // [P] record base, [P] arena base (send side)
+    size_t srec = 0, sar = 0, rrec = 0, rar = 0;
+};
+
+// snd[2*o] / snd[2*o+1]: records / arena bytes this rank sends to owner o;
+// rcv[2*s] / rcv[2*s+1]: what it receives from source s.
+static ExchPlan exch_plan(int P, const unsigned long long* snd, const unsigned long long* rcv) {
+    ExchPlan x;
+    for (auto* v : {&x.sc, &x.sd, &x.rc, &x.rd, &x.asc, &x.asd, &x.arc, &x.ard}) v->assign(P, 0);
+    x.hbase.assign(2 * P, 0);
+    for (int o = 0; o < P; o++) {
+        x.hbase[o] = x.srec;
+        x.hbase[P + o] = x.sar;
+        x.sc[o] = snd[2 * o] * sizeof(WireRec); x.sd[o] = x.srec * sizeof(WireRec); x.srec += snd[2 * o];
+        x.asc[o] = snd[2 * o + 1]; x.asd[o] = x.sar; x.sar += snd[2 * o + 1];
+        x.rc[o] = rcv[2 * o] * sizeof(WireRec); x.rd[o] = x.rrec * sizeof(WireRec); x.rrec += rcv[2 * o];
+        x.arc[o] = rcv[2 * o + 1]; x.ard[o] = x.rar; x.rar += rcv[2 * o + 1];
+    }
+    return x;
+}
+
+// Per-rank device state of one exchange.  scratch: [2P] send counts, [2P] receive
+// counts, [2P] pack cursors, [2P] send bases.
+struct ExchSide {
+    DevBuf scratch, sbuf, sar_b, rbuf, rar_b, rmeta;
+    std::vector<unsigned long long> snd, rcv;
+    ExchPlan plan;
+    unsigned long long* d_cnt(int P) { return (unsigned long long*)scratch.p; }
+    unsigned long long* d_rcv(int P) { return d_cnt(P) + 2 * P; }
+    unsigned long long* d_cur(int P) { return d_cnt(P) + 4 * P; }
+    uint64_t* d_base(int P) { return (uint64_t*)(d_cnt(P) + 6 * P); }
+};
+
+// Step 1: count records / arena bytes per owner rank (on the device, async).
+static int exch_count(mrg_ctx* c, const Recs& r, int P, ExchSide& x) {
+    size_t meta = sizeof(unsigned long long) * (8 * P + 8);
+    HCHK(c, x.scratch.ensure(meta));
+    HCHK(c, hipMemsetAsync(x.scratch.p, 0, meta, c->s));
+    if (r.n) owner_count_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, x.d_cnt(P));
+    HCHK(c, hipGetLastError());
+    return MRG_OK;
+}
+
+// Step 2 (x.snd / x.rcv known on the host): size the buffers and pack the
+// per-owner segments.  Step 3 is the transport (RCCL or in-process copies).
+static int exch_pack(mrg_ctx* c, const Recs& r, int P, ExchSide& x) {
+    x.plan = exch_plan(P, x.snd.data(), x.rcv.data());
+    HCHK(c, x.sbuf.ensure(x.plan.srec * sizeof(WireRec) + 64));
+    HCHK(c, x.rbuf.ensure(x.plan.rrec * sizeof(WireRec) + 64));
+    HCHK(c, x.sar_b.ensure(x.plan.sar + 64));
+    HCHK(c, x.rar_b.ensure(x.plan.rar + 64));
+    HCHK(c, hipMemcpyAsync(x.d_base(P), x.plan.hbase.data(), 16 * P, hipMemcpyHostToDevice, c->s));
+    if (r.n)
+        pack_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, x.d_base(P), x.d_base(P) + P, x.d_cur(P),
+                                             (WireRec*)x.sbuf.p, (uint8_t*)x.sar_b.p);
+    HCHK(c, hipGetLastError());
+    return MRG_OK;
+}
+
+// Step 4: unpack the received records into a Recs view and re-aggregate exactly.
+static int exch_finish(mrg_ctx* c, const mrg_parts* local, int P, ExchSide& x, mrg_parts** owned) {
+    int rc;
+    const ExchPlan& pl = x.plan;
+    std::vector<uint64_t> hsrc(2 * P);
+    for (int o = 0; o < P; o++) { hsrc[o] = pl.rd[o] / sizeof(WireRec); hsrc[P + o] = pl.ard[o]; }
+    HCHK(c, x.rmeta.ensure(16 * P));
+    HCHK(c, hipMemcpyAsync(x.rmeta.p, hsrc.data(), 16 * P, hipMemcpyHostToDevice, c->s));
+    mrg_parts* tmp = nullptr;
+    if ((rc = parts_alloc(c, pl.rrec, 0, local->app, local->nreduce, &tmp))) return rc;
+    cache_put(c->device, tmp->arena, tmp->arena_bytes);  // nothing has used it yet
+    tmp->arena = (uint8_t*)x.rar_b.adopt(&tmp->arena_bytes);  // adopt the received arena
+    tmp->r.arena = tmp->arena;
+    tmp->r.arena_n = pl.rar;
+    if (pl.rrec)
+        unpack_kernel<<<1024, 256, 0, c->s>>>((const WireRec*)x.rbuf.p, pl.rrec, (const uint64_t*)x.rmeta.p,
+                                              (const uint64_t*)x.rmeta.p + P, (uint32_t)P, tmp->r);
+    if (hipGetLastError() != hipSuccess) { mrg_parts_free(tmp); return fail(c, MRG_EDEVICE, "unpack launch"); }
+    rc = aggregate(c, {tmp->r}, local->app, local->nreduce, owned);
+    hipError_t e = hipStreamSynchronize(c->s);
+    mrg_parts_free(tmp);
+    x.sbuf.release(); x.rbuf.release(); x.sar_b.release(); x.rmeta.release(); x.scratch.release();
+    if (rc) return rc;
+    HCHK(c, e);
+    return MRG_OK;
+}
+
 int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     if (!c || !local || !owned) return MRG_EINVAL;
     int rc;
@@ -1043,66 +1133,103 @@ int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     }
     HCHK(c, hipEventRecord(c->ev[6], c->s));
     const Recs& r = local->r;
-    DevBuf scratch;
-    std::vector<uint64_t> h(4 * P + 8, 0);
-    // counts per owner
-    size_t meta = sizeof(unsigned long long) * (8 * P + 8);
-    HCHK(c, scratch.ensure(meta));
-    unsigned long long* d_cnt = (unsigned long long*)scratch.p;          // [2P] send counts (rec, arena)
-    unsigned long long* d_rcv = d_cnt + 2 * P;                           // [2P] recv counts
-    unsigned long long* d_cur = d_cnt + 4 * P;                           // [2P] pack cursors
-    uint64_t* d_base = (uint64_t*)(d_cnt + 6 * P);                       // [2P] rec base, arena base
-    HCHK(c, hipMemsetAsync(scratch.p, 0, meta, c->s));
-    if (r.n) owner_count_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, d_cnt);
-    NCHK(c, ncclAllToAll(d_cnt, d_rcv, 2, ncclUint64, c->comm, c->s));
-    std::vector<unsigned long long> snd(2 * P), rcv(2 * P);
-    HCHK(c, hipMemcpyAsync(snd.data(), d_cnt, 16 * P, hipMemcpyDeviceToHost, c->s));
-    HCHK(c, hipMemcpyAsync(rcv.data(), d_rcv, 16 * P, hipMemcpyDeviceToHost, c->s));
+    ExchSide x;
+    if ((rc = exch_count(c, r, P, x))) return rc;
+    NCHK(c, ncclAllToAll(x.d_cnt(P), x.d_rcv(P), 2, ncclUint64, c->comm, c->s));
+    x.snd.assign(2 * P, 0);
+    x.rcv.assign(2 * P, 0);
+    HCHK(c, hipMemcpyAsync(x.snd.data(), x.d_cnt(P), 16 * P, hipMemcpyDeviceToHost, c->s));
+    HCHK(c, hipMemcpyAsync(x.rcv.data(), x.d_rcv(P), 16 * P, hipMemcpyDeviceToHost, c->s));
     HCHK(c, hipStreamSynchronize(c->s));
-    std::vector<size_t> sc(P), sd(P), rc_(P), rd(P), asc(P), asd(P), arc(P), ard(P);
-    std::vector<uint64_t> hbase(2 * P);
-    size_t srec = 0, sar = 0, rrec = 0, rar = 0;
-    for (int o = 0; o < P; o++) {
-        hbase[o] = srec;
-        hbase[P + o] = sar;
-        sc[o] = snd[2 * o] * sizeof(WireRec); sd[o] = srec * sizeof(WireRec); srec += snd[2 * o];
-        asc[o] = snd[2 * o + 1]; asd[o] = sar; sar += snd[2 * o + 1];
-        rc_[o] = rcv[2 * o] * sizeof(WireRec); rd[o] = rrec * sizeof(WireRec); rrec += rcv[2 * o];
-        arc[o] = rcv[2 * o + 1]; ard[o] = rar; rar += rcv[2 * o + 1];
-    }
-    DevBuf sbuf, rbuf, sar_b, rar_b, rmeta;
-    HCHK(c, sbuf.ensure(srec * sizeof(WireRec) + 64));
-    HCHK(c, rbuf.ensure(rrec * sizeof(WireRec) + 64));
-    HCHK(c, sar_b.ensure(sar + 64));
-    HCHK(c, rar_b.ensure(rar + 64));
-    HCHK(c, hipMemcpyAsync(d_base, hbase.data(), 16 * P, hipMemcpyHostToDevice, c->s));
-    if (r.n)
-        pack_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, d_base, d_base + P, d_cur, (WireRec*)sbuf.p, (uint8_t*)sar_b.p);
-    HCHK(c, hipGetLastError());
-    NCHK(c, ncclAllToAllv(sbuf.p, sc.data(), sd.data(), rbuf.p, rc_.data(), rd.data(), ncclUint8, c->comm, c->s));
-    NCHK(c, ncclAllToAllv(sar_b.p, asc.data(), asd.data(), rar_b.p, arc.data(), ard.data(), ncclUint8, c->comm, c->s));
+    if ((rc = exch_pack(c, r, P, x))) return rc;
+    const ExchPlan& pl = x.plan;
+    NCHK(c, ncclAllToAllv(x.sbuf.p, pl.sc.data(), pl.sd.data(), x.rbuf.p, pl.rc.data(), pl.rd.data(), ncclUint8,
+                          c->comm, c->s));
+    NCHK(c, ncclAllToAllv(x.sar_b.p, pl.asc.data(), pl.asd.data(), x.rar_b.p, pl.arc.data(), pl.ard.data(),
+                          ncclUint8, c->comm, c->s));
     HCHK(c, hipEventRecord(c->ev[7], c->s));
-    // unpack received records into a Recs view, then aggregate exactly
-    std::vector<uint64_t> hsrc(2 * P);
-    for (int o = 0; o < P; o++) { hsrc[o] = rd[o] / sizeof(WireRec); hsrc[P + o] = ard[o]; }
-    HCHK(c, rmeta.ensure(16 * P));
-    HCHK(c, hipMemcpyAsync(rmeta.p, hsrc.data(), 16 * P, hipMemcpyHostToDevice, c->s));
-    mrg_parts* tmp = nullptr;
-    if ((rc = parts_alloc(c, rrec, 0, local->app, local->nreduce, &tmp))) return rc;
-    cache_put(c->device, tmp->arena, tmp->arena_bytes);  // nothing has used it yet
-    tmp->arena = (uint8_t*)rar_b.adopt(&tmp->arena_bytes);  // adopt the received arena
-    tmp->r.arena = tmp->arena;
-    tmp->r.arena_n = rar;
-    if (rrec)
-        unpack_kernel<<<1024, 256, 0, c->s>>>((const WireRec*)rbuf.p, rrec, (const uint64_t*)rmeta.p,
-                                              (const uint64_t*)rmeta.p + P, (uint32_t)P, tmp->r);
-    HCHK(c, hipGetLastError());
-    rc = aggregate(c, {tmp->r}, local->app, local->nreduce, owned);
-    HCHK(c, hipStreamSynchronize(c->s));
+    rc = exch_finish(c, local, P, x, owned);
     c->stats.exchange_ms = ev_ms(c->ev[6], c->ev[7]);
-    mrg_parts_free(tmp);
-    sbuf.release(); rbuf.release(); sar_b.release(); rmeta.release(); scratch.release();
     return rc;
+}
+
+// The same exchange with P contexts driven by one host thread (one per GPU, or
+// several on one device): count / pack on every context, then the all-to-all
+// is peer copies, then unpack + aggregate on every owner.
+int mrg_exchange_group(mrg_ctx* const* ctxs, int P, const mrg_parts* const* local, mrg_parts** owned) {
+    if (!ctxs || !local || !owned || P < 1) return MRG_EINVAL;
+    for (int i = 0; i < P; i++) {
+        if (!ctxs[i] || !local[i]) return MRG_EINVAL;
+        owned[i] = nullptr;
+        if (local[i]->app != local[0]->app || local[i]->nreduce != local[0]->nreduce)
+            return fail(ctxs[i], MRG_EINVAL, "exchange_group: parts differ in app or nreduce");
+        for (int j = 0; j < i; j++)
+            if (ctxs[j] == ctxs[i]) return fail(ctxs[i], MRG_EINVAL, "exchange_group: context used twice");
+    }
+    std::vector<ExchSide> xs(P);
+    int rc;
+    auto undo = [&](int code) {
+        for (int i = 0; i < P; i++) {
+            if (owned[i]) mrg_parts_free(owned[i]);
+            owned[i] = nullptr;
+        }
+        for (int i = 0; i < P; i++) hipSetDevice(ctxs[i]->device), hipStreamSynchronize(ctxs[i]->s);
+        return code;
+    };
+    for (int i = 0; i < P; i++) {
+        mrg_ctx* c = ctxs[i];
+        if ((rc = bind(c))) return undo(rc);
+        HCHK(c, hipEventRecord(c->ev[6], c->s));
+        if ((rc = exch_count(c, local[i]->r, P, xs[i]))) return undo(rc);
+        xs[i].snd.assign(2 * P, 0);
+        if (hipMemcpyAsync(xs[i].snd.data(), xs[i].d_cnt(P), 16 * P, hipMemcpyDeviceToHost, c->s) != hipSuccess)
+            return undo(fail(c, MRG_EDEVICE, "exchange_group: count copy"));
+    }
+    for (int i = 0; i < P; i++) {
+        hipSetDevice(ctxs[i]->device);
+        if (hipStreamSynchronize(ctxs[i]->s) != hipSuccess) return undo(fail(ctxs[i], MRG_EDEVICE, "count sync"));
+    }
+    for (int j = 0; j < P; j++) {  // what owner j receives from source s = what s sends to j
+        xs[j].rcv.assign(2 * P, 0);
+        for (int s = 0; s < P; s++) {
+            xs[j].rcv[2 * s] = xs[s].snd[2 * j];
+            xs[j].rcv[2 * s + 1] = xs[s].snd[2 * j + 1];
+        }
+    }
+    for (int i = 0; i < P; i++) {
+        if ((rc = bind(ctxs[i]))) return undo(rc);
+        if ((rc = exch_pack(ctxs[i], local[i]->r, P, xs[i]))) return undo(rc);
+    }
+    for (int i = 0; i < P; i++) {  // every send segment is packed before any copy reads it
+        hipSetDevice(ctxs[i]->device);
+        if (hipStreamSynchronize(ctxs[i]->s) != hipSuccess) return undo(fail(ctxs[i], MRG_EDEVICE, "pack sync"));
+    }
+    for (int j = 0; j < P; j++) {
+        mrg_ctx* c = ctxs[j];
+        if ((rc = bind(c))) return undo(rc);
+        for (int s = 0; s < P; s++) {
+            const ExchPlan& ps = xs[s].plan;
+            const ExchPlan& pj = xs[j].plan;
+            if (pj.rc[s])
+                HCHK(c, hipMemcpyPeerAsync((uint8_t*)xs[j].rbuf.p + pj.rd[s], c->device,
+                                           (const uint8_t*)xs[s].sbuf.p + ps.sd[j], ctxs[s]->device, pj.rc[s], c->s));
+            if (pj.arc[s])
+                HCHK(c, hipMemcpyPeerAsync((uint8_t*)xs[j].rar_b.p + pj.ard[s], c->device,
+                                           (const uint8_t*)xs[s].sar_b.p + ps.asd[j], ctxs[s]->device, pj.arc[s],
+                                           c->s));
+        }
+        HCHK(c, hipEventRecord(c->ev[7], c->s));
+    }
+    for (int j = 0; j < P; j++) {  // the copies of owner j read every source's buffers: drain them all first
+        hipSetDevice(ctxs[j]->device);
+        if (hipStreamSynchronize(ctxs[j]->s) != hipSuccess) return undo(fail(ctxs[j], MRG_EDEVICE, "copy sync"));
+    }
+    for (int j = 0; j < P; j++) {
+        if ((rc = bind(ctxs[j]))) return undo(rc);
+        if ((rc = exch_finish(ctxs[j], local[j], P, xs[j], &owned[j]))) return undo(rc);
+        ctxs[j]->stats.exchange_ms = ev_ms(ctxs[j]->ev[6], ctxs[j]->ev[7]);
+    }
+    return MRG_OK;
 }
 
 int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const uint8_t* pat, size_t plen,

@@ -38,6 +38,7 @@ EXPORTED = [
     "mrg_open", "mrg_close", "mrg_last_error", "mrg_device_count", "mrg_map", "mrg_parts_merge",
     "mrg_parts_info", "mrg_parts_export", "mrg_parts_import", "mrg_parts_free", "mrg_reduce",
     "mrg_reduce_all", "mrg_run_job", "mrg_comm_unique_id", "mrg_comm_init", "mrg_exchange",
+    "mrg_exchange_group",
     "mrg_device_alloc", "mrg_device_free", "mrg_memcpy_h2d", "mrg_memcpy_d2h", "mrg_sync",
     "mrg_get_stats", "mrg_set_option", "mrg_ihash", "mrg_free",
 ]
@@ -107,6 +108,7 @@ def load_library(path: str | None = None):
     L.mrg_comm_unique_id.argtypes = [POINTER(c_uint8)]
     L.mrg_comm_init.argtypes = [vp, POINTER(c_uint8), c_int, c_int]
     L.mrg_exchange.argtypes = [vp, vp, POINTER(vp)]
+    L.mrg_exchange_group.argtypes = [POINTER(vp), c_int, POINTER(vp), POINTER(vp)]
     L.mrg_device_alloc.argtypes = [vp, c_size_t, POINTER(vp)]
     L.mrg_device_free.argtypes = [vp, vp]
     L.mrg_memcpy_h2d.argtypes = [vp, vp, vp, c_size_t]
@@ -298,6 +300,18 @@ class Context:
         out = c_void_p()
         self._check(self.L.mrg_exchange(self.h, parts.h, byref(out)), "mrg_exchange")
         return Parts(self, out)
+
+    @staticmethod
+    def exchange_group(ctxs: list["Context"], parts: list[Parts]) -> list[Parts]:
+        """mrg_exchange_group: the shuffle across P contexts of this process;
+        result i holds the partitions r with r % P == i, on ctxs[i]."""
+        P = len(ctxs)
+        assert P == len(parts) and P >= 1
+        hc = (c_void_p * P)(*[c.h for c in ctxs])
+        hp = (c_void_p * P)(*[p.h for p in parts])
+        out = (c_void_p * P)()
+        ctxs[0]._check(ctxs[0].L.mrg_exchange_group(hc, P, hp, out), "mrg_exchange_group")
+        return [Parts(ctxs[i], c_void_p(out[i])) for i in range(P)]
 
     # -- device memory
     def device_alloc(self, n: int) -> int:

@@ -125,6 +125,12 @@ int mrg_comm_unique_id(uint8_t id[128]);
 int mrg_comm_init(mrg_ctx* ctx, const uint8_t id[128], int nranks, int rank);
 /* Send every key to the owner of its partition; returns the owned partials. */
 int mrg_exchange(mrg_ctx* ctx, const mrg_parts* local, mrg_parts** owned);
+/* The same shuffle for P contexts driven by one host thread (one context per
+ * GPU of a single-process driver, or several on one device): owned[i] receives
+ * the partitions r with r % P == i from every local[j].  The all-to-all is peer
+ * copies instead of RCCL; packing, ownership and re-aggregation are shared with
+ * mrg_exchange.  Replaces the same mr/worker.go:80-122 file shuffle. */
+int mrg_exchange_group(mrg_ctx* const* ctxs, int nctx, const mrg_parts* const* local, mrg_parts** owned);
 
 /* Device memory helpers so callers can keep inputs resident in HBM. */
 int mrg_device_alloc(mrg_ctx* ctx, size_t n, void** dptr);

@@ -175,8 +175,9 @@ def test_exchange_single_rank(ctx):
 
 
 def test_exchange_rccl_one_rank():
-    """The RCCL path of mrg_exchange (pack, ncclAllToAll counts, ncclAllToAllv payload,
-    unpack, re-aggregate) with a 1-rank communicator, in its own context."""
+    """mrg_comm_init + mrg_exchange / mrg_run_job with a 1-rank RCCL communicator
+    (RCCL refuses two ranks on one GPU; the P > 1 pack / unpack path is covered
+    by test_exchange_group_multi_rank)."""
     from mrgpu import Context
     files = cases.synthetic(C.KIND_UTF8, 20000, [600_000], 17, 0.001)
     with Context(0) as c2:
@@ -185,6 +186,42 @@ def test_exchange_rccl_one_rank():
         q = c2.exchange(p)
         assert c2.reduce_all(q) == O.c_partitioned("wc", files, 6)
         assert c2.run_job(MRG_APP_WC, files[0], nreduce=6) == O.c_partitioned("wc", files, 6)
+
+
+@pytest.mark.parametrize("P,app,R", [(2, "wc", 10), (3, "wc", 64), (4, "grep:distributed", 10), (8, "wc", 64)])
+def test_exchange_group_multi_rank(P, app, R):
+    """The P > 1 shuffle (owner counts, pack per owner, all-to-all, unpack with the
+    sources' arena displacements, exact re-aggregation on the owner) with P
+    contexts on one device (mrg_exchange_group: peer copies where mrg_exchange
+    uses RCCL; everything else is the same code).  Rank i maps its own splits;
+    partition r comes from owner r % P and must equal the oracle's mr-out-r over
+    all ranks' inputs.  Long words (> 16 B, arena bytes) and UTF-8 included."""
+    from mrgpu import Context
+    a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
+    pat = b"" if app == "wc" else app[5:].encode()
+    files = []
+    for i in range(P):
+        if app == "wc":
+            f = cases.synthetic(C.KIND_UTF8, 20000, [200_000 + 37_000 * i], 40 + i, 0.001)[0]
+            f = f + b" " + b"longword" * (3 + i) + b" " + b"Z" * (17 + i) + b"\n"
+        else:
+            voc = C.Vocab(C.KIND_UTF8, 1.07, 20000, 50 + i)
+            f = bytes(voc.fill_files([150_000], [60 + i], C.grep_params(match_rate=0.03))[0])
+        files.append(f)
+    want = O.c_partitioned(app, files, R)
+    ctxs = [Context(0) for _ in range(P)]
+    try:
+        local = [ctxs[i].map(a, files[i], pattern=pat, nreduce=R) for i in range(P)]
+        owned = Context.exchange_group(ctxs, local)
+        for i in range(P):
+            out = ctxs[i].reduce_all(owned[i])
+            for r in range(R):
+                assert out[r] == (want[r] if r % P == i else b""), f"rank {i} partition {r}"
+        for q in local + owned:
+            q.free()
+    finally:
+        for c in ctxs:
+            c.close()
 
 
 def test_export_matches_host_codec(ctx):
