@@ -188,6 +188,7 @@ def main():
     ap.add_argument("--cpu-sample-files", type=int, default=16)
     ap.add_argument("--cpu-sample-mb", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--opt", action="append", default=[], help="library option name=value (experiments; repeatable)")
     args = ap.parse_args()
     w = WORKLOADS[args.workload]
     args.file_mb = args.file_mb or w["file_mb"]
@@ -214,6 +215,9 @@ def main():
     log(f"generated {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
 
     ctx = Context(local)
+    for o in args.opt:
+        k, v = o.split("=")
+        ctx.set_option(k, int(v))
     if world > 1:
         obj = [Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
@@ -309,7 +313,7 @@ def main():
             "data": "synthetic (deterministic Zipf corpus from csrc/corpus.c; reference pg-*.txt not bundled)",
             "config": {"workload": f"{w['desc']}; {nbytes / 1e9:.2f} GB per GPU ({args.files} files x "
                                    f"{args.file_mb} MB), device-resident input",
-                       "nreduce": args.nreduce, "input_bytes_per_gpu": nbytes, "parallelism": f"dp{world}",
+                       "nreduce": args.nreduce, "input_bytes_per_gpu": nbytes, "parallelism": f"dp{world}", **({"options": args.opt} if args.opt else {}),
                        "shuffle": "RCCL all-to-all" if world > 1 else "none (single GPU)"},
             "roofline": {"bound": "hbm", "kernel": "grep_map_kernel" if grep else "wc_map_kernel",
                          "achieved": round(achieved, 1),
@@ -326,6 +330,7 @@ def main():
             "spilled_words": int(last["lds_overflow"]),
             "spill_region_full_words": int(last["spill_ovf"]),
             "aggregator_miss_words": int(last["agg_miss"]),
+            "aggregation_rounds": int(last["agg_rounds"]),
             "output_bytes": int(last["output_bytes"]),
             "checks": checks,
             "cpu_baseline": cpu,

@@ -111,6 +111,13 @@ struct DevBuf {
         if (e == hipSuccess) cap = c;
         return e;
     }
+    // Like ensure(), but a growing buffer gets 25 % headroom: sizes that vary a
+    // little from call to call (spill totals) must not hipFree + hipMalloc
+    // gigabytes every step (measured: +1.3 ms per C2 step, seconds at C5).
+    hipError_t ensure_grow(size_t n) {
+        if (n <= cap) return hipSuccess;
+        return ensure(n + n / 4);
+    }
     void release() {
         if (p) hipFree(p);
         p = nullptr;
@@ -135,13 +142,21 @@ struct mrg_ctx {
     uint32_t* d_l2 = nullptr;
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
     DevBuf bflag, dict, dict_cnt, sample, recbuf, recarena, sortbuf, dbg;
+    DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
+    int agg_rounds = 8;                 // bucket aggregation rounds at most (the last sends leftovers to HBM)
+    // Misses per bucket below which a round settles them in the HBM table instead
+    // of carrying them.  0 (default): always carry.  Measured on C5: 4096 made
+    // the aggregation 59 ms -> 2.8 s (HBM inserts of hot leftover keys), while
+    // carrying C2's ~200 misses per bucket costs one short extra round.
+    uint32_t agg_carry_min = 0;
+    double spill_scale = 1.0;           // spill stream capacity factor (from the dictionary sample's miss rate)
     bool debug_times = getenv("MRG_DEBUG_TIMES") != nullptr;
     uint64_t rec_cap = 1u << 21;       // record output buffer capacity (grows on overflow)
     bool sh_clean = false;             // ShortTable known to be empty (skip its clear)
     int dict_mode = 0;                 // <0: never build the hot-key dictionary
     uint64_t dict_min_bytes = 32ull << 20;
     uint64_t dict_sample_bytes = 16ull << 20;  // C2: 16 vs 64 MB loses 0.13% of dictionary hits, halves the build
-    uint64_t spill_sub_keys = 0, spill_sub8 = 0, spill_amiss_cap = 0;
+    uint64_t spill_sub_keys = 0, spill_sub8 = 0;
     uint32_t spill_nwg = 1;
     int64_t spill_force_sub = 0;
     int map_mode = 0;  // benchmark ablation of wc_map_kernel phases (0 = normal)
@@ -151,6 +166,7 @@ struct mrg_ctx {
     ReduceWs* rws = nullptr;
     mrg_stats stats{};
     Counters* h_ctr = nullptr;     // pinned
+    uint64_t* h_scr = nullptr;     // pinned scratch for small device -> host reads (8 words)
     uint8_t* h_out = nullptr;      // pinned result buffer for mrg_run_job
     size_t h_out_cap = 0;
     ncclComm_t comm = nullptr;
@@ -213,8 +229,16 @@ static Tables make_tables(mrg_ctx* c) {
     t.sp.nwg = c->spill_nwg;
     t.sp.counts = (uint32_t*)c->spmeta.p;
     t.sp.counts8 = c->spmeta.p ? t.sp.counts + (size_t)kSpillBuckets * c->spill_nwg : nullptr;
-    t.sp.amiss = c->spool.p ? (uint4*)(t.sp.pool8 + c->spill_sub8 * kSpillBuckets * c->spill_nwg) : nullptr;
-    t.sp.amiss_cap = (uint32_t)c->spill_amiss_cap;
+    t.sp.seg_off8 = t.sp.seg_off16 = nullptr;
+    t.sp.seg_n_in = nullptr;
+    t.sp.seg_n_out = nullptr;
+    t.sp.seg8_in = nullptr;
+    t.sp.seg8_out = nullptr;
+    t.sp.seg16_in = nullptr;
+    t.sp.seg16_out = nullptr;
+    t.sp.round = 0;
+    t.sp.last = 1;
+    t.sp.carry_min = c->agg_carry_min;
     t.out = Recs{};
     t.out_cap = 0;
     t.nreduce = 1;
@@ -242,14 +266,15 @@ static Recs rec_view(mrg_ctx* c) {
     return r;
 }
 
-// Spill pool for LDS-combiner misses: 1.5 bytes of pool per input byte (C2
+// Spill pool for dictionary misses: 1.5 bytes of pool per input byte (C2
 // spills ~0.5 bytes of records per input byte), split into kSpillBuckets x nwg
-// streams of 16-byte records (0.75 B/B) and as many of 8-byte records (0.75 B/B).
+// streams of 16-byte records (0.75 B/B) and as many of 8-byte records (0.75 B/B),
+// times c->spill_scale when the dictionary sample shows a higher miss rate.
 // A stream that fills up sends the rest of its keys to the HBM table, so the
 // size only affects speed, never results.
 static int ensure_spill(mrg_ctx* c, uint64_t n) {
     const uint32_t nwg = wc_map_grid(n, c->grid);
-    uint64_t sub = (n - n / 4) / 16 / ((uint64_t)kSpillBuckets * nwg) + 64;
+    uint64_t sub = (uint64_t)((double)((n - n / 4) / 16 / ((uint64_t)kSpillBuckets * nwg)) * c->spill_scale) + 64;
     sub = (sub + 63) & ~63ull;
     uint64_t sub8 = 2 * sub;
     if (c->spill_force_sub > 0) sub = sub8 = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
@@ -259,9 +284,7 @@ static int ensure_spill(mrg_ctx* c, uint64_t n) {
     c->spill_nwg = nwg;
     c->spill_sub_keys = sub;
     c->spill_sub8 = sub8;
-    c->spill_amiss_cap = c->spill_force_sub > 0 ? sub : 8 * sub;  // per bucket; beyond it misses insert inline
-    HCHK(c, c->spool.ensure((sub * sizeof(uint4) + sub8 * sizeof(uint64_t)) * kSpillBuckets * nwg +
-                            c->spill_amiss_cap * sizeof(uint4) * kSpillBuckets));
+    HCHK(c, c->spool.ensure_grow((sub * sizeof(uint4) + sub8 * sizeof(uint64_t)) * kSpillBuckets * nwg));
     HCHK(c, c->spmeta.ensure((size_t)2 * kSpillBuckets * nwg * sizeof(uint32_t)));
     return MRG_OK;
 }
@@ -420,7 +443,7 @@ static void print_stamps(mrg_ctx* c, const char* what, uint32_t nblocks, uint32_
 // become the records the final dictionary is built from.  Only speed depends
 // on the dictionary: every key it misses is counted exactly through the spill.
 static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win, uint32_t nwin, LetterTables lt,
-                       bool with_dict, uint64_t* nrec_out) {
+                       bool with_dict, uint64_t* nrec_out, double* spill_rate = nullptr) {
     const uint64_t stride = ((len - win) / nwin) & ~15ull;
     const uint64_t sn = (uint64_t)nwin * (win + 16);
     HCHK(c, c->sample.ensure(sn + 64));
@@ -441,6 +464,7 @@ static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win
     print_stamps(c, with_dict ? "sample agg (level 2)" : "sample agg (level 1)", kSpillBuckets);
     if ((rc = read_counters(c))) return rc;
     *nrec_out = std::min<uint64_t>(c->h_ctr->nrec, c->rec_cap);
+    if (spill_rate) *spill_rate = (double)(c->h_ctr->spilled + c->h_ctr->spill_ovf) / (double)sn;
     return MRG_OK;
 }
 
@@ -477,11 +501,78 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
     if (nrec == 0) return MRG_OK;
     if ((rc = dict_from_recs(c, nrec))) return rc;
     if (target > small) {
-        if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, target / win), lt, true, &nrec))) return rc;
+        double rate = 0;
+        if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, target / win), lt, true, &nrec, &rate)))
+            return rc;
         if (nrec && (rc = dict_from_recs(c, nrec))) return rc;
+        // Spill streams hold 0.094 8-byte records per input byte at scale 1 (C2
+        // spills 0.04).  A split whose sample misses its (first-level) dictionary
+        // more often gets proportionally longer streams, 30 % over the estimate
+        // (the final dictionary only hits more).  Never shrinks within a context.
+        const double need = 1.3 * rate / (2.0 * 0.75 / 16.0);
+        if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
     }
     c->stats.dict_keys = nrec;
     *have = true;
+    return MRG_OK;
+}
+
+// Bucket aggregation in rounds.  Round 0 reads the map's spill streams; the
+// keys a bucket's LDS tables cannot hold go to per-(bucket, wave) miss segments,
+// which are the next round's input (a fresh table per bucket and round).  The
+// last round (c->agg_rounds, or the first with nothing carried) counts the rest
+// in the HBM table.  Typical splits finish in round 0; 1e7-key splits need a
+// few rounds, each re-reading only the keys still unsettled.
+static int aggregate_rounds(mrg_ctx* c, Tables& t) {
+    constexpr uint64_t E = (uint64_t)kSpillBuckets * kAggSegs;
+    const size_t meta = 2 * E * 4 + 2 * (E + 1) * 8 + 2 * (2 * E * 4) + 64;
+    HCHK(c, c->segmeta.ensure(meta));
+    uint32_t* tmp = (uint32_t*)c->segmeta.p;
+    uint64_t* off8 = (uint64_t*)(tmp + 2 * E);
+    uint64_t* off16 = off8 + E + 1;
+    uint32_t* cnt[2] = {(uint32_t*)(off16 + E + 1), (uint32_t*)(off16 + E + 1) + 2 * E};
+    launch_seg_layout(t, tmp, off8, off16, c->s);
+    uint64_t* tot = c->h_scr;  // pinned
+    HCHK(c, hipMemcpyAsync(&tot[0], off8 + E, 8, hipMemcpyDeviceToHost, c->s));
+    HCHK(c, hipMemcpyAsync(&tot[1], off16 + E, 8, hipMemcpyDeviceToHost, c->s));
+    HCHK(c, hipStreamSynchronize(c->s));
+    for (int i = 0; i < 2; i++) {
+        HCHK(c, c->seg8[i].ensure_grow(tot[0] * 8 + 64));
+        HCHK(c, c->seg16[i].ensure_grow(tot[1] * 16 + 64));
+    }
+    t.sp.seg_off8 = off8;
+    t.sp.seg_off16 = off16;
+    const int rounds = std::max(1, c->agg_rounds);
+    int r = 0;
+    for (;; r++) {
+        const int o = r & 1, p = o ^ 1;
+        t.sp.round = (uint32_t)r;
+        t.sp.last = r + 1 >= rounds;
+        t.sp.seg_n_in = cnt[p];
+        t.sp.seg_n_out = cnt[o];
+        t.sp.seg8_in = (const uint64_t*)c->seg8[p].p;
+        t.sp.seg8_out = (uint64_t*)c->seg8[o].p;
+        t.sp.seg16_in = (const uint4*)c->seg16[p].p;
+        t.sp.seg16_out = (uint4*)c->seg16[o].p;
+        HCHK(c, hipMemsetAsync(&t.ctr->carried, 0, 8, c->s));
+        if (c->debug_times) HCHK(c, hipEventRecord(c->ev[11], c->s));
+        launch_wc_agg(t, c->map_mode, 1, c->s);
+        HCHK(c, hipGetLastError());
+        if (c->debug_times) {  // diagnostics: per-round time and carried misses
+            HCHK(c, hipEventRecord(c->ev[5], c->s));
+            HCHK(c, hipMemcpyAsync(&c->h_scr[3], &t.ctr->carried, 8, hipMemcpyDeviceToHost, c->s));
+            HCHK(c, hipStreamSynchronize(c->s));
+            fprintf(stderr, "[mrg rounds] round %d: %.3f ms, carried %llu\n", r, ev_ms(c->ev[11], c->ev[5]),
+                    (unsigned long long)c->h_scr[3]);
+        }
+        if (t.sp.last) break;
+        if ((r & 1) == 0) continue;  // rounds go in pairs: one host round trip per two (typical splits: 2 rounds)
+        HCHK(c, hipMemcpyAsync(&c->h_scr[2], &t.ctr->carried, 8, hipMemcpyDeviceToHost, c->s));
+        HCHK(c, hipStreamSynchronize(c->s));
+        if (c->h_scr[2] == 0) break;
+    }
+    t.sp.round = 0;
+    t.sp.last = 1;
     return MRG_OK;
 }
 
@@ -494,6 +585,9 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
     HCHK(c, hipEventRecord(c->ev[9], c->s));
     bool have_dict = false;
     if (c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict))) return rc;
+    // the sample may have raised spill_scale: size the streams for this split now,
+    // not only from the next call on (overflowing streams merge through HBM: slow)
+    if ((rc = ensure_spill(c, len))) return rc;
     HCHK(c, hipEventRecord(c->ev[10], c->s));
     for (int attempt = 0; attempt < 8; attempt++) {
         if ((rc = ensure_tables(c)) || (rc = ensure_recbuf(c))) return rc;
@@ -508,7 +602,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             return fail(c, MRG_EINVAL, "split too large for 32-bit chunk indices (%llu bytes)", (unsigned long long)len);
         HCHK(c, hipEventRecord(c->ev[1], c->s));
         print_stamps(c, "map", nwg, kSpillBuckets);
-        launch_wc_agg(t, c->map_mode, 1, c->s);
+        if ((rc = aggregate_rounds(c, t))) return rc;
         print_stamps(c, "agg", kSpillBuckets);
         if (have_dict) launch_dict_emit(t, nwg, c->s);
         HCHK(c, hipEventRecord(c->ev[8], c->s));
@@ -556,6 +650,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         c->stats.lds_overflow = h.spilled + h.spill_ovf;
         c->stats.spill_ovf = h.spill_ovf;
         c->stats.agg_miss = h.agg_miss;
+        c->stats.agg_rounds = (uint64_t)__builtin_popcountll(h.round_mask);
         c->stats.dict_hits = h.dict_hits;
         c->stats.distinct_keys = h.nrec;
         c->stats.long_keys = h.nlong_rec;
@@ -594,7 +689,8 @@ int mrg_open(int device, mrg_ctx** out) {
     }
     hipMemcpy(c->d_l1, mrg_letter_l1_init, sizeof(mrg_letter_l1_init), hipMemcpyHostToDevice);
     hipMemcpy(c->d_l2, mrg_letter_l2_init, sizeof(mrg_letter_l2_init), hipMemcpyHostToDevice);
-    if (hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_scr, 8 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
         mrg_close(c);
         return MRG_ENOMEM;
     }
@@ -610,11 +706,13 @@ void mrg_close(mrg_ctx* c) {
     if (c->s) hipStreamSynchronize(c->s);
     if (c->comm) ncclCommDestroy(c->comm);
     DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spmeta,
-                    &c->bflag, &c->dict, &c->dict_cnt, &c->sample, &c->recbuf, &c->recarena, &c->sortbuf};
+                    &c->bflag, &c->dict, &c->dict_cnt, &c->sample, &c->recbuf, &c->recarena, &c->sortbuf,
+                    &c->segmeta, &c->seg8[0], &c->seg8[1], &c->seg16[0], &c->seg16[1]};
     for (DevBuf* b : bs) b->release();
     if (c->d_l1) hipFree(c->d_l1);
     if (c->d_l2) hipFree(c->d_l2);
     if (c->h_ctr) hipHostFree(c->h_ctr);
+    if (c->h_scr) hipHostFree(c->h_scr);
     if (c->h_out) hipHostFree(c->h_out);
     reduce_ws_free(c->rws);
     for (auto& e : c->ev)
@@ -633,6 +731,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "map_grid")) c->grid = v > 0 ? (int)v : map_grid_size(c->device);
     else if (!strcmp(name, "map_mode")) c->map_mode = (int)v;
     else if (!strcmp(name, "spill_stream_keys")) c->spill_force_sub = v > 0 ? v : 0;
+    else if (!strcmp(name, "agg_rounds")) c->agg_rounds = v > 0 ? (int)v : 8;
+    else if (!strcmp(name, "agg_carry_min")) c->agg_carry_min = v > 0 ? (uint32_t)v : 0u;
     else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
     else if (!strcmp(name, "dict_min_bytes")) c->dict_min_bytes = v > 0 ? (uint64_t)v : (32ull << 20);
     else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);

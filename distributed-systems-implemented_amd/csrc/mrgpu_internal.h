@@ -56,7 +56,9 @@ struct Counters {
     unsigned long long agg_miss;   // spill keys that missed the bucket aggregator's LDS table
     unsigned long long bflush;     // spill buckets merged through the HBM table (overflow somewhere)
     unsigned long long dict_hits;  // occurrences counted by the hot-key dictionary
-    unsigned long long pad[3];
+    unsigned long long carried;    // aggregator misses carried to the next round
+    unsigned long long round_mask; // bit r: aggregation round r had input
+    unsigned long long pad[1];
 };
 
 // Spill of dictionary misses, hash-partitioned into kSpillBuckets buckets.
@@ -68,6 +70,7 @@ struct Counters {
 // the HBM table instead.
 constexpr int kSpillBuckets = 512;
 constexpr int kMaxMapWGs = 512;   // map workgroups (spill streams per bucket) at most
+constexpr int kAggSegs = 8;       // aggregator waves per bucket = miss segments per bucket
 // Keys of at most 8 bytes (k1 == 0) are spilled as 8-byte records into pool8,
 // longer ones as 16-byte records into pool: the combiner's misses are mostly
 // tail words, and most words are short, so this roughly halves spill traffic.
@@ -77,9 +80,23 @@ struct Spill {
     uint64_t sub_keys, sub8;         // stream capacities (records)
     uint32_t* counts;                // [kSpillBuckets * nwg] records in each 16-byte stream
     uint32_t* counts8;               // [kSpillBuckets * nwg] records in each 8-byte stream
-    uint4* amiss;                    // [kSpillBuckets][amiss_cap] aggregator misses, inserted after its loop
-    uint32_t amiss_cap;
     uint32_t nwg;
+    // Multi-round bucket aggregation (high-cardinality buckets): the keys a round
+    // could not hold in LDS are the next round's input.  Misses are appended to
+    // per-(bucket, aggregator wave) segments; a segment's capacity is the records
+    // that wave read in round 0 (a wave only ever re-reads its own segment), so the
+    // offsets seg_off* are fixed over the rounds and the buffers ping-pong.
+    const uint64_t* seg_off8;        // [kSpillBuckets * kAggSegs + 1] 8-byte segment offsets (records)
+    const uint64_t* seg_off16;       // [kSpillBuckets * kAggSegs + 1] 16-byte segment offsets
+    const uint32_t* seg_n_in;        // [2][kSpillBuckets * kAggSegs] records in each input segment (8-B, 16-B)
+    uint32_t* seg_n_out;             // same layout: records appended this round
+    const uint64_t* seg8_in;
+    uint64_t* seg8_out;
+    const uint4* seg16_in;
+    uint4* seg16_out;
+    uint32_t round;                  // 0: the input is the map's spill streams; > 0: seg*_in
+    uint32_t last;                   // nonzero: unsettled misses go to the HBM table (final round)
+    uint32_t carry_min;              // a bucket with fewer misses than this settles them in the HBM table
 };
 
 // Hot-key dictionary (wc): a static table of the most frequent keys of a
@@ -139,6 +156,10 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
 //       1 = emit records directly unless the bucket overflowed (then merge through HBM),
 //       2 = sample mode: emit table keys, drop misses (approximate counts for the dictionary)
 void launch_wc_agg(const Tables& t, int mode, int emit, hipStream_t s);
+// Segment layout of the multi-round aggregation (Spill::seg_off*) from the map's
+// stream counts; off8[E] / off16[E] (E = kSpillBuckets * kAggSegs) are the totals.
+// tmp: 2 * E u32 of scratch.
+void launch_seg_layout(const Tables& t, uint32_t* tmp, uint64_t* off8, uint64_t* off16, hipStream_t s);
 void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s);
 // Gather `nwin` windows of `win` bytes (stride `stride`) of in[0,n) into dst, each followed by '\n'.
 void launch_sample_gather(const uint8_t* in, uint64_t n, uint64_t win, uint64_t stride, uint32_t nwin, uint8_t* dst,

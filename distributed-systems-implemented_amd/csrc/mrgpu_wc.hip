@@ -511,8 +511,9 @@ struct alignas(16) AggLds {
     uint32_t sc[kAggShortSets * 4 + kWave];      // counts (+ per-lane dummies for branch-free adds)
     uint32_t mc[kAggMidSets * 4];
     unsigned long long red[4 * kAggWaves + 4];   // block_add4 / block_alloc scratch
-    uint32_t nmiss;                              // keys appended to the bucket's miss list
+    uint32_t ncur8[kAggWaves], ncur16[kAggWaves];  // misses appended to each wave's segments
 };
+static_assert(kAggWaves == kAggSegs, "one miss segment per aggregator wave");
 static_assert(2 * sizeof(AggLds) <= 160 * 1024, "two aggregator workgroups per CU");
 
 __device__ __forceinline__ uint32_t second_hash(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 16) * 0xC2B2AE3Du; }
@@ -638,25 +639,33 @@ __device__ __forceinline__ void put_short(const Tables& t, unsigned long long o,
 // together); hits add (a per-lane dummy counter for lanes without one), and
 // only first occurrences and collisions take the claim path.
 
+// A key the tables could not take: appended to the wave's own miss segment
+// (LDS cursor, no HBM round trip in the loop).  It never exceeds the segment:
+// a wave's misses are at most the records it reads.
 __device__ __forceinline__ void defer_miss(AggLds& A, const Tables& t, uint64_t k0, uint64_t k1, bool keep_miss,
-                                           uint64_t& miss) {
-    const uint32_t pos = atomicAdd(&A.nmiss, 1u);  // no HBM round trip in the loop
+                                           uint32_t wv, uint64_t& miss) {
     if (keep_miss) {
-        if (pos < t.sp.amiss_cap)
-            t.sp.amiss[(uint64_t)blockIdx.x * t.sp.amiss_cap + pos] =
+        const uint64_t seg = (uint64_t)blockIdx.x * kAggSegs + wv;
+        if (k1 == 0) {
+            const uint32_t pos = atomicAdd(&A.ncur8[wv], 1u);
+            t.sp.seg8_out[t.sp.seg_off8[seg] + pos] = k0;
+        } else {
+            const uint32_t pos = atomicAdd(&A.ncur16[wv], 1u);
+            t.sp.seg16_out[t.sp.seg_off16[seg] + pos] =
                 make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
-        else
-            short_insert(t, k0, k1, 1);
+        }
     }
     miss++;
 }
 
 template <uint32_t amode, bool kMid, uint32_t kAggUnroll>
 __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void* pool_b, const uint32_t* gcounts,
-                                         uint64_t gstride, bool keep_miss, uint64_t& miss) {
+                                         uint64_t gstride, uint32_t nwg, const uint64_t* gbase, bool keep_miss,
+                                         uint64_t& miss) {
+    // streams s < nwg: gcounts[s] records at pool_b[gbase ? gbase[s] : s * gstride]
     constexpr uint32_t kAggBlock = kAggUnroll * kWave;
     static_assert(kMaxMapWGs <= kAggWaves * kWave, "a wave's stream counts fit one VGPR");
-    const uint32_t nwg = t.sp.nwg, lane = threadIdx.x & 63;
+    const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // The wave's streams are wv + kAggWaves * j, j < js; lane j holds stream j's
     // record count, so moving to the next stream is a readlane, not a load.
@@ -670,7 +679,8 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
     }
     uint4 cur[kAggUnroll], nxt[kAggUnroll];
     auto load = [&](uint32_t jj, uint32_t o, uint32_t c, uint4* r) {
-        const uint64_t row = (uint64_t)(wv + kAggWaves * jj) * gstride;
+        const uint32_t sid = wv + kAggWaves * jj;
+        const uint64_t row = gbase ? (jj < js ? gbase[sid] : 0ull) : (uint64_t)sid * gstride;
 #pragma unroll
         for (uint32_t u = 0; u < kAggUnroll; u++) {
             const uint32_t i = o + u * kWave + lane;
@@ -722,7 +732,7 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
             for (uint32_t u = 0; u < kAggUnroll; u++) {
                 if (slow[u]) {
                     const uint64_t k = ((uint64_t)cur[u].y << 32) | cur[u].x;
-                    if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, miss);
+                    if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
                 }
             }
         } else {
@@ -730,7 +740,7 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
             for (uint32_t u = 0; u < kAggUnroll; u++) {
                 if ((cur[u].x | cur[u].y) != 0) {
                     const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
-                    if (!mid_insert(A, k0, k1, h[u], 1)) defer_miss(A, t, k0, k1, keep_miss, miss);
+                    if (!mid_insert(A, k0, k1, h[u], 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
                 }
             }
         }
@@ -747,7 +757,18 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
 template <uint32_t amode>
 __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit) {
     __shared__ AggLds A;
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uint64_t b = blockIdx.x;
+    constexpr uint32_t E = (uint32_t)kSpillBuckets * kAggSegs;
+    const bool later = t.sp.round != 0;
+    if (later) {  // a later round: buckets with nothing carried over have nothing to do
+        uint32_t tot = 0;
+        for (uint32_t i = 0; i < kAggSegs; i++) tot += t.sp.seg_n_in[b * kAggSegs + i] + t.sp.seg_n_in[E + b * kAggSegs + i];
+        if (tot == 0) {
+            if (tid < kAggSegs) t.sp.seg_n_out[b * kAggSegs + tid] = t.sp.seg_n_out[E + b * kAggSegs + tid] = 0;
+            return;
+        }
+    }
     if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
     for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4 + kWave; i += kAggThreads) A.sc[i] = 0;
     for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) A.sk[i] = 0;
@@ -756,22 +777,34 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
         A.mk[2 * i + 1] = kUnwritten;
         A.mc[i] = 0;
     }
-    if (tid == 0) A.nmiss = 0;
+    if (tid < kAggWaves) A.ncur8[tid] = A.ncur16[tid] = 0;
+    if (tid == 0 && emit == 1) atomicOr(&t.ctr->round_mask, 1ull << (t.sp.round & 63));
     __syncthreads();
-    const uint64_t b = blockIdx.x;
     const bool keep_miss = emit != 2;
-    uint64_t miss = 0;
-    // bucket b's stream of workgroup g: pool[(g * kSpillBuckets + b) * sub]
-    agg_pool<amode, false, 8>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg,
-                           (uint64_t)kSpillBuckets * t.sp.sub8, keep_miss, miss);
-    agg_pool<amode, true, 4>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
-                          (uint64_t)kSpillBuckets * t.sp.sub_keys, keep_miss, miss);
+    uint64_t miss = 0, carried = 0;
+    if (!later) {
+        // round 0: bucket b's stream of map workgroup g is pool[(g * kSpillBuckets + b) * sub]
+        agg_pool<amode, false, 8>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg,
+                                  (uint64_t)kSpillBuckets * t.sp.sub8, t.sp.nwg, nullptr, keep_miss, miss);
+        agg_pool<amode, true, 4>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
+                                 (uint64_t)kSpillBuckets * t.sp.sub_keys, t.sp.nwg, nullptr, keep_miss, miss);
+    } else {
+        // later rounds: wave w re-reads its own segment of the previous round's misses
+        agg_pool<amode, false, 8>(A, t, t.sp.seg8_in, t.sp.seg_n_in + b * kAggSegs, 0, kAggSegs,
+                                  t.sp.seg_off8 + b * kAggSegs, keep_miss, miss);
+        agg_pool<amode, true, 4>(A, t, t.sp.seg16_in, t.sp.seg_n_in + E + b * kAggSegs, 0, kAggSegs,
+                                 t.sp.seg_off16 + b * kAggSegs, keep_miss, miss);
+    }
     __syncthreads();
-    const uint32_t nm = min(A.nmiss, t.sp.amiss_cap);
+    // this wave's miss segments (written by its own lanes in the loop above)
+    const uint64_t seg = b * kAggSegs + wv;
+    const uint32_t n8 = keep_miss ? A.ncur8[wv] : 0u, n16 = keep_miss ? A.ncur16[wv] : 0u;
+    uint64_t* s8 = keep_miss ? t.sp.seg8_out + t.sp.seg_off8[seg] : nullptr;
+    uint4* s16 = keep_miss ? t.sp.seg16_out + t.sp.seg_off16[seg] : nullptr;
     // merge: a key of this bucket went to the HBM table from the map kernel
-    // (stream overflow) or a deferred miss did not fit the miss list, so the same
-    // key may be on both sides: merge the whole bucket through the HBM table.
-    const bool merge = emit == 0 || (emit == 1 && (t.bflag[b] != 0 || A.nmiss > t.sp.amiss_cap));
+    // (stream overflow), so the same key may be on both sides: merge the whole
+    // bucket (tables and misses) through the HBM table.
+    const bool merge = emit == 0 || (emit == 1 && t.bflag[b] != 0);
     if (merge) {
         for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) {
             const uint64_t k0 = A.sk[i];
@@ -781,30 +814,59 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
             const uint64_t k0 = A.mk[2 * i];
             if (k0 != 0) short_insert(t, k0, A.mk[2 * i + 1], A.mc[i]);
         }
-        for (uint32_t i = tid; i < nm; i += kAggThreads) {  // deferred misses, all lanes in flight
-            const uint4 k = t.sp.amiss[b * t.sp.amiss_cap + i];
-            short_insert(t, ((uint64_t)k.y << 32) | k.x, ((uint64_t)k.w << 32) | k.z, 1);
+        for (uint32_t i = lane; i < n8; i += kWave) {  // misses, all lanes in flight
+            const uint64_t k0 = s8[i];
+            if (k0 != 0) short_insert(t, k0, 0, 1);
         }
+        for (uint32_t i = lane; i < n16; i += kWave) {
+            const uint4 k = s16[i];
+            const uint64_t k0 = ((uint64_t)k.y << 32) | k.x;
+            if (k0 != 0) short_insert(t, k0, ((uint64_t)k.w << 32) | k.z, 1);
+        }
+        if (t.sp.seg_n_out && lane == 0) t.sp.seg_n_out[seg] = t.sp.seg_n_out[E + seg] = 0;
         if (tid == 0) atomicAdd(&t.ctr->bflush, 1ull);
     } else {
-        // Deferred misses: counted in the (now stable) tables when their key is
-        // there, otherwise in the HBM table — so the tables' keys and the HBM
-        // table's keys of this bucket are disjoint and the tables are emitted as is.
-        if (emit == 1)
-            for (uint32_t i = tid; i < nm; i += kAggThreads) {
-                const uint4 k = t.sp.amiss[b * t.sp.amiss_cap + i];
-                const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
-                const uint32_t h = fold32(k.x, k.y, k.z, k.w);
-                if (k1 == 0) {
-                    const int slot = short_find_exact(A, k0, h);
+        // Settle the misses against the (now stable) tables: a key that is there
+        // is counted there and its record cleared; the others are carried to the
+        // next round (or, in the last round, counted in the HBM table).  So the
+        // keys of every round's tables and of the HBM table are disjoint, and the
+        // tables are emitted as they are.
+        if (emit == 1) {
+            // A bucket with fewer misses than carry_min (option; 0 = never)
+            // settles them in the HBM table now instead of carrying them.
+            uint32_t left = 0;
+            for (uint32_t w = 0; w < kAggWaves; w++) left += A.ncur8[w] + A.ncur16[w];
+            const bool last = t.sp.last != 0 || left < t.sp.carry_min;
+            for (uint32_t i = lane; i < n8; i += kWave) {
+                const uint64_t k0 = s8[i];
+                if (k0 == 0) continue;
+                const int slot = short_find_exact(A, k0, fold32((uint32_t)k0, (uint32_t)(k0 >> 32), 0, 0));
+                if (slot >= 0 || last) {
                     if (slot >= 0) atomicAdd(&A.sc[slot], 1u);
-                    else short_insert(t, k0, k1, 1);
+                    else short_insert(t, k0, 0, 1);
+                    s8[i] = 0;
                 } else {
-                    const int slot = mid_find_exact(A, k0, k1, h);
-                    if (slot >= 0) atomicAdd(&A.mc[slot], 1u);
-                    else short_insert(t, k0, k1, 1);
+                    carried++;
                 }
             }
+            for (uint32_t i = lane; i < n16; i += kWave) {
+                const uint4 k = s16[i];
+                const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
+                if (k0 == 0) continue;
+                const int slot = mid_find_exact(A, k0, k1, fold32(k.x, k.y, k.z, k.w));
+                if (slot >= 0 || last) {
+                    if (slot >= 0) atomicAdd(&A.mc[slot], 1u);
+                    else short_insert(t, k0, k1, 1);
+                    s16[i] = make_uint4(0, 0, 0, 0);
+                } else {
+                    carried++;
+                }
+            }
+            if (t.sp.seg_n_out && lane == 0) {
+                t.sp.seg_n_out[seg] = last ? 0u : n8;
+                t.sp.seg_n_out[E + seg] = last ? 0u : n16;
+            }
+        }
         __syncthreads();
         // one cursor allocation per workgroup, then each thread writes its keys
         uint32_t mine = 0;
@@ -821,8 +883,62 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
         }
     }
     if (amode != 0 && miss == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // no DCE in ablation builds
-    block_add4<kAggWaves>(&t.ctr->agg_miss, nullptr, nullptr, nullptr, amode == 0 ? miss : 0, 0, 0, 0, A.red);
+    block_add4<kAggWaves>(&t.ctr->agg_miss, &t.ctr->carried, nullptr, nullptr, amode == 0 ? miss : 0, carried, 0, 0,
+                          A.red);
     if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+}
+
+// Multi-round layout, step 1: records of bucket b's streams per aggregator wave
+// (wave w reads streams w, w + kAggWaves, ...), clamped like the aggregator's reads.
+__global__ void __launch_bounds__(kMaxMapWGs) seg_count_kernel(Spill sp, uint32_t* tmp) {
+    __shared__ uint32_t sum[2 * kAggSegs];
+    const uint32_t b = blockIdx.x, g = threadIdx.x;
+    if (g < 2 * kAggSegs) sum[g] = 0;
+    __syncthreads();
+    if (g < sp.nwg) {
+        atomicAdd(&sum[g % kAggSegs], sp.counts8[(uint64_t)b * sp.nwg + g]);
+        atomicAdd(&sum[kAggSegs + g % kAggSegs], sp.counts[(uint64_t)b * sp.nwg + g]);
+    }
+    __syncthreads();
+    constexpr uint32_t E = (uint32_t)kSpillBuckets * kAggSegs;
+    if (g < kAggSegs) {
+        tmp[b * kAggSegs + g] = sum[g];
+        tmp[E + b * kAggSegs + g] = sum[kAggSegs + g];
+    }
+}
+
+// Step 2: exclusive scans (one workgroup; 4 entries per thread), totals at [E].
+__global__ void __launch_bounds__(1024) seg_scan_kernel(const uint32_t* tmp, uint64_t* off8, uint64_t* off16) {
+    constexpr uint32_t E = (uint32_t)kSpillBuckets * kAggSegs, PER = E / 1024;
+    static_assert(E % 1024 == 0, "scan layout");
+    __shared__ unsigned long long part[2][1024];
+    const uint32_t tid = threadIdx.x;
+    uint64_t a = 0, c = 0;
+    for (uint32_t q = 0; q < PER; q++) {
+        a += tmp[tid * PER + q];
+        c += tmp[E + tid * PER + q];
+    }
+    part[0][tid] = a;
+    part[1][tid] = c;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan of the thread totals
+        const unsigned long long x = tid >= d ? part[0][tid - d] : 0ull, y = tid >= d ? part[1][tid - d] : 0ull;
+        __syncthreads();
+        part[0][tid] += x;
+        part[1][tid] += y;
+        __syncthreads();
+    }
+    uint64_t o8 = part[0][tid] - a, o16 = part[1][tid] - c;
+    for (uint32_t q = 0; q < PER; q++) {
+        off8[tid * PER + q] = o8;
+        off16[tid * PER + q] = o16;
+        o8 += tmp[tid * PER + q];
+        o16 += tmp[E + tid * PER + q];
+    }
+    if (tid == 1023) {
+        off8[E] = o8;
+        off16[E] = o16;
+    }
 }
 
 // ------------------------------------------------------------ dictionary
@@ -974,6 +1090,11 @@ void launch_wc_agg(const Tables& t, int mode, int emit, hipStream_t s) {
     if (mode & 512) wc_agg_kernel<128><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
     if (mode & 128) wc_agg_kernel<128><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
     else wc_agg_kernel<0><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
+}
+
+void launch_seg_layout(const Tables& t, uint32_t* tmp, uint64_t* off8, uint64_t* off16, hipStream_t s) {
+    seg_count_kernel<<<kSpillBuckets, kMaxMapWGs, 0, s>>>(t.sp, tmp);
+    seg_scan_kernel<<<1, 1024, 0, s>>>(tmp, off8, off16);
 }
 
 void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s) {

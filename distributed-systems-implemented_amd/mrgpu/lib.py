@@ -68,6 +68,7 @@ class Stats(ctypes.Structure):
         ("dict_ms", ctypes.c_double),
         ("dict_keys", c_uint64),
         ("dict_hits", c_uint64),
+        ("agg_rounds", c_uint64),
     ]
 
     def as_dict(self):

@@ -25,8 +25,10 @@ def main(db_path, out_path):
         # wc_map_kernel / wc_agg_kernel run on the dictionary samples (a few MB)
         # and on the whole split: report the split's launches on their own row so
         # their average is the one bench.py's roofline uses (> 1 ms at C2 sizes)
-        if "wc_map_kernel" in k or "wc_agg_kernel" in k:
+        if "wc_map_kernel" in k:
             k += " [split]" if dur > 1_000_000 else " [dictionary sample]"
+        elif "wc_agg_kernel" in k:  # round 0 of a split vs samples and later (carried-miss) rounds
+            k += " [split round 0]" if dur > 1_000_000 else " [sample / later round]"
         a = agg.setdefault(k, [0, 0.0, float("inf"), 0.0])
         a[0] += 1
         a[1] += dur

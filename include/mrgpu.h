@@ -86,6 +86,7 @@ typedef struct {
     double dict_ms;           /* wc: sample + hot-key dictionary build */
     uint64_t dict_keys;       /* wc: sample keys offered to the dictionary */
     uint64_t dict_hits;       /* wc: occurrences counted by the dictionary in LDS */
+    uint64_t agg_rounds;      /* wc: bucket aggregation rounds run (high-cardinality splits need > 1) */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);

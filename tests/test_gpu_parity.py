@@ -114,12 +114,27 @@ def test_wc_record_buffer_growth(wctx):
         wctx.set_option("rec_cap", 0)
 
 
-def test_wc_bucket_aggregator_overflow(ctx):
-    """More distinct spilled keys per bucket than the aggregator's LDS table holds."""
+@pytest.mark.parametrize("rounds", [0, 1, 2])
+def test_wc_bucket_aggregator_overflow(ctx, rounds):
+    """More distinct spilled keys per bucket than the aggregator's LDS table holds:
+    misses carried through further aggregation rounds (default), counted in the
+    HBM table right away (1 round), or after one carried round (2)."""
     voc = C.Vocab(C.KIND_ASCII, 1.07, 3_000_000, 16)  # every word of a 3M vocabulary at least once
     files = [bytes(voc.fill_files([26_000_000], [16], C.wc_params(vocab_lo=0, vocab_hi=3_000_000))[0])]
-    check(ctx, "wc", files, nreduces=(10,))
-    assert ctx.stats()["agg_miss"] > 0
+    ctx.set_option("agg_rounds", rounds)
+    ctx.set_option("agg_carry_min", 0)  # default: carry every miss
+    try:
+        check(ctx, "wc", files, nreduces=(10,))
+        st = ctx.stats()
+        assert st["agg_miss"] > 0
+        assert st["agg_rounds"] == (rounds if rounds else st["agg_rounds"])
+        if rounds == 0:
+            assert st["agg_rounds"] > 1
+        ctx.set_option("agg_carry_min", 4096)  # buckets with < 4096 misses settle them in HBM
+        check(ctx, "wc", files, nreduces=(10,))
+    finally:
+        ctx.set_option("agg_rounds", 0)
+        ctx.set_option("agg_carry_min", 0)
 
 
 def test_wc_large_vs_oracle(wctx):
