@@ -105,14 +105,36 @@ __device__ __forceinline__ const uint8_t* rec_bytes(const Recs& r, uint32_t j, u
     return tmp16;
 }
 
+// Big-endian 8-byte word of key bytes [pos, pos + 8), zero past the key's end.
+__device__ __forceinline__ uint64_t key_word_be(const uint8_t* p, uint32_t pos, uint32_t len) {
+    uint64_t w = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 8; k++) w |= (pos + k < len ? (uint64_t)p[pos + k] : 0ull) << (56 - 8 * k);
+    return w;
+}
+
+// Bytewise order (worker.go:27, shorter prefix first) by 8-byte words: the
+// first 16 bytes are the records' k0/k1 (zero-padded), the rest come from the
+// arena.  Comparing zero-padded words and then lengths is exactly bytewise order:
+// a word can only differ at a padding position of the shorter key if the longer
+// key has a nonzero byte there, and then the shorter key is the smaller.
 __device__ int rec_cmp(const Recs& r, uint32_t a, uint32_t b) {
-    uint8_t ta[16], tb[16];
-    const uint8_t* pa = rec_bytes(r, a, ta);
-    const uint8_t* pb = rec_bytes(r, b, tb);
-    uint32_t la = r.len[a], lb = r.len[b];
-    uint32_t m = la < lb ? la : lb;
-    for (uint32_t k = 0; k < m; k++)
-        if (pa[k] != pb[k]) return pa[k] < pb[k] ? -1 : 1;
+    const uint64_t a0 = __builtin_bswap64(r.k0[a]), b0 = __builtin_bswap64(r.k0[b]);
+    if (a0 != b0) return a0 < b0 ? -1 : 1;
+    const uint64_t a1 = __builtin_bswap64(r.k1[a]), b1 = __builtin_bswap64(r.k1[b]);
+    if (a1 != b1) return a1 < b1 ? -1 : 1;
+    const uint32_t la = r.len[a], lb = r.len[b];
+    if (la > 16 && lb > 16) {
+        const uint8_t* pa = r.arena + r.koff[a];
+        const uint8_t* pb = r.arena + r.koff[b];
+        const uint32_t mx = la > lb ? la : lb;
+        for (uint32_t pos = 16; pos < mx; pos += 8) {
+            const uint64_t wa = key_word_be(pa, pos, la), wb = key_word_be(pb, pos, lb);
+            if (wa != wb) return wa < wb ? -1 : 1;
+        }
+    }
+    // equal zero-padded words: the shorter key is a prefix of the longer one (if
+    // one key has <= 16 bytes, the other's bytes past it up to 16 are zero)
     return (la > lb) - (la < lb);
 }
 
@@ -164,6 +186,14 @@ __global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_
     }
 }
 
+// Every member of a tied run (lng[i] != 0), for keys whose runs are best
+// merge-sorted as a whole (grep lines: long keys, runs of any length).
+__global__ void mark_all_ties_kernel(const uint8_t* tie, uint64_t n, uint8_t* lng) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        lng[i] = tie[i] | (i + 1 < n ? tie[i + 1] : (uint8_t)0);
+}
+
 // (partition, key) order of two records: the order the whole sort produces.
 struct FullLess {
     Recs r;
@@ -194,6 +224,27 @@ __global__ void line_len_kernel(Recs r, const uint32_t* perm, uint64_t n, int ap
         uint32_t j = perm[i];
         uint64_t len = r.len[j];
         ll[i] = len + 2 + (app == 1 ? ndigits(r.cnt[j]) : len);
+    }
+}
+
+// grep lines ("L L\n"): one wave per line, lanes on consecutive output bytes
+// (coalesced loads and stores).  Key bytes from the arena, or from k0/k1 for a
+// record without arena bytes (<= 16 bytes).
+__global__ void write_lines_wave_kernel(Recs r, const uint32_t* perm, uint64_t n, const uint64_t* off, uint8_t* out) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
+    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nw) {
+        const uint32_t j = perm[i];
+        const uint32_t len = r.len[j];
+        const uint64_t ko = r.koff[j], k0 = r.k0[j], k1 = r.k1[j];
+        const uint8_t* kb = r.arena + (ko == ~0ull ? 0 : ko);
+        uint8_t* o = out + off[i];
+        for (uint32_t k = lane; k < 2 * len + 2; k += 64) {
+            const uint32_t src = k < len ? k : k - len - 1;
+            const uint8_t b = k == len || k == 2 * len + 1 ? (uint8_t)0
+                              : ko != ~0ull ? kb[src] : (uint8_t)((src < 8 ? k0 : k1) >> (8 * (src & 7)));
+            o[k] = k == len ? (uint8_t)' ' : k == 2 * len + 1 ? (uint8_t)'\n' : b;
+        }
     }
 }
 
@@ -414,12 +465,19 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     // run); longer ones are marked.  Returns whether any run was long; with
     // `merge`, the long runs are then merge-sorted by full comparison.
     constexpr uint64_t kMaxRun = 64;
-    auto fix_ties = [&](bool with_k1, bool merge, bool* any_long) -> int {
+    auto fix_ties = [&](bool with_k1, bool merge, bool* any_long, bool all_runs = false) -> int {
         uint8_t* tie = ws->key_a.as<uint8_t>();
         uint8_t* lng = tie + n;
         RCHK(hipMemsetAsync(lng, 0, n, s));
-        RCHK(hipMemsetAsync(flags + 3, 0, 8, s));
+        RCHK(hipMemsetAsync(flags + 2, 0, 16, s));
         mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1);
+        if (all_runs) {  // every tied run goes to the merge sort (no per-run insertion sort)
+            mark_all_ties_kernel<<<grid_for(n), 256, 0, s>>>(tie, n, lng);
+            RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 2, 8, hipMemcpyDeviceToHost, s));
+            RCHK(hipStreamSynchronize(s));
+            *any_long = ws->h_pinned[3] != 0;
+            return *any_long ? sort_long_runs(ws, r, pa, n, lng, s) : 0;
+        }
         fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, kMaxRun, flags, lng);
         RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 3, 8, hipMemcpyDeviceToHost, s));
         RCHK(hipStreamSynchronize(s));
@@ -428,8 +486,14 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         return 0;
     };
     int e;
-    if ((e = sort_all(false))) return e;
-    if (has_k1 || has_long || app != 1) {
+    // grep keys are whole lines (> 16 bytes, often sharing their first words):
+    // sort with the k1 pass from the start
+    const bool k1_first = has_long && app != 1;
+    if ((e = sort_all(k1_first))) return e;
+    if (k1_first) {
+        bool any_long = false;
+        if ((e = fix_ties(true, true, &any_long, true))) return e;
+    } else if (has_k1 || has_long || app != 1) {
         // keys of 9-16 bytes sharing an 8-byte prefix in a long run: sort again with
         // the k1 pass (cheaper than a comparison sort); any other long run (keys
         // > 16 bytes, grep lines): comparison merge sort of the run members
@@ -453,7 +517,10 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     const uint64_t total = ws->h_pinned[0] + ws->h_pinned[1];
     RCHK(ws->out.ensure(total + 16));
     uint8_t* out = ws->out.as<uint8_t>();
-    write_lines_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, app, off, out);
+    if (app != 1)
+        write_lines_wave_kernel<<<2048, 256, 0, s>>>(r, pa, n, off, out);
+    else
+        write_lines_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, app, off, out);
     if (all) {
         RCHK(ws->offs.ensure((size_t)(nparts + 1) * 8));
         part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, total, nparts, ws->offs.as<uint64_t>());
