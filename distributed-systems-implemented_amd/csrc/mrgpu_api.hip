@@ -133,7 +133,11 @@ constexpr uint64_t kHostMagic = 0x4D524748424F5354ull;  // "MRGHBOST"
 
 }  // namespace
 
+struct ExchSide;
+static void exch_free(ExchSide* x);
+
 struct mrg_ctx {
+    ExchSide* exch = nullptr;  // RCCL shuffle buffers, kept across calls (no hipMalloc / hipFree per step)
     int device = 0;
     hipStream_t s = nullptr;
     hipEvent_t ev[12] = {};  // 0-3, 8-10: map phases; 4-5 reduce; 6-7 exchange / d2h
@@ -718,6 +722,7 @@ void mrg_close(mrg_ctx* c) {
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
     if (c->s) hipStreamDestroy(c->s);
+    exch_free(c->exch);
     delete c;
 }
 
@@ -1164,7 +1169,7 @@ struct ExchSide {
     DevBuf scratch, sbuf, sar_b, rbuf, rar_b, rmeta;
     std::vector<unsigned long long> snd, rcv;
     ExchPlan plan;
-    unsigned long long* d_cnt(int P) { return (unsigned long long*)scratch.p; }
+    unsigned long long* d_cnt(int) { return (unsigned long long*)scratch.p; }
     unsigned long long* d_rcv(int P) { return d_cnt(P) + 2 * P; }
     unsigned long long* d_cur(int P) { return d_cnt(P) + 4 * P; }
     uint64_t* d_base(int P) { return (uint64_t*)(d_cnt(P) + 6 * P); }
@@ -1184,10 +1189,10 @@ static int exch_count(mrg_ctx* c, const Recs& r, int P, ExchSide& x) {
 // per-owner segments.  Step 3 is the transport (RCCL or in-process copies).
 static int exch_pack(mrg_ctx* c, const Recs& r, int P, ExchSide& x) {
     x.plan = exch_plan(P, x.snd.data(), x.rcv.data());
-    HCHK(c, x.sbuf.ensure(x.plan.srec * sizeof(WireRec) + 64));
-    HCHK(c, x.rbuf.ensure(x.plan.rrec * sizeof(WireRec) + 64));
-    HCHK(c, x.sar_b.ensure(x.plan.sar + 64));
-    HCHK(c, x.rar_b.ensure(x.plan.rar + 64));
+    HCHK(c, x.sbuf.ensure_grow(x.plan.srec * sizeof(WireRec) + 64));
+    HCHK(c, x.rbuf.ensure_grow(x.plan.rrec * sizeof(WireRec) + 64));
+    HCHK(c, x.sar_b.ensure_grow(x.plan.sar + 64));
+    HCHK(c, x.rar_b.ensure_cached(x.plan.rar + 64, c->device));  // handed to the received parts object
     HCHK(c, hipMemcpyAsync(x.d_base(P), x.plan.hbase.data(), 16 * P, hipMemcpyHostToDevice, c->s));
     if (r.n)
         pack_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, x.d_base(P), x.d_base(P) + P, x.d_cur(P),
@@ -1217,11 +1222,12 @@ static int exch_finish(mrg_ctx* c, const mrg_parts* local, int P, ExchSide& x, m
     rc = aggregate(c, {tmp->r}, local->app, local->nreduce, owned);
     hipError_t e = hipStreamSynchronize(c->s);
     mrg_parts_free(tmp);
-    x.sbuf.release(); x.rbuf.release(); x.sar_b.release(); x.rmeta.release(); x.scratch.release();
     if (rc) return rc;
     HCHK(c, e);
     return MRG_OK;
 }
+
+static void exch_free(ExchSide* x) { delete x; }
 
 int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     if (!c || !local || !owned) return MRG_EINVAL;
@@ -1233,7 +1239,8 @@ int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     }
     HCHK(c, hipEventRecord(c->ev[6], c->s));
     const Recs& r = local->r;
-    ExchSide x;
+    if (!c->exch) c->exch = new ExchSide();
+    ExchSide& x = *c->exch;
     if ((rc = exch_count(c, r, P, x))) return rc;
     NCHK(c, ncclAllToAll(x.d_cnt(P), x.d_rcv(P), 2, ncclUint64, c->comm, c->s));
     x.snd.assign(2 * P, 0);
