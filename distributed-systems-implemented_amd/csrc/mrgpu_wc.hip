@@ -533,9 +533,12 @@ __device__ __forceinline__ void short_set_masks(const AggLds& A, uint32_t base, 
 // retried once (the winner, often the same key, published it with its CAS).
 // Returns false (a miss: the caller defers the key, where it is still counted
 // exactly) when both sets are full without the key or claims keep racing.
-__device__ bool short_insert_slow(AggLds& A, uint64_t k, uint32_t h, uint32_t add) {
+// first_full: the caller's read of the first set found it full without the key
+// (ways are never freed, so it still is): start at the second set.
+__device__ bool short_insert_slow(AggLds& A, uint64_t k, uint32_t h, uint32_t add, bool first_full) {
     for (int attempt = 0; attempt < 2; attempt++) {
-        for (int c = 0; c < 2; c++) {
+        bool raced = false;
+        for (int c = first_full ? 1 : 0; c < 2 && !raced; c++) {
             const uint32_t base = set_base<kAggShortSets>(c == 0 ? h : second_hash(h));
             uint32_t m, z;
             short_set_masks(A, base, k, m, z);
@@ -550,10 +553,11 @@ __device__ bool short_insert_slow(AggLds& A, uint64_t k, uint32_t h, uint32_t ad
                     atomicAdd(&A.sc[w], add);
                     return true;
                 }
-                break;  // lost the way to another key: re-read from the first set
+                raced = true;  // lost the way to another key: re-read from the first set
             }
             // set full without the key: the second set (after the first)
         }
+        if (!raced) return false;  // both sets full without the key: a retry reads the same
     }
     return false;
 }
@@ -573,7 +577,8 @@ __device__ __forceinline__ void mid_set_masks(const AggLds& A, uint32_t base, ui
 
 __device__ bool mid_insert(AggLds& A, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
     for (int attempt = 0; attempt < 2; attempt++) {
-        for (int c = 0; c < 2; c++) {
+        bool raced = false;
+        for (int c = 0; c < 2 && !raced; c++) {
             const uint32_t base = set_base<kAggMidSets>(c == 0 ? h : second_hash(h));
             uint32_t m, z, pend;
             mid_set_masks(A, base, k0, k1, m, z, pend);
@@ -581,7 +586,10 @@ __device__ bool mid_insert(AggLds& A, uint64_t k0, uint64_t k1, uint32_t h, uint
                 atomicAdd(&A.mc[base + __builtin_ctz(m)], add);
                 return true;
             }
-            if (pend) break;  // a way of this k0 is being published: retry (or defer)
+            if (pend) {  // a way of this k0 is being published: retry (or defer)
+                raced = true;
+                continue;
+            }
             if (z) {
                 const uint32_t w = base + __builtin_ctz(z);
                 if (atomicCAS(&A.mk[2 * w], 0ull, (unsigned long long)k0) == 0ull) {
@@ -589,9 +597,10 @@ __device__ bool mid_insert(AggLds& A, uint64_t k0, uint64_t k1, uint32_t h, uint
                     atomicAdd(&A.mc[w], add);
                     return true;
                 }
-                break;
+                raced = true;
             }
         }
+        if (!raced) return false;  // both sets full without the key
     }
     return false;
 }
@@ -732,7 +741,7 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
             for (uint32_t u = 0; u < kAggUnroll; u++) {
                 if (slow[u]) {
                     const uint64_t k = ((uint64_t)cur[u].y << 32) | cur[u].x;
-                    if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
+                    if (!short_insert_slow(A, k, h[u], 1, z[u] == 0)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
                 }
             }
         } else {
