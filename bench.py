@@ -256,6 +256,7 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     log("map kernel ms per timed step: " + " ".join(f"{k:.2f}" for k in kern_ms))
+    log("aggregation ms per timed step: " + " ".join(f"{st['agg_ms']:.2f}" for st in stats))
 
     t_max = elapsed
     if world > 1:

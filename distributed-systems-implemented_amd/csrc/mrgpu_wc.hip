@@ -533,12 +533,12 @@ __device__ __forceinline__ void short_set_masks(const AggLds& A, uint32_t base, 
 // retried once (the winner, often the same key, published it with its CAS).
 // Returns false (a miss: the caller defers the key, where it is still counted
 // exactly) when both sets are full without the key or claims keep racing.
-// first_full: the caller's read of the first set found it full without the key
-// (ways are never freed, so it still is): start at the second set.
-__device__ bool short_insert_slow(AggLds& A, uint64_t k, uint32_t h, uint32_t add, bool first_full) {
+// (Measured: passing the caller's "first set full" to start at the second set
+// made C5's aggregation 51 -> 79 ms, a code-generation effect; not done.)
+__device__ bool short_insert_slow(AggLds& A, uint64_t k, uint32_t h, uint32_t add) {
     for (int attempt = 0; attempt < 2; attempt++) {
         bool raced = false;
-        for (int c = first_full ? 1 : 0; c < 2 && !raced; c++) {
+        for (int c = 0; c < 2 && !raced; c++) {
             const uint32_t base = set_base<kAggShortSets>(c == 0 ? h : second_hash(h));
             uint32_t m, z;
             short_set_masks(A, base, k, m, z);
@@ -741,7 +741,7 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
             for (uint32_t u = 0; u < kAggUnroll; u++) {
                 if (slow[u]) {
                     const uint64_t k = ((uint64_t)cur[u].y << 32) | cur[u].x;
-                    if (!short_insert_slow(A, k, h[u], 1, z[u] == 0)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
+                    if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
                 }
             }
         } else {
