@@ -147,6 +147,7 @@ struct mrg_ctx {
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
     DevBuf bflag, dict, dict_cnt, sample, recbuf, recarena, sortbuf, dbg;
     DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
+    DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     int agg_rounds = 8;                 // bucket aggregation rounds at most (the last sends leftovers to HBM)
     // Misses per bucket below which a round settles them in the HBM table instead
     // of carrying them.  0 (default): always carry.  Measured on C5: 4096 made
@@ -980,6 +981,197 @@ int mrg_parts_export(mrg_ctx* c, const mrg_parts* p, uint32_t r, void** bytes, s
     if ((rc = select_recs(c->rws, p->r, p->nreduce, r, &d, c->s))) { mrg_parts_free(sel); return fail(c, MRG_EDEVICE, "select failed"); }
     rc = parts_to_host(c, d, p->app, p->nreduce, r, bytes, nb);  // arena shared with p (whole arena exported)
     mrg_parts_free(sel);
+    return rc;
+}
+
+// ---- reference-format intermediate files (mr/worker.go:80-92 / :100-122) ----
+static void* json_grow(void* ctx, size_t n) {
+    mrg_ctx* c = (mrg_ctx*)ctx;
+    return c->jtmp.ensure_grow(n) == hipSuccess ? c->jtmp.p : nullptr;
+}
+
+int mrg_parts_export_json(mrg_ctx* c, const mrg_parts* p, uint32_t r, void** bytes, size_t* nb) {
+    if (!c || !p || !bytes || !nb) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    if (r != 0xFFFFFFFFu && r >= p->nreduce) return fail(c, MRG_EINVAL, "export_json: partition %u >= nreduce %u", r, p->nreduce);
+    mrg_parts* sel = nullptr;
+    Recs src = p->r;
+    if (r != 0xFFFFFFFFu) {
+        if ((rc = parts_alloc(c, p->r.n, 0, p->app, p->nreduce, &sel))) return rc;
+        Recs d = sel->r;
+        if (select_recs(c->rws, p->r, p->nreduce, r, &d, c->s)) { mrg_parts_free(sel); return fail(c, MRG_EDEVICE, "select failed"); }
+        src = d;
+    }
+    const uint64_t n = src.n;
+    uint64_t total = 0;
+    uint8_t* h = nullptr;
+    if (n) {
+        hipError_t e = c->jmeta.ensure_grow(n * 6 * 8 + 64);
+        if (e != hipSuccess) { mrg_parts_free(sel); return fail(c, MRG_ENOMEM, "export_json: scratch"); }
+        uint64_t* L = (uint64_t*)c->jmeta.p;
+        uint64_t *T = L + n, *P = T + n, *loff = P + n, *toff = loff + n, *poff = toff + n;
+        if (json_lengths(src, p->app, L, T, P, loff, toff, poff, json_grow, c, c->s)) {
+            mrg_parts_free(sel);
+            return fail(c, MRG_EDEVICE, "export_json: lengths");
+        }
+        uint64_t* hs = c->h_scr;  // last entries of the three scans and of L, T, P
+        const uint64_t* src6[6] = {loff + n - 1, L + n - 1, toff + n - 1, T + n - 1, poff + n - 1, P + n - 1};
+        for (int i = 0; i < 6; i++) HCHK(c, hipMemcpyAsync(&hs[i], src6[i], 8, hipMemcpyDeviceToHost, c->s));
+        HCHK(c, hipStreamSynchronize(c->s));
+        const uint64_t nlines = hs[0] + hs[1];
+        total = hs[2] + hs[3];
+        const uint64_t npieces = hs[4] + hs[5];
+        if (c->jlines.ensure_grow(nlines + 64) != hipSuccess || c->jout.ensure_grow(total + 64) != hipSuccess) {
+            mrg_parts_free(sel);
+            return fail(c, MRG_ENOMEM, "export_json: %llu output bytes", (unsigned long long)total);
+        }
+        if (json_write(src, p->app, L, loff, toff, poff, npieces, total, (uint8_t*)c->jlines.p, (uint8_t*)c->jout.p, c->s)) {
+            mrg_parts_free(sel);
+            return fail(c, MRG_EDEVICE, "export_json: write");
+        }
+    }
+    h = (uint8_t*)host_result(total);
+    if (!h) { mrg_parts_free(sel); return fail(c, MRG_ENOMEM, "host alloc %llu", (unsigned long long)total); }
+    hipError_t e = total ? hipMemcpyAsync(h, c->jout.p, total, hipMemcpyDeviceToHost, c->s) : hipSuccess;
+    if (e == hipSuccess) e = hipStreamSynchronize(c->s);
+    mrg_parts_free(sel);
+    if (e != hipSuccess) { mrg_free(h); return fail(c, MRG_EDEVICE, "export_json copy: %s", hipGetErrorString(e)); }
+    *bytes = h;
+    *nb = total;
+    return MRG_OK;
+}
+
+// One JSON string at s[i] (after its opening quote) -> raw bytes, as Go's
+// decoder unquotes it (encoding/json unquoteBytes): \uXXXX with UTF-16
+// surrogate pairs, a lone surrogate -> U+FFFD.  Returns the index after the
+// closing quote, or 0 on malformed input.
+static size_t json_unquote(const uint8_t* s, size_t i, size_t n, std::string& out) {
+    auto hex4 = [&](size_t at, uint32_t* v) -> bool {
+        if (at + 4 > n) return false;
+        uint32_t x = 0;
+        for (size_t k = at; k < at + 4; k++) {
+            const uint8_t ch = s[k];
+            x <<= 4;
+            if (ch >= '0' && ch <= '9') x |= ch - '0';
+            else if (ch >= 'a' && ch <= 'f') x |= ch - 'a' + 10;
+            else if (ch >= 'A' && ch <= 'F') x |= ch - 'A' + 10;
+            else return false;
+        }
+        *v = x;
+        return true;
+    };
+    auto put = [&](uint32_t cp) {
+        if (cp < 0x80) out.push_back((char)cp);
+        else if (cp < 0x800) { out.push_back((char)(0xC0 | (cp >> 6))); out.push_back((char)(0x80 | (cp & 63))); }
+        else if (cp < 0x10000) {
+            out.push_back((char)(0xE0 | (cp >> 12)));
+            out.push_back((char)(0x80 | ((cp >> 6) & 63)));
+            out.push_back((char)(0x80 | (cp & 63)));
+        } else {
+            out.push_back((char)(0xF0 | (cp >> 18)));
+            out.push_back((char)(0x80 | ((cp >> 12) & 63)));
+            out.push_back((char)(0x80 | ((cp >> 6) & 63)));
+            out.push_back((char)(0x80 | (cp & 63)));
+        }
+    };
+    while (i < n) {
+        const uint8_t ch = s[i];
+        if (ch == '"') return i + 1;
+        if (ch != '\\') { out.push_back((char)ch); i++; continue; }
+        if (i + 1 >= n) return 0;
+        const uint8_t e = s[i + 1];
+        i += 2;
+        switch (e) {
+            case '"': case '\\': case '/': out.push_back((char)e); break;
+            case 'b': out.push_back('\b'); break;
+            case 'f': out.push_back('\f'); break;
+            case 'n': out.push_back('\n'); break;
+            case 'r': out.push_back('\r'); break;
+            case 't': out.push_back('\t'); break;
+            case 'u': {
+                uint32_t v;
+                if (!hex4(i, &v)) return 0;
+                i += 4;
+                if (v >= 0xD800 && v < 0xDC00) {  // high surrogate: a low one must follow
+                    uint32_t lo;
+                    if (i + 6 <= n && s[i] == '\\' && s[i + 1] == 'u' && hex4(i + 2, &lo) && lo >= 0xDC00 && lo < 0xE000) {
+                        i += 6;
+                        v = 0x10000 + ((v - 0xD800) << 10) + (lo - 0xDC00);
+                    } else {
+                        v = 0xFFFD;
+                    }
+                } else if (v >= 0xDC00 && v < 0xE000) {
+                    v = 0xFFFD;
+                }
+                put(v);
+                break;
+            }
+            default: return 0;
+        }
+    }
+    return 0;
+}
+
+int mrg_parts_import_json(mrg_ctx* c, int app, uint32_t nreduce, const void* bytes, size_t nb, mrg_parts** out) {
+    if (!c || !out || (nb && !bytes)) return MRG_EINVAL;
+    if ((app != MRG_APP_WC && app != MRG_APP_GREP) || nreduce == 0) return fail(c, MRG_EINVAL, "import_json: app / nreduce");
+    // Decode the lines on the host (the format is text with escapes), one record
+    // per line with count 1, then count equal keys on the GPU (aggregate()).
+    const uint8_t* s = (const uint8_t*)bytes;
+    static const char kHead[] = "{\"Key\":\"";
+    static const char kMid[] = ",\"Value\":\"";
+    std::vector<uint64_t> k0, k1, koff, cnt;
+    std::vector<uint32_t> len, part;
+    std::string arena, key, val;
+    size_t i = 0;
+    while (i < nb) {
+        if (nb - i < sizeof(kHead) - 1 || memcmp(s + i, kHead, sizeof(kHead) - 1)) return fail(c, MRG_EFORMAT, "import_json: line at byte %zu", i);
+        key.clear();
+        val.clear();
+        size_t j = json_unquote(s, i + sizeof(kHead) - 1, nb, key);
+        if (!j || nb - j < sizeof(kMid) - 1 || memcmp(s + j, kMid, sizeof(kMid) - 1)) return fail(c, MRG_EFORMAT, "import_json: key at byte %zu", i);
+        j = json_unquote(s, j + sizeof(kMid) - 1, nb, val);
+        if (!j || j + 2 > nb || s[j] != '}' || s[j + 1] != '\n') return fail(c, MRG_EFORMAT, "import_json: value at byte %zu", i);
+        i = j + 2;
+        if (key.size() > 0xFFFFFFFFu) return fail(c, MRG_EFORMAT, "import_json: key too long");
+        uint64_t a = 0, b = 0;
+        for (size_t q = 0; q < key.size() && q < 16; q++)
+            (q < 8 ? a : b) |= (uint64_t)(uint8_t)key[q] << (8 * (q & 7));
+        k0.push_back(a);
+        k1.push_back(b);
+        cnt.push_back(1);  // Reduce sees one value per line (worker.go:129-140)
+        len.push_back((uint32_t)key.size());
+        uint32_t h = 2166136261u;
+        for (char ch : key) h = fnv1a32_step(h, (uint8_t)ch);
+        part.push_back((h & 0x7fffffffu) % nreduce);
+        if (key.size() > 16) {
+            koff.push_back(arena.size());
+            arena += key;
+        } else {
+            koff.push_back(~0ull);
+        }
+    }
+    int rc;
+    if ((rc = bind(c))) return rc;
+    const uint64_t n = k0.size();
+    mrg_parts* raw = nullptr;
+    if ((rc = parts_alloc(c, n, arena.size(), app, nreduce, &raw))) return rc;
+    hipError_t e = hipSuccess;
+    auto cp = [&](void* d, const void* h, size_t b) {
+        if (e == hipSuccess && b) e = hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, c->s);
+    };
+    cp(raw->r.k0, k0.data(), n * 8);
+    cp(raw->r.k1, k1.data(), n * 8);
+    cp(raw->r.cnt, cnt.data(), n * 8);
+    cp(raw->r.koff, koff.data(), n * 8);
+    cp(raw->r.len, len.data(), n * 4);
+    cp(raw->r.part, part.data(), n * 4);
+    cp(raw->r.arena, arena.data(), arena.size());
+    if (e == hipSuccess) e = hipStreamSynchronize(c->s);  // the host vectors go out of scope
+    if (e != hipSuccess) { mrg_parts_free(raw); return fail(c, MRG_EDEVICE, "import_json copy: %s", hipGetErrorString(e)); }
+    rc = aggregate(c, {raw->r}, app, nreduce, out);
+    mrg_parts_free(raw);
     return rc;
 }
 

@@ -195,6 +195,16 @@ int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64
 // Stable radix sort of (u32 key, u32 value) pairs; result in k_out / v_out.
 int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, uint64_t n,
                    unsigned bits, hipStream_t s);
+// ---- reference JSON-lines intermediate format (mrgpu_json.hip) ----
+// Per record: L = escaped {"Key":..,"Value":..}\n line bytes, T = L * count,
+// P = 4 KiB output pieces; loff / toff / poff their exclusive scans.  grow(gctx, n)
+// returns >= n bytes of device scratch.  Returns 0 or -1.
+int json_lengths(const Recs& r, int app, uint64_t* L, uint64_t* T, uint64_t* P, uint64_t* loff, uint64_t* toff,
+                 uint64_t* poff, void* (*grow)(void*, size_t), void* gctx, hipStream_t s);
+// Escaped lines into `lines` (at loff), then the output (total bytes) with each
+// record's line repeated count times.
+int json_write(const Recs& r, int app, const uint64_t* L, const uint64_t* loff, const uint64_t* toff,
+               const uint64_t* poff, uint64_t npieces, uint64_t total, uint8_t* lines, uint8_t* out, hipStream_t s);
 // Compact recs with part == p (or owner rank) into dst (device), returns count on host.
 int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst_host_desc, hipStream_t s);
 

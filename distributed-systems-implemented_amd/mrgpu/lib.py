@@ -36,7 +36,8 @@ ALL_PARTS = 0xFFFFFFFF
 # every symbol declared in include/mrgpu.h (checked by tests/test_abi.py)
 EXPORTED = [
     "mrg_open", "mrg_close", "mrg_last_error", "mrg_device_count", "mrg_map", "mrg_parts_merge",
-    "mrg_parts_info", "mrg_parts_export", "mrg_parts_import", "mrg_parts_free", "mrg_reduce",
+    "mrg_parts_info", "mrg_parts_export", "mrg_parts_import",
+    "mrg_parts_export_json", "mrg_parts_import_json", "mrg_parts_free", "mrg_reduce",
     "mrg_reduce_all", "mrg_run_job", "mrg_comm_unique_id", "mrg_comm_init", "mrg_exchange",
     "mrg_exchange_group",
     "mrg_device_alloc", "mrg_device_free", "mrg_memcpy_h2d", "mrg_memcpy_d2h", "mrg_sync",
@@ -100,6 +101,8 @@ def load_library(path: str | None = None):
     L.mrg_parts_info.argtypes = [vp, POINTER(c_uint64), POINTER(c_uint32), POINTER(c_int)]
     L.mrg_parts_export.argtypes = [vp, vp, c_uint32, POINTER(vp), POINTER(c_size_t)]
     L.mrg_parts_import.argtypes = [vp, vp, c_size_t, POINTER(vp)]
+    L.mrg_parts_export_json.argtypes = [vp, vp, c_uint32, POINTER(vp), POINTER(c_size_t)]
+    L.mrg_parts_import_json.argtypes = [vp, c_int, c_uint32, vp, c_size_t, POINTER(vp)]
     L.mrg_parts_free.argtypes = [vp]
     L.mrg_parts_free.restype = None
     L.mrg_reduce.argtypes = [vp, vp, c_uint32, POINTER(vp), POINTER(c_size_t)]
@@ -249,6 +252,19 @@ class Context:
         out = c_void_p()
         p, _keep = _buf(data)
         self._check(self.L.mrg_parts_import(self.h, p, len(data), byref(out)), "mrg_parts_import")
+        return Parts(self, out)
+
+    def export_json(self, parts: Parts, r: int = ALL_PARTS) -> bytes:
+        """mr-X-r in the reference's format (mr/worker.go:80-92): a JSON line per occurrence."""
+        p, n = c_void_p(), c_size_t()
+        self._check(self.L.mrg_parts_export_json(self.h, parts.h, r, byref(p), byref(n)), "mrg_parts_export_json")
+        return self._take(p, n.value)
+
+    def import_json(self, app: int, nreduce: int, data: bytes) -> Parts:
+        """mr-X-Y JSON lines written by reference workers -> parts (equal keys counted)."""
+        out = c_void_p()
+        p, _keep = _buf(data) if data else (None, None)
+        self._check(self.L.mrg_parts_import_json(self.h, app, nreduce, p, len(data), byref(out)), "mrg_parts_import_json")
         return Parts(self, out)
 
     def reduce(self, parts: Parts, r: int) -> bytes:

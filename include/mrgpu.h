@@ -107,6 +107,15 @@ int mrg_parts_info(const mrg_parts* p, uint64_t* nkeys, uint32_t* nreduce, int* 
 int mrg_parts_export(mrg_ctx* ctx, const mrg_parts* p, uint32_t r, void** bytes, size_t* n);
 int mrg_parts_import(mrg_ctx* ctx, const void* bytes, size_t n, mrg_parts** out);
 void mrg_parts_free(mrg_parts* p);
+/* The reference's own intermediate format, for mixed clusters of GPU and
+ * reference workers.  export_json: partition r (UINT32_MAX: all) as the exact
+ * bytes mr/worker.go:80-92 writes to mr-X-r — one json.Encoder line
+ * {"Key":k,"Value":"1"} (wc) / {"Key":k,"Value":""} (grep) per occurrence, so a
+ * record of count c is c lines (Go 1.16-1.21 escaping); library-owned host bytes.
+ * import_json: mr-X-Y bytes written by reference workers (worker.go:100-122
+ * reads them) -> parts with equal keys counted (one value per line). */
+int mrg_parts_export_json(mrg_ctx* ctx, const mrg_parts* p, uint32_t r, void** bytes, size_t* n);
+int mrg_parts_import_json(mrg_ctx* ctx, int app, uint32_t nreduce, const void* bytes, size_t n, mrg_parts** out);
 
 /* Reduce partition r: exact mr-out-r bytes (library-owned host buffer). */
 int mrg_reduce(mrg_ctx* ctx, const mrg_parts* p, uint32_t r, void** bytes, size_t* n);

@@ -194,3 +194,57 @@ def mr_partitioned(app: str, files: list[bytes], nreduce: int) -> list[bytes]:
         for key in mapf(f"file{k}", data):
             buckets[ihash(key) % nreduce].append(key)
     return [_group_reduce(b, reducef) for b in buckets]
+
+
+# ---------------------------------------------------------------- intermediate files
+def go_json_string(s: bytes) -> bytes:
+    """encoding/json ``encodeState.string(s, escapeHTML=true)`` (json.Encoder's
+    default), Go 1.16-1.21: the encoding of a KeyValue string in mr-X-Y
+    (worker.go:84-86).  '"' and '\\' get a backslash, \\n \\r \\t their short
+    forms, other bytes < 0x20 and '<' '>' '&' become \\u00XX; a byte that
+    decodes to RuneError of width 1 becomes \\ufffd; U+2028 / U+2029 become
+    \\u2028 / \\u2029; everything else is copied.  (Go 1.22 added \\b and \\f.)"""
+    out = bytearray(b'"')
+    i, n = 0, len(s)
+    while i < n:
+        b = s[i]
+        if b < 0x80:
+            if b >= 0x20 and b not in b'"\\<>&':
+                out.append(b)
+            elif b in b'"\\':
+                out += b"\\" + bytes([b])
+            elif b == 0x0A:
+                out += b"\\n"
+            elif b == 0x0D:
+                out += b"\\r"
+            elif b == 0x09:
+                out += b"\\t"
+            else:
+                out += b"\\u00" + b"%02x" % b
+            i += 1
+            continue
+        cp, w = decode_rune(s, i)
+        if cp == RUNE_ERROR and w == 1:
+            out += b"\\ufffd"
+        elif cp in (0x2028, 0x2029):
+            out += b"\\u%04x" % cp
+        else:
+            out += s[i:i + w]
+        i += w
+    out += b'"'
+    return bytes(out)
+
+
+def go_json_kv_line(key: bytes, value: bytes) -> bytes:
+    """One ``json.NewEncoder(f).Encode(&kv)`` line (worker.go:84-86)."""
+    return b'{"Key":' + go_json_string(key) + b',"Value":' + go_json_string(value) + b"}\n"
+
+
+def intermediate_json_lines(app: str, files: list[bytes], nreduce: int, r: int) -> list[bytes]:
+    """The lines a reference map worker writes to mr-X-r for these inputs
+    (worker.go:69-92): one per emitted KeyValue of bucket r, in emission order."""
+    mapf, _ = _map_reduce_fns(app)
+    value = b"1" if app == "wc" else b""
+    return [go_json_kv_line(key, value)
+            for k, data in enumerate(files) for key in mapf(f"file{k}", data)
+            if ihash(key) % nreduce == r]

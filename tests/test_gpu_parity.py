@@ -249,3 +249,66 @@ def test_export_matches_host_codec(ctx):
     want = collections.Counter(O.mr_oracle.wc_map(files[0]))
     assert dict(zip(d["keys"], (int(c) for c in d["count"]))) == dict(want)
     assert all(int(pp) == O.c_ihash(k) % 7 for k, pp in zip(d["keys"], d["kpart"]))
+
+
+JSON_GREP_LINES = (b'plain distributed line\n'
+                   b'quote " and backslash \\ distributed <b>&amp;</b>\n'
+                   b'ctrl \x01\x08\x0c\t\r distributed\n'
+                   + "unicode distributed \u00e9\u4e2d\U0001F600 \u2028 \u2029 x\n".encode()
+                   + b'invalid \xff\xe2\x80 distributed\n'
+                   + b'distributed\n' * 3 + b'short distributed\n' * 2)
+
+
+@pytest.mark.parametrize("app", ["wc", "grep:distributed"])
+def test_export_json_matches_reference_format(ctx, app):
+    """mrg_parts_export_json: the lines mr/worker.go:80-92 writes to mr-X-r (one per
+    occurrence, Go's json.Encoder escaping), as a multiset, for every partition."""
+    import mr_oracle as M
+    if app == "wc":
+        files = cases.synthetic(C.KIND_UTF8, 3000, [60_000], 31, 0.002)
+        files.append(b"Zzzzzzzzzzzzzzzzzzzzzz " * 3 + b"\n")
+    else:
+        files = [JSON_GREP_LINES * 3]
+    a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
+    pat = b"" if app == "wc" else app[5:].encode()
+    R = 7
+    p = ctx.map(a, b"\n".join(files), pattern=pat, nreduce=R)
+    allj = []
+    for r in range(R):
+        got = ctx.export_json(p, r)
+        want = M.intermediate_json_lines(app, files, R, r)
+        assert sorted(got.splitlines(keepends=True)) == sorted(want), f"partition {r}"
+        allj.append(got)
+    assert sorted(ctx.export_json(p).splitlines(keepends=True)) == sorted(
+        l for r in range(R) for l in M.intermediate_json_lines(app, files, R, r))
+    p.free()
+
+
+@pytest.mark.parametrize("app", ["wc", "grep:distributed"])
+def test_import_json_reference_intermediates(ctx, app):
+    """mrg_parts_import_json over mr-X-Y files as reference map workers write them
+    (oracle encoder), then the GPU reduce: mr-out-r equals the reference's reduce
+    of the decoded keys (worker.go:100-146; invalid UTF-8 in a grep line comes back
+    as U+FFFD, the reference's own JSON round trip)."""
+    import json
+
+    import mr_oracle as M
+    if app == "wc":
+        files = cases.synthetic(C.KIND_UTF8, 3000, [50_000, 30_000], 32, 0.002)
+    else:
+        files = [JSON_GREP_LINES * 2, JSON_GREP_LINES]
+    a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
+    R = 5
+    _, reducef = M._map_reduce_fns(app)
+    for r in range(R):
+        data = b"".join(l for f in files for l in M.intermediate_json_lines(app, [f], R, r)[::-1])  # any line order
+        parts = ctx.import_json(a, R, data)
+        keys = [json.loads(l)["Key"].encode("utf-8") for l in data.splitlines()]
+        want = M._group_reduce([k for k in keys if M.ihash(k) % R == r], reducef)
+        assert ctx.reduce(parts, r) == want, f"partition {r}"
+        parts.free()
+    empty = ctx.import_json(a, R, b"")
+    assert ctx.reduce(empty, 0) == b""
+    empty.free()
+    with pytest.raises(Exception):
+        ctx.import_json(a, R, b'{"Key":"x"}\n')

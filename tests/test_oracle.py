@@ -140,3 +140,35 @@ def test_c_decoder_matches_python():
     rnd = random.Random(99)
     data = bytes(rnd.randrange(256) for _ in range(200000))
     assert O.c_mrsequential("wc", [data]) == M.mrsequential("wc", [data])
+
+
+# encoding/json string encoding of mr-X-Y lines (worker.go:84-86), Go 1.16-1.21
+JSON_KAT = [
+    (b"the", b'"the"'),
+    (b"<a&b>", b'"\\u003ca\\u0026b\\u003e"'),
+    (b'a"b\\c', b'"a\\"b\\\\c"'),
+    (b"\n\r\t\x08\x0c\x01\x1f", b'"\\n\\r\\t\\u0008\\u000c\\u0001\\u001f"'),
+    (b"\x7f/", b'"\x7f/"'),
+    (b"\xff", b'"\\ufffd"'),
+    (b"\xe2\x80", b'"\\ufffd\\ufffd"'),               # truncated sequence: RuneError per byte
+    ("\u2028\u2029".encode(), b'"\\u2028\\u2029"'),
+    ("é中\U0001F600".encode(), '"é中\U0001F600"'.encode()),
+    (b"\xed\xa0\x80", b'"\\ufffd\\ufffd\\ufffd"'),     # surrogate encoding is invalid UTF-8
+]
+
+
+@pytest.mark.parametrize("raw,want", JSON_KAT)
+def test_go_json_string_kat(raw, want):
+    import mr_oracle as M
+    assert M.go_json_string(raw) == want
+
+
+def test_go_json_lines_roundtrip_valid_utf8():
+    """For valid UTF-8 keys the encoding is lossless: json.loads gives the key back."""
+    import json
+
+    import mr_oracle as M
+    for key in [b"hello", "na\u00efve \u2028 \u2029 <tag> & \"q\" \\ \t".encode(), "\U0001F600x".encode()]:
+        line = M.go_json_kv_line(key, b"1")
+        d = json.loads(line)
+        assert d["Key"].encode() == key and d["Value"] == "1"
