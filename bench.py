@@ -294,6 +294,21 @@ def main():
         except Exception:
             traffic = None
 
+    # PCIe-inclusive rate (never `value`): one whole job with the split in pageable
+    # host memory, so the H2D copy is inside the job (mrg_run_job, MRG_INPUT_HOST)
+    pcie = None
+    if world == 1:
+        ctx.sync()
+        t0 = time.perf_counter()
+        if grep:
+            ctx.run_job(MRG_APP_GREP, host, pattern=PATTERN, nreduce=args.nreduce, copy_out=False)
+        else:
+            ctx.run_job(MRG_APP_WC, host, nreduce=args.nreduce, copy_out=False)
+        ctx.sync()
+        th = time.perf_counter() - t0
+        pcie = {"value": round(nbytes / th / 1e9, 3), "unit": "GB/s", "ms": round(th * 1e3, 3),
+                "note": "one job with the input in pageable host memory (H2D inside the job)"}
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, args.cpu_sample_files, args.cpu_sample_mb, args.nreduce, ctx)
@@ -334,6 +349,7 @@ def main():
             "aggregation_rounds": int(last["agg_rounds"]),
             "output_bytes": int(last["output_bytes"]),
             "checks": checks,
+            "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
