@@ -155,7 +155,8 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
 // emit: 0 = flush every bucket table into the HBM table (legacy),
 //       1 = emit records directly unless the bucket overflowed (then merge through HBM),
 //       2 = sample mode: emit table keys, drop misses (approximate counts for the dictionary)
-void launch_wc_agg(const Tables& t, int mode, int emit, hipStream_t s);
+// big: 1024-thread workgroups with twice the LDS table (later rounds)
+void launch_wc_agg(const Tables& t, int mode, int emit, bool big, hipStream_t s);
 // Segment layout of the multi-round aggregation (Spill::seg_off*) from the map's
 // stream counts; off8[E] / off16[E] (E = kSpillBuckets * kAggSegs) are the totals.
 // tmp: 2 * E u32 of scratch.

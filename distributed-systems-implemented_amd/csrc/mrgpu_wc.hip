@@ -501,27 +501,35 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 //     published (kUnwritten until then; 0xFF bytes never occur in UTF-8).
 // Ways are never freed, so once a key's first set is full a key absent from it
 // can never appear there later: lookups and claims agree on the key's set.
-constexpr int kAggShortSets = 1024;  // 4096 short keys (a bucket holds ~1/512 of the split's distinct keys)
-constexpr int kAggMidSets = 256;     // 1024 mid keys
-constexpr uint32_t kAggWaves = kAggThreads / kWave;
-
-struct alignas(16) AggLds {
-    unsigned long long sk[kAggShortSets * 4];
-    unsigned long long mk[kAggMidSets * 4 * 2];  // way w of set s: mk[2(4s+w)] = k0, mk[2(4s+w)+1] = k1
-    uint32_t sc[kAggShortSets * 4 + kWave];      // counts (+ per-lane dummies for branch-free adds)
-    uint32_t mc[kAggMidSets * 4];
-    unsigned long long red[4 * kAggWaves + 4];   // block_add4 / block_alloc scratch
-    uint32_t ncur8[kAggWaves], ncur16[kAggWaves];  // misses appended to each wave's segments
+// Two table sizes: round 0 uses 512-thread workgroups, two per CU (1024 short
+// sets = 4096 short keys + 1024 mid keys: a C2 bucket holds ~2 K distinct
+// keys); later rounds of high-cardinality splits use one 1024-thread workgroup
+// per CU with twice the keys, so a bucket settles in fewer rounds.
+template <int NS, int NM, int NW>
+struct alignas(16) AggLdsT {
+    static constexpr int kShortSets = NS, kMidSets = NM;
+    static constexpr uint32_t kWaves = NW;
+    static constexpr uint32_t kParts = NW / kAggSegs;  // waves per miss segment
+    unsigned long long sk[NS * 4];
+    unsigned long long mk[NM * 4 * 2];  // way w of set s: mk[2(4s+w)] = k0, mk[2(4s+w)+1] = k1
+    uint32_t sc[NS * 4 + kWave];        // counts (+ per-lane dummies for branch-free adds)
+    uint32_t mc[NM * 4];
+    unsigned long long red[4 * NW + 4];  // block_add4 / block_alloc scratch
+    uint32_t ncur8[kAggSegs], ncur16[kAggSegs];  // misses appended to each segment
 };
-static_assert(kAggWaves == kAggSegs, "one miss segment per aggregator wave");
+using AggLds = AggLdsT<1024, 256, kAggThreads / kWave>;
+using AggLdsBig = AggLdsT<2048, 512, 2 * kAggThreads / kWave>;
+static_assert(AggLds::kWaves == kAggSegs && AggLdsBig::kWaves == 2 * kAggSegs, "waves per miss segment");
 static_assert(2 * sizeof(AggLds) <= 160 * 1024, "two aggregator workgroups per CU");
+static_assert(sizeof(AggLdsBig) <= 160 * 1024, "one big aggregator workgroup per CU");
 
 __device__ __forceinline__ uint32_t second_hash(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 16) * 0xC2B2AE3Du; }
 template <int NSETS>
 __device__ __forceinline__ uint32_t set_base(uint32_t h) { return __umulhi(h, NSETS) * 4; }
 
 // 4-bit masks of the ways of a short set holding k / holding 0
-__device__ __forceinline__ void short_set_masks(const AggLds& A, uint32_t base, uint64_t k, uint32_t& m, uint32_t& z) {
+template <class AL>
+__device__ __forceinline__ void short_set_masks(const AL& A, uint32_t base, uint64_t k, uint32_t& m, uint32_t& z) {
     const u64x2 a = *(const lds_u64x2*)(&A.sk[base]);
     const u64x2 b = *(const lds_u64x2*)(&A.sk[base + 2]);
     m = (a.x == k ? 1u : 0u) | (a.y == k ? 2u : 0u) | (b.x == k ? 4u : 0u) | (b.y == k ? 8u : 0u);
@@ -535,11 +543,12 @@ __device__ __forceinline__ void short_set_masks(const AggLds& A, uint32_t base, 
 // exactly) when both sets are full without the key or claims keep racing.
 // (Measured: passing the caller's "first set full" to start at the second set
 // made C5's aggregation 51 -> 79 ms, a code-generation effect; not done.)
-__device__ bool short_insert_slow(AggLds& A, uint64_t k, uint32_t h, uint32_t add) {
+template <class AL>
+__device__ bool short_insert_slow(AL& A, uint64_t k, uint32_t h, uint32_t add) {
     for (int attempt = 0; attempt < 2; attempt++) {
         bool raced = false;
         for (int c = 0; c < 2 && !raced; c++) {
-            const uint32_t base = set_base<kAggShortSets>(c == 0 ? h : second_hash(h));
+            const uint32_t base = set_base<AL::kShortSets>(c == 0 ? h : second_hash(h));
             uint32_t m, z;
             short_set_masks(A, base, k, m, z);
             if (m) {
@@ -563,7 +572,8 @@ __device__ bool short_insert_slow(AggLds& A, uint64_t k, uint32_t h, uint32_t ad
 }
 
 // Mid keys: way masks of a set (64 bytes, four b128 reads)
-__device__ __forceinline__ void mid_set_masks(const AggLds& A, uint32_t base, uint64_t k0, uint64_t k1, uint32_t& m,
+template <class AL>
+__device__ __forceinline__ void mid_set_masks(const AL& A, uint32_t base, uint64_t k0, uint64_t k1, uint32_t& m,
                                               uint32_t& z, uint32_t& pend) {
     m = z = pend = 0;
 #pragma unroll
@@ -575,11 +585,12 @@ __device__ __forceinline__ void mid_set_masks(const AggLds& A, uint32_t base, ui
     }
 }
 
-__device__ bool mid_insert(AggLds& A, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
+template <class AL>
+__device__ bool mid_insert(AL& A, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
     for (int attempt = 0; attempt < 2; attempt++) {
         bool raced = false;
         for (int c = 0; c < 2 && !raced; c++) {
-            const uint32_t base = set_base<kAggMidSets>(c == 0 ? h : second_hash(h));
+            const uint32_t base = set_base<AL::kMidSets>(c == 0 ? h : second_hash(h));
             uint32_t m, z, pend;
             mid_set_masks(A, base, k0, k1, m, z, pend);
             if (m) {
@@ -606,17 +617,19 @@ __device__ bool mid_insert(AggLds& A, uint64_t k0, uint64_t k1, uint32_t h, uint
 }
 
 // Exact lookups in tables no lane is claiming in any more; -1 if absent.
-__device__ __forceinline__ int short_find_exact(const AggLds& A, uint64_t k, uint32_t h) {
+template <class AL>
+__device__ __forceinline__ int short_find_exact(const AL& A, uint64_t k, uint32_t h) {
     for (int c = 0; c < 2; c++) {
-        const uint32_t base = set_base<kAggShortSets>(c == 0 ? h : second_hash(h));
+        const uint32_t base = set_base<AL::kShortSets>(c == 0 ? h : second_hash(h));
         for (uint32_t w = 0; w < 4; w++)
             if (A.sk[base + w] == k) return (int)(base + w);
     }
     return -1;
 }
-__device__ __forceinline__ int mid_find_exact(const AggLds& A, uint64_t k0, uint64_t k1, uint32_t h) {
+template <class AL>
+__device__ __forceinline__ int mid_find_exact(const AL& A, uint64_t k0, uint64_t k1, uint32_t h) {
     for (int c = 0; c < 2; c++) {
-        const uint32_t base = set_base<kAggMidSets>(c == 0 ? h : second_hash(h));
+        const uint32_t base = set_base<AL::kMidSets>(c == 0 ? h : second_hash(h));
         for (uint32_t w = 0; w < 4; w++)
             if (A.mk[2 * (base + w)] == k0 && A.mk[2 * (base + w) + 1] == k1) return (int)(base + w);
     }
@@ -651,15 +664,17 @@ __device__ __forceinline__ void put_short(const Tables& t, unsigned long long o,
 // A key the tables could not take: appended to the wave's own miss segment
 // (LDS cursor, no HBM round trip in the loop).  It never exceeds the segment:
 // a wave's misses are at most the records it reads.
-__device__ __forceinline__ void defer_miss(AggLds& A, const Tables& t, uint64_t k0, uint64_t k1, bool keep_miss,
+template <class AL>
+__device__ __forceinline__ void defer_miss(AL& A, const Tables& t, uint64_t k0, uint64_t k1, bool keep_miss,
                                            uint32_t wv, uint64_t& miss) {
     if (keep_miss) {
-        const uint64_t seg = (uint64_t)blockIdx.x * kAggSegs + wv;
+        const uint32_t sg = wv % kAggSegs;  // the wave's segment (kParts waves share one)
+        const uint64_t seg = (uint64_t)blockIdx.x * kAggSegs + sg;
         if (k1 == 0) {
-            const uint32_t pos = atomicAdd(&A.ncur8[wv], 1u);
+            const uint32_t pos = atomicAdd(&A.ncur8[sg], 1u);
             t.sp.seg8_out[t.sp.seg_off8[seg] + pos] = k0;
         } else {
-            const uint32_t pos = atomicAdd(&A.ncur16[wv], 1u);
+            const uint32_t pos = atomicAdd(&A.ncur16[sg], 1u);
             t.sp.seg16_out[t.sp.seg_off16[seg] + pos] =
                 make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
         }
@@ -667,19 +682,32 @@ __device__ __forceinline__ void defer_miss(AggLds& A, const Tables& t, uint64_t 
     miss++;
 }
 
-template <uint32_t amode, bool kMid, uint32_t kAggUnroll>
-__device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void* pool_b, const uint32_t* gcounts,
+template <uint32_t amode, bool kMid, uint32_t kAggUnroll, class AL>
+__device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* pool_b, const uint32_t* gcounts,
                                          uint64_t gstride, uint32_t nwg, const uint64_t* gbase, bool keep_miss,
                                          uint64_t& miss) {
-    // streams s < nwg: gcounts[s] records at pool_b[gbase ? gbase[s] : s * gstride]
+    // Streams s < nwg.  Map streams (gbase null): gcounts[s] records at
+    // pool_b[s * gstride].  Miss segments (gbase set, nwg = kAggSegs * kParts):
+    // stream s is part s / kAggSegs of segment s % kAggSegs (gcounts[seg]
+    // records at gbase[seg]), split evenly between the segment's waves.
+    constexpr uint32_t kAggWaves = AL::kWaves;
     constexpr uint32_t kAggBlock = kAggUnroll * kWave;
     static_assert(kMaxMapWGs <= kAggWaves * kWave, "a wave's stream counts fit one VGPR");
+    auto part_range = [&](uint32_t sid, uint32_t& begin) -> uint32_t {
+        const uint32_t nseg = gcounts[sid % kAggSegs], pt = sid / kAggSegs;
+        begin = (uint32_t)((uint64_t)nseg * pt / AL::kParts);
+        return (uint32_t)((uint64_t)nseg * (pt + 1) / AL::kParts) - begin;
+    };
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     // The wave's streams are wv + kAggWaves * j, j < js; lane j holds stream j's
     // record count, so moving to the next stream is a readlane, not a load.
     const uint32_t js = nwg > wv ? (nwg - wv + kAggWaves - 1) / kAggWaves : 0u;
-    const uint32_t vcnt = lane < js ? gcounts[wv + kAggWaves * lane] : 0u;
+    uint32_t vcnt = 0;
+    if (lane < js) {
+        uint32_t b0;
+        vcnt = gbase ? part_range(wv + kAggWaves * lane, b0) : gcounts[wv + kAggWaves * lane];
+    }
     // wave-uniform cursor: stream j, record offset off within it (cnt records)
     uint32_t j = 0, off = 0, cnt = __builtin_amdgcn_readlane(vcnt, 0);
     while (j < js && off >= cnt) {
@@ -689,7 +717,12 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
     uint4 cur[kAggUnroll], nxt[kAggUnroll];
     auto load = [&](uint32_t jj, uint32_t o, uint32_t c, uint4* r) {
         const uint32_t sid = wv + kAggWaves * jj;
-        const uint64_t row = gbase ? (jj < js ? gbase[sid] : 0ull) : (uint64_t)sid * gstride;
+        uint64_t row = (uint64_t)sid * gstride;
+        if (gbase) {
+            uint32_t b0 = 0;
+            if (jj < js) part_range(sid, b0);
+            row = jj < js ? gbase[sid % kAggSegs] + b0 : 0ull;
+        }
 #pragma unroll
         for (uint32_t u = 0; u < kAggUnroll; u++) {
             const uint32_t i = o + u * kWave + lane;
@@ -725,7 +758,7 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
             uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
 #pragma unroll
             for (uint32_t u = 0; u < kAggUnroll; u++) {
-                base[u] = set_base<kAggShortSets>(h[u]);
+                base[u] = set_base<AL::kShortSets>(h[u]);
                 short_set_masks(A, base[u], ((uint64_t)cur[u].y << 32) | cur[u].x, m[u], z[u]);
             }
             bool slow[kAggUnroll];
@@ -734,7 +767,7 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
                 const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
                 const bool hit = valid && m[u] != 0;
                 slow[u] = valid && m[u] == 0;
-                const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)kAggShortSets * 4 + lane;
+                const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)AL::kShortSets * 4 + lane;
                 __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
 #pragma unroll
@@ -763,9 +796,11 @@ __device__ __forceinline__ void agg_pool(AggLds& A, const Tables& t, const void*
 
 // amode (benchmark ablation only, compile-time; results are wrong unless 0):
 // 128 = read + hash the records only.  emit: see launch_wc_agg.
-template <uint32_t amode>
-__global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit) {
-    __shared__ AggLds A;
+template <uint32_t amode, class AL>
+__global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int emit) {
+    __shared__ AL A;
+    constexpr uint32_t kAggWaves = AL::kWaves, kNT = kAggWaves * kWave;
+    constexpr uint32_t kAggShortSets = AL::kShortSets, kAggMidSets = AL::kMidSets;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t b = blockIdx.x;
     constexpr uint32_t E = (uint32_t)kSpillBuckets * kAggSegs;
@@ -779,14 +814,14 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
         }
     }
     if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4 + kWave; i += kAggThreads) A.sc[i] = 0;
-    for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) A.sk[i] = 0;
-    for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kAggThreads) {
+    for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4 + kWave; i += kNT) A.sc[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kNT) A.sk[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kNT) {
         A.mk[2 * i] = 0;
         A.mk[2 * i + 1] = kUnwritten;
         A.mc[i] = 0;
     }
-    if (tid < kAggWaves) A.ncur8[tid] = A.ncur16[tid] = 0;
+    if (tid < kAggSegs) A.ncur8[tid] = A.ncur16[tid] = 0;
     if (tid == 0 && emit == 1) atomicOr(&t.ctr->round_mask, 1ull << (t.sp.round & 63));
     __syncthreads();
     const bool keep_miss = emit != 2;
@@ -799,15 +834,18 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
                                  (uint64_t)kSpillBuckets * t.sp.sub_keys, t.sp.nwg, nullptr, keep_miss, miss);
     } else {
         // later rounds: wave w re-reads its own segment of the previous round's misses
-        agg_pool<amode, false, 8>(A, t, t.sp.seg8_in, t.sp.seg_n_in + b * kAggSegs, 0, kAggSegs,
+        agg_pool<amode, false, 8>(A, t, t.sp.seg8_in, t.sp.seg_n_in + b * kAggSegs, 0, kAggWaves,
                                   t.sp.seg_off8 + b * kAggSegs, keep_miss, miss);
-        agg_pool<amode, true, 4>(A, t, t.sp.seg16_in, t.sp.seg_n_in + E + b * kAggSegs, 0, kAggSegs,
+        agg_pool<amode, true, 4>(A, t, t.sp.seg16_in, t.sp.seg_n_in + E + b * kAggSegs, 0, kAggWaves,
                                  t.sp.seg_off16 + b * kAggSegs, keep_miss, miss);
     }
     __syncthreads();
-    // this wave's miss segments (written by its own lanes in the loop above)
-    const uint64_t seg = b * kAggSegs + wv;
-    const uint32_t n8 = keep_miss ? A.ncur8[wv] : 0u, n16 = keep_miss ? A.ncur16[wv] : 0u;
+    // this wave's miss segments (written in the loop above by the kParts waves
+    // sharing them; each walks its own interleaved share below)
+    const uint32_t sg = wv % kAggSegs, i0 = lane + kWave * (wv / kAggSegs);
+    constexpr uint32_t kStep = kWave * AL::kParts;
+    const uint64_t seg = b * kAggSegs + sg;
+    const uint32_t n8 = keep_miss ? A.ncur8[sg] : 0u, n16 = keep_miss ? A.ncur16[sg] : 0u;
     uint64_t* s8 = keep_miss ? t.sp.seg8_out + t.sp.seg_off8[seg] : nullptr;
     uint4* s16 = keep_miss ? t.sp.seg16_out + t.sp.seg_off16[seg] : nullptr;
     // merge: a key of this bucket went to the HBM table from the map kernel
@@ -815,24 +853,24 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
     // bucket (tables and misses) through the HBM table.
     const bool merge = emit == 0 || (emit == 1 && t.bflag[b] != 0);
     if (merge) {
-        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) {
+        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kNT) {
             const uint64_t k0 = A.sk[i];
             if (k0 != 0) short_insert(t, k0, 0, A.sc[i]);
         }
-        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kAggThreads) {
+        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kNT) {
             const uint64_t k0 = A.mk[2 * i];
             if (k0 != 0) short_insert(t, k0, A.mk[2 * i + 1], A.mc[i]);
         }
-        for (uint32_t i = lane; i < n8; i += kWave) {  // misses, all lanes in flight
+        for (uint32_t i = i0; i < n8; i += kStep) {  // misses, all lanes in flight
             const uint64_t k0 = s8[i];
             if (k0 != 0) short_insert(t, k0, 0, 1);
         }
-        for (uint32_t i = lane; i < n16; i += kWave) {
+        for (uint32_t i = i0; i < n16; i += kStep) {
             const uint4 k = s16[i];
             const uint64_t k0 = ((uint64_t)k.y << 32) | k.x;
             if (k0 != 0) short_insert(t, k0, ((uint64_t)k.w << 32) | k.z, 1);
         }
-        if (t.sp.seg_n_out && lane == 0) t.sp.seg_n_out[seg] = t.sp.seg_n_out[E + seg] = 0;
+        if (t.sp.seg_n_out && i0 == 0) t.sp.seg_n_out[seg] = t.sp.seg_n_out[E + seg] = 0;
         if (tid == 0) atomicAdd(&t.ctr->bflush, 1ull);
     } else {
         // Settle the misses against the (now stable) tables: a key that is there
@@ -844,9 +882,9 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
             // A bucket with fewer misses than carry_min (option; 0 = never)
             // settles them in the HBM table now instead of carrying them.
             uint32_t left = 0;
-            for (uint32_t w = 0; w < kAggWaves; w++) left += A.ncur8[w] + A.ncur16[w];
+            for (uint32_t w = 0; w < kAggSegs; w++) left += A.ncur8[w] + A.ncur16[w];
             const bool last = t.sp.last != 0 || left < t.sp.carry_min;
-            for (uint32_t i = lane; i < n8; i += kWave) {
+            for (uint32_t i = i0; i < n8; i += kStep) {
                 const uint64_t k0 = s8[i];
                 if (k0 == 0) continue;
                 const int slot = short_find_exact(A, k0, fold32((uint32_t)k0, (uint32_t)(k0 >> 32), 0, 0));
@@ -858,7 +896,7 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
                     carried++;
                 }
             }
-            for (uint32_t i = lane; i < n16; i += kWave) {
+            for (uint32_t i = i0; i < n16; i += kStep) {
                 const uint4 k = s16[i];
                 const uint64_t k0 = ((uint64_t)k.y << 32) | k.x, k1 = ((uint64_t)k.w << 32) | k.z;
                 if (k0 == 0) continue;
@@ -871,7 +909,7 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
                     carried++;
                 }
             }
-            if (t.sp.seg_n_out && lane == 0) {
+            if (t.sp.seg_n_out && i0 == 0) {
                 t.sp.seg_n_out[seg] = last ? 0u : n8;
                 t.sp.seg_n_out[E + seg] = last ? 0u : n16;
             }
@@ -879,14 +917,14 @@ __global__ void __launch_bounds__(kAggThreads) wc_agg_kernel(Tables t, int emit)
         __syncthreads();
         // one cursor allocation per workgroup, then each thread writes its keys
         uint32_t mine = 0;
-        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) mine += A.sk[i] != 0;
-        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kAggThreads) mine += A.mk[2 * i] != 0;
+        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kNT) mine += A.sk[i] != 0;
+        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kNT) mine += A.mk[2 * i] != 0;
         unsigned long long o = block_alloc<kAggWaves>(&t.ctr->nrec, mine, A.red);
-        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kAggThreads) {
+        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kNT) {
             const uint64_t k0 = A.sk[i];
             if (k0 != 0) put_short(t, o++, k0, 0, A.sc[i], emit == 1);
         }
-        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kAggThreads) {
+        for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kNT) {
             const uint64_t k0 = A.mk[2 * i];
             if (k0 != 0) put_short(t, o++, k0, A.mk[2 * i + 1], A.mc[i], emit == 1);
         }
@@ -1093,12 +1131,17 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     return true;
 }
 
-void launch_wc_agg(const Tables& t, int mode, int emit, hipStream_t s) {
+void launch_wc_agg(const Tables& t, int mode, int emit, bool big, hipStream_t s) {
     // mode 512 (diagnostic only, wrong results): a read-only pass first, so the
     // timed pass runs with warm caches and address translations
-    if (mode & 512) wc_agg_kernel<128><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
-    if (mode & 128) wc_agg_kernel<128><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
-    else wc_agg_kernel<0><<<kSpillBuckets, kAggThreads, 0, s>>>(t, emit);
+    if (mode & 512) wc_agg_kernel<128, AggLds><<<kSpillBuckets, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+    if (big) {
+        if (mode & 128) wc_agg_kernel<128, AggLdsBig><<<kSpillBuckets, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
+        else wc_agg_kernel<0, AggLdsBig><<<kSpillBuckets, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
+    } else {
+        if (mode & 128) wc_agg_kernel<128, AggLds><<<kSpillBuckets, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+        else wc_agg_kernel<0, AggLds><<<kSpillBuckets, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+    }
 }
 
 void launch_seg_layout(const Tables& t, uint32_t* tmp, uint64_t* off8, uint64_t* off16, hipStream_t s) {

@@ -114,8 +114,8 @@ def test_wc_record_buffer_growth(wctx):
         wctx.set_option("rec_cap", 0)
 
 
-@pytest.mark.parametrize("rounds", [0, 1, 2])
-def test_wc_bucket_aggregator_overflow(ctx, rounds):
+@pytest.mark.parametrize("rounds,big", [(0, 0), (1, 0), (2, 0), (0, 2), (0, -1), (3, -1)])
+def test_wc_bucket_aggregator_overflow(ctx, rounds, big):
     """More distinct spilled keys per bucket than the aggregator's LDS table holds:
     misses carried through further aggregation rounds (default), counted in the
     HBM table right away (1 round), or after one carried round (2)."""
@@ -123,6 +123,10 @@ def test_wc_bucket_aggregator_overflow(ctx, rounds):
     files = [bytes(voc.fill_files([26_000_000], [16], C.wc_params(vocab_lo=0, vocab_hi=3_000_000))[0])]
     ctx.set_option("agg_rounds", rounds)
     ctx.set_option("agg_carry_min", 0)  # default: carry every miss
+    # big = 0: 1024-thread tables in every round (default); -1: 512-thread tables
+    # in every round; 2: 512-thread round 0, 1024-thread later rounds
+    ctx.set_option("agg_big0", -1 if big != 0 else 0)
+    ctx.set_option("agg_big_later", -1 if big < 0 else 0)
     try:
         check(ctx, "wc", files, nreduces=(10,))
         st = ctx.stats()
@@ -135,6 +139,8 @@ def test_wc_bucket_aggregator_overflow(ctx, rounds):
     finally:
         ctx.set_option("agg_rounds", 0)
         ctx.set_option("agg_carry_min", 0)
+        ctx.set_option("agg_big0", 0)
+        ctx.set_option("agg_big_later", 0)
 
 
 def test_wc_large_vs_oracle(wctx):
