@@ -188,6 +188,7 @@ def main():
     ap.add_argument("--cpu-sample-files", type=int, default=16)
     ap.add_argument("--cpu-sample-mb", type=int, default=64)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-input) job")
     ap.add_argument("--opt", action="append", default=[], help="library option name=value (experiments; repeatable)")
     args = ap.parse_args()
     w = WORKLOADS[args.workload]
@@ -297,7 +298,7 @@ def main():
     # PCIe-inclusive rate (never `value`): one whole job with the split in pageable
     # host memory, so the H2D copy is inside the job (mrg_run_job, MRG_INPUT_HOST)
     pcie = None
-    if world == 1:
+    if world == 1 and not args.no_pcie:
         ctx.sync()
         t0 = time.perf_counter()
         if grep:

@@ -150,10 +150,10 @@ struct mrg_ctx {
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     int agg_rounds = 8;                 // bucket aggregation rounds at most (the last sends leftovers to HBM)
     // Misses per bucket below which a round settles them in the HBM table instead
-    // of carrying them.  0 (default): always carry.  Measured on C5: 4096 made
-    // the aggregation 59 ms -> 2.8 s (HBM inserts of hot leftover keys), while
-    // carrying C2's ~200 misses per bucket costs one short extra round.
-    uint32_t agg_carry_min = 0;
+    // of carrying them (C2: ~5 per bucket, so no second round).  Kept small:
+    // measured on C5, 4096 made the aggregation 59 ms -> 2.8 s (HBM inserts of
+    // hot leftover keys serialize).
+    uint32_t agg_carry_min = 64;
     // 1024-thread aggregator workgroups with twice the LDS table (one per CU)
     // instead of 512-thread ones (two per CU), in round 0 / later rounds.
     // Measured: C2 aggregation 1.63 -> 1.56 ms, C5 50 -> 30 ms (4 rounds, not 6).
@@ -744,7 +744,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "agg_rounds")) c->agg_rounds = v > 0 ? (int)v : 8;
     else if (!strcmp(name, "agg_big_later")) c->agg_big_later = v >= 0;  // -1: off
     else if (!strcmp(name, "agg_big0")) c->agg_big0 = v >= 0;  // -1: off
-    else if (!strcmp(name, "agg_carry_min")) c->agg_carry_min = v > 0 ? (uint32_t)v : 0u;
+    else if (!strcmp(name, "agg_carry_min")) c->agg_carry_min = v > 0 ? (uint32_t)v : v < 0 ? 0u : 64u;  // -1: always carry
     else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
     else if (!strcmp(name, "dict_min_bytes")) c->dict_min_bytes = v > 0 ? (uint64_t)v : (32ull << 20);
     else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);

@@ -122,7 +122,7 @@ def test_wc_bucket_aggregator_overflow(ctx, rounds, big):
     voc = C.Vocab(C.KIND_ASCII, 1.07, 3_000_000, 16)  # every word of a 3M vocabulary at least once
     files = [bytes(voc.fill_files([26_000_000], [16], C.wc_params(vocab_lo=0, vocab_hi=3_000_000))[0])]
     ctx.set_option("agg_rounds", rounds)
-    ctx.set_option("agg_carry_min", 0)  # default: carry every miss
+    ctx.set_option("agg_carry_min", -1)  # carry every miss (default: < 64 per bucket settle in HBM)
     # big = 0: 1024-thread tables in every round (default); -1: 512-thread tables
     # in every round; 2: 512-thread round 0, 1024-thread later rounds
     ctx.set_option("agg_big0", -1 if big != 0 else 0)
