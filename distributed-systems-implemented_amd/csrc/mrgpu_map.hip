@@ -44,48 +44,130 @@ __device__ __forceinline__ uint32_t eq_mask16(uint4 v, uint32_t rep) {
     return m;
 }
 
+// Streaming literal search.  Each wave streams its chunks through a private
+// two-slot LDS ring, one buffer_load_dwordx4 ... lds per chunk (64 lanes x 16 B:
+// lanes 0-59 the chunk's 960 own bytes, lanes 60-63 a 64-byte look-ahead),
+// issued one chunk ahead.  The DMA is inline asm, invisible to hipcc's waitcnt
+// pass, and the loop issues no other VMEM instruction on its common path, so the
+// wait for a chunk is a counted vmcnt(1) — a compiler-visible load or a global
+// pattern read in the loop would make hipcc wait vmcnt(0) and serialize the
+// prefetch (measured: 7.0 ms per 10 GB that way).  The pattern sits in LDS.
+// Candidates: positions whose byte and next byte equal the pattern's first two
+// (exact SWAR compares), verified in LDS for patterns of <= 65 bytes (longer
+// ones read HBM and drain with vmcnt(0)).  Matches are buffered per wave in LDS
+// and flushed to the list with ONE cursor atomic per flush: a same-address
+// device atomic per match serializes at the memory side (~12 ns each; C3's
+// ~600 K matches cost 7 ms that way, the whole kernel time).
+constexpr uint32_t kGrepOwn = 960;  // own bytes per chunk (lanes 0-59)
+constexpr uint32_t kGrepBuf = 256;  // buffered matches per wave
+typedef int gi32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void grep_dma(const uint8_t* in, uint64_t n, uint64_t cs, uint32_t lane, uint32_t lds_base) {
+    // descriptor base = the window start rounded down to 1 GiB: 32-bit offsets
+    const uint64_t base = cs & ~((1ull << 30) - 1);
+    const uint64_t r = n - base;  // wraps if base >= n
+    const uint32_t rhi = (uint32_t)(r >> 32), rlo = (uint32_t)r;
+    const uint32_t nrec = (int32_t)rhi < 0 ? 0u : (rhi != 0 || rlo > 0xFFFFFF00u) ? 0xFFFFFF00u : rlo;
+    const uint64_t b = (uint64_t)(in + base);
+    const gi32x4 rs = {(int)__builtin_amdgcn_readfirstlane((uint32_t)b),
+                       (int)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32) & 0xFFFFu),
+                       (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000};
+    const uint32_t voff = (uint32_t)(cs - base) + 16u * lane;
+    lds_base = __builtin_amdgcn_readfirstlane(lds_base);
+    asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds_base)
+                 : "memory", "m0");
+}
+
 __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
                                                             const uint8_t* __restrict__ pat, uint32_t plen, Tables t) {
-    __shared__ uint4 Wl[kWavesPerWG][kBuf / 16];
-    const uint32_t tid = threadIdx.x;
-    const uint32_t lane = tid & 63;
-    lds_uint4* W4 = (lds_uint4*)Wl[tid >> 6];
-    const lds_u8* Wb = (const lds_u8*)W4;
-    const uint32_t p0 = pat[0];
-    const uint32_t rep = p0 * 0x01010101u;
-    const bool in_lds = plen <= (uint32_t)kAhead;
-    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
-    uint64_t c = (uint64_t)blockIdx.x * kWavesPerWG + (tid >> 6);
-    ChunkRegs cur, nxt;
-    if (c < nchunks) load_chunk(in, n, c * kChunk, lane, cur);
-    for (; c < nchunks; c += stride) {
-        const uint64_t cs = c * kChunk;
-        if (c + stride < nchunks) load_chunk(in, n, (c + stride) * kChunk, lane, nxt);
-        stage_chunk(W4, cur, lane);
-        wave_sync();
-        {
-            uint32_t m = eq_mask16(cur.a, rep);
-            const uint32_t base = 16 * lane;
-            while (m) {
-                const uint32_t bit = __builtin_ctz(m);
-                m &= m - 1;
-                const uint64_t pos = cs + base + bit;
-                if (pos + plen > n) continue;
-                bool ok = true;
-                if (in_lds) {
-                    const lds_u8* q = Wb + kBack + base + bit;
-                    for (uint32_t k = 1; k < plen; k++)
-                        if (q[k] != pat[k]) { ok = false; break; }
-                } else {
-                    for (uint32_t k = 1; k < plen; k++)
-                        if (in[pos + k] != pat[k]) { ok = false; break; }
-                }
-                if (ok) list_append(t, pos);
-            }
+    __shared__ uint4 ring[kWavesPerWG][2][kChunk / 16];
+    __shared__ uint8_t P[kAhead + 16];
+    __shared__ unsigned long long mbuf[kWavesPerWG][kGrepBuf];  // buffered match positions
+    __shared__ uint32_t mcnt[kWavesPerWG];
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    if (tid < plen && tid < (uint32_t)sizeof(P)) P[tid] = pat[tid];
+    if (tid < kWavesPerWG) mcnt[tid] = 0;
+    __syncthreads();
+    lds_u32* wcnt = (lds_u32*)&mcnt[wv];
+    auto flush = [&]() {  // the wave's buffered matches -> the list (one atomic)
+        const uint32_t cnt = min(*wcnt, (uint32_t)kGrepBuf);
+        if (cnt == 0) return;
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(&t.ctr->nlist, (unsigned long long)cnt);
+        base = __shfl(base, 0);
+        for (uint32_t i = lane; i < cnt; i += 64) {
+            if (base + i < t.list_cap) t.list[base + i] = mbuf[wv][i];
+            else set_status(t.ctr, kStListFull);
         }
         wave_sync();
-        cur = nxt;
+        if (lane == 0) *wcnt = 0;
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        wave_sync();
+    };
+    const bool in_lds = plen <= (uint32_t)kAhead + 1;
+    const uint32_t p0 = P[0], p1 = plen > 1 ? P[1] : 0u;
+    const uint32_t rep0 = p0 * 0x01010101u, rep1 = p1 * 0x01010101u;
+    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
+    const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
+    const uint32_t slot0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ring[wv][0];
+    const uint64_t cstep = stride * kGrepOwn;
+    grep_dma(in, n, c0 * kGrepOwn, lane, slot0);
+    uint32_t k = 0;
+    uint64_t cs = c0 * kGrepOwn;
+    for (uint64_t c = c0; c < nchunks; c += stride, cs += cstep, k ^= 1u) {
+        grep_dma(in, n, cs + cstep, lane, slot0 + (k ^ 1u) * kChunk);  // next chunk into the other slot
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");              // this chunk's DMA has landed
+        const uint64_t n4 = n & ~3ull;
+        if ((n & 3) && n4 >= cs && n4 < cs + kChunk) {
+            // the split's last n % 4 bytes sit in a dword the range check zero-filled
+            if (lane < (uint32_t)(n & 3)) ((lds_u8*)ring[wv][k])[n4 - cs + lane] = in[n4 + lane];
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            wave_sync();
+        }
+        const lds_uint4* b4 = (const lds_uint4*)ring[wv][k];
+        const lds_u8* bb = (const lds_u8*)b4;
+        const uint4 v = from_v4(b4[lane]);
+        uint32_t m = lane < kGrepOwn / 16 ? eq_mask16(v, rep0) : 0u;
+        if (plen > 1) {
+            const uint32_t m1 = eq_mask16(v, rep1);
+            const uint32_t nb = (uint32_t)__shfl_down((int)(m1 & 1u), 1);  // next lane's byte 0 (lane 59 -> 60: look-ahead)
+            m &= (m1 >> 1) | (nb << 15);
+        }
+        bool any = false;
+        while (m) {
+            const uint32_t bit = __builtin_ctz(m);
+            m &= m - 1;
+            const uint32_t at = 16 * lane + bit;
+            const uint64_t pos = cs + at;
+            if (pos + plen > n) continue;
+            bool ok = true;
+            if (in_lds) {
+                for (uint32_t q = 2; q < plen; q++)
+                    if (bb[at + q] != P[q]) { ok = false; break; }
+            } else {
+                for (uint32_t q = 2; q < plen; q++)
+                    if (in[pos + q] != pat[q]) { ok = false; break; }
+                any = true;
+            }
+            if (ok) {
+                const uint32_t at_m = __hip_atomic_fetch_add(wcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (at_m < (uint32_t)kGrepBuf) {
+                    mbuf[wv][at_m] = pos;
+                } else {  // buffer full inside one chunk (pathological): append directly
+                    __hip_atomic_fetch_add(wcnt, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    list_append(t, pos);
+                    any = true;
+                }
+            }
+        }
+        if (__ballot(any)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rare paths: drain
+        wave_sync();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's LDS reads are done before it is refilled
+        if (*wcnt >= (uint32_t)kGrepBuf - 64) flush();
     }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last prefetch lands before the workgroup exits
+    flush();
 }
 
 // Empty pattern: every line (strings.Split yields len(sep-count)+1 lines).
@@ -228,10 +310,10 @@ void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables
 
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
                      hipStream_t s) {
-    const uint64_t nchunks = (n + kChunk - 1) / kChunk;
+    const uint64_t nchunks = (n + kGrepOwn - 1) / kGrepOwn;
     if (nchunks == 0 || plen == 0) return;
     uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
-    const uint64_t gmax = (uint64_t)grid * 4;
+    const uint64_t gmax = (uint64_t)grid * 2;
     if (g > gmax) g = gmax;
     grep_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, d_pat, plen, t);
 }

@@ -63,6 +63,18 @@ def mixed_words(n: int, seed: int) -> bytes:
     return bytes(out)
 
 
+def _seams(pat: bytes, nseams: int) -> bytes:
+    """Occurrences of pat starting 1..12 bytes before every 960-byte seam (so each
+    one crosses a seam), a "di" decoy before each, lines of 'q' in between."""
+    b = bytearray(b"q" * (960 * (nseams + 1)))
+    for i in range(1, nseams + 1):
+        at = 960 * i - 1 - (i % 12)
+        b[at - 4:at - 1] = b"di\n"
+        b[at:at + len(pat)] = pat
+        b[at + len(pat)] = 0x0A
+    return bytes(b)
+
+
 def grep_edge_cases() -> dict[str, tuple[list[bytes], bytes]]:
     return {
         "basic": ([b"a distributed system\nnothing here\ndistributed\n\ndistributed distributed x\n"], b"distributed"),
@@ -78,6 +90,13 @@ def grep_edge_cases() -> dict[str, tuple[list[bytes], bytes]]:
         "long_lines": ([(b"w" * 5000 + b" distributed " + b"v" * 3000 + b"\n") * 3], b"distributed"),
         # > 64 distinct matching lines with one 16-byte prefix, in scrambled order,
         # and lines that are prefixes of others: the reduce's long tied run
+        # the pattern ending exactly at the split's end, for every n % 4 (the
+        # grep map streams 16-byte range-checked loads and patches the last dword)
+        "tail_n_mod4": ([b"x\n" + b"y" * k + b" distributed" for k in range(4)], b"distributed"),
+        # occurrences straddling every 960-byte chunk seam (own bytes + look-ahead),
+        # a 2-byte-prefix decoy before each, and a 65-byte pattern across seams
+        "chunk_seams": ([_seams(b"distributed", 40)], b"distributed"),
+        "pattern_65_seams": ([b"".join(b"r" * (960 * i - 30) + b"z" * 65 + b"\n" for i in range(1, 12))], b"z" * 65),
         "tied_lines": ([b"".join(b"the distributed system " + str((i * 7919) % 1000).encode() * (1 + i % 3) + b"\n"
                                  for i in range(1000)) + b"the distributed system \nthe distributed system\n"],
                        b"distributed"),
