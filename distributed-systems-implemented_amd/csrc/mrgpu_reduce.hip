@@ -45,7 +45,7 @@ struct DBuf {
 };
 
 struct ReduceWs {
-    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs;
+    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext;
     uint64_t* h_pinned = nullptr;  // small pinned staging
 };
 
@@ -57,7 +57,7 @@ ReduceWs* reduce_ws_new() {
 
 void reduce_ws_free(ReduceWs* w) {
     if (!w) return;
-    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs};
+    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext};
     for (DBuf* b : bs) b->release();
     if (w->h_pinned) hipHostFree(w->h_pinned);
     delete w;
@@ -83,15 +83,22 @@ __global__ void iota_kernel(uint32_t* p, uint64_t n) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) p[i] = (uint32_t)i;
 }
 
-// which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part
-__global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32) {
+// Long keys (grep lines) carry key bytes 16-63 as kExtWords big-endian words
+// (ext_words_kernel); the first two are radix passes, all of them shorten the
+// comparison sort's compares to independent 8-byte loads.
+constexpr int kExtWords = 6;
+
+// which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part, 4 / 5 = ext words 0 / 1 (key bytes 16-23 / 24-31)
+__global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32,
+                                  const uint64_t* ext) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint32_t j = perm[i];
         if (which == 0) k32[i] = r.len[j];
         else if (which == 1) k64[i] = __builtin_bswap64(r.k1[j]);
         else if (which == 2) k64[i] = __builtin_bswap64(r.k0[j]);
-        else k32[i] = r.part[j];
+        else if (which == 3) k32[i] = r.part[j];
+        else k64[i] = ext[kExtWords * (uint64_t)j + (which - 4)];
     }
 }
 
@@ -138,8 +145,51 @@ __device__ int rec_cmp(const Recs& r, uint32_t a, uint32_t b) {
     return (la > lb) - (la < lb);
 }
 
-__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b, bool with_k1) {
-    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && (!with_k1 || r.k1[a] == r.k1[b]);
+// Key bytes 16-63 of each record as kExtWords big-endian words (zero past the
+// key's end).  Words 0-1 extend the radix prefix to 32 bytes, so that only keys
+// equal in their first 32 zero-padded bytes need the comparison sort.
+__global__ void ext_words_kernel(Recs r, uint64_t* ext) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < r.n; j += stride) {
+        const uint32_t len = r.len[j];
+        const uint8_t* p = len > 16 ? r.arena + r.koff[j] : nullptr;
+#pragma unroll
+        for (int w = 0; w < kExtWords; w++) ext[kExtWords * j + w] = p ? key_word_be(p, 16 + 8 * w, len) : 0ull;
+    }
+}
+
+// rec_cmp with key bytes 16-63 from the ext words: the common case is a handful
+// of independent 8-byte loads instead of a chain of arena byte loads.
+__device__ int rec_cmp_ext(const Recs& r, const uint64_t* ext, uint32_t a, uint32_t b) {
+    const uint64_t a0 = __builtin_bswap64(r.k0[a]), b0 = __builtin_bswap64(r.k0[b]);
+    if (a0 != b0) return a0 < b0 ? -1 : 1;
+    const uint64_t a1 = __builtin_bswap64(r.k1[a]), b1 = __builtin_bswap64(r.k1[b]);
+    if (a1 != b1) return a1 < b1 ? -1 : 1;
+    const uint64_t* ea = ext + kExtWords * (uint64_t)a;
+    const uint64_t* eb = ext + kExtWords * (uint64_t)b;
+#pragma unroll
+    for (int w = 0; w < kExtWords; w++)
+        if (ea[w] != eb[w]) return ea[w] < eb[w] ? -1 : 1;
+    constexpr uint32_t kCovered = 16 + 8 * kExtWords;
+    const uint32_t la = r.len[a], lb = r.len[b];
+    if (la > kCovered && lb > kCovered) {
+        const uint8_t* pa = r.arena + r.koff[a];
+        const uint8_t* pb = r.arena + r.koff[b];
+        const uint32_t mx = la > lb ? la : lb;
+        for (uint32_t pos = kCovered; pos < mx; pos += 8) {
+            const uint64_t wa = key_word_be(pa, pos, la), wb = key_word_be(pb, pos, lb);
+            if (wa != wb) return wa < wb ? -1 : 1;
+        }
+    }
+    // equal zero-padded words up to here: the shorter key is a prefix of the longer
+    return (la > lb) - (la < lb);
+}
+
+__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b, bool with_k1, const uint64_t* ext) {
+    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && (!with_k1 || r.k1[a] == r.k1[b]) &&
+           (ext == nullptr ||
+            (ext[kExtWords * (uint64_t)a] == ext[kExtWords * (uint64_t)b] &&
+             ext[kExtWords * (uint64_t)a + 1] == ext[kExtWords * (uint64_t)b + 1]));
 }
 
 // tie[i] = 1 when sorted position i has the same (part, prefix) as i-1, the
@@ -147,11 +197,11 @@ __device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t 
 // distinct keys with equal zero-padded prefixes are only ordered by a full
 // bytewise comparison.
 __global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8_t* tie, unsigned long long* flags,
-                                 bool with_k1) {
+                                 bool with_k1, const uint64_t* ext) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint8_t t = 0;
-        if (i > 0 && same_prefix(r, perm[i - 1], perm[i], with_k1)) t = 1;
+        if (i > 0 && same_prefix(r, perm[i - 1], perm[i], with_k1, ext)) t = 1;
         tie[i] = t;
         if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
     }
@@ -197,9 +247,10 @@ __global__ void mark_all_ties_kernel(const uint8_t* tie, uint64_t n, uint8_t* ln
 // (partition, key) order of two records: the order the whole sort produces.
 struct FullLess {
     Recs r;
+    const uint64_t* ext;  // kExtWords per record, or nullptr
     __device__ bool operator()(const uint32_t& a, const uint32_t& b) const {
         if (r.part[a] != r.part[b]) return r.part[a] < r.part[b];
-        return rec_cmp(r, a, b) < 0;
+        return (ext ? rec_cmp_ext(r, ext, a, b) : rec_cmp(r, a, b)) < 0;
     }
 };
 
@@ -365,7 +416,8 @@ struct MarkedPos {
 // runs are contiguous and already in (partition, prefix) order, which the full
 // order refines, so sorting all marked members together keeps every run in its
 // own positions.  Scratch: sel (positions), key_b (values, two halves).
-static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t n, const uint8_t* lng, hipStream_t s) {
+static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t n, const uint8_t* lng, const uint64_t* ext,
+                          hipStream_t s) {
     RCHK(ws->sel.ensure(n * 4 + 1024));
     RCHK(ws->offs.ensure(64));
     uint32_t* pos = ws->sel.as<uint32_t>();
@@ -384,9 +436,9 @@ static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
     const unsigned g = (unsigned)((m + 255) / 256 < 4096 ? (m + 255) / 256 : 4096);
     gather_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, va);
     tb = 0;
-    RCHK(rocprim::merge_sort(nullptr, tb, va, vb, (size_t)m, FullLess{r}, s));
+    RCHK(rocprim::merge_sort(nullptr, tb, va, vb, (size_t)m, FullLess{r, ext}, s));
     RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::merge_sort(ws->tmp.p, tb, va, vb, (size_t)m, FullLess{r}, s));
+    RCHK(rocprim::merge_sort(ws->tmp.p, tb, va, vb, (size_t)m, FullLess{r, ext}, s));
     scatter_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, vb);
     return 0;
 }
@@ -433,14 +485,23 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
 
     uint32_t* pa = ws->perm_a.as<uint32_t>();
     uint32_t* pb = ws->perm_b.as<uint32_t>();
+    // grep keys are whole lines (> 16 bytes, often sharing their first words):
+    // sort with the k1 pass and the key-byte 16-31 passes from the start
+    const bool k1_first = has_long && app != 1;
+    const uint64_t* ext = nullptr;
+    if (k1_first) {
+        RCHK(ws->ext.ensure(n * 8 * kExtWords));
+        ext_words_kernel<<<grid_for(n), 256, 0, s>>>(r, ws->ext.as<uint64_t>());
+        ext = ws->ext.as<uint64_t>();
+    }
     auto pass32 = [&](int which, unsigned bits) -> int {
-        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, nullptr, ws->key_a.as<uint32_t>());
+        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, nullptr, ws->key_a.as<uint32_t>(), ext);
         int e = sort_pass<uint32_t>(ws, ws->key_a.as<uint32_t>(), ws->key_b.as<uint32_t>(), pa, pb, n, bits, s);
         std::swap(pa, pb);
         return e;
     };
     auto pass64 = [&](int which) -> int {
-        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, ws->key_a.as<uint64_t>(), nullptr);
+        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, ws->key_a.as<uint64_t>(), nullptr, ext);
         int e = sort_pass<uint64_t>(ws, ws->key_a.as<uint64_t>(), ws->key_b.as<uint64_t>(), pa, pb, n, 64, s);
         std::swap(pa, pb);
         return e;
@@ -452,6 +513,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     auto sort_all = [&](bool with_k1) -> int {
         int e;
         iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
+        if (with_k1 && ext && ((e = pass64(5)) || (e = pass64(4)))) return e;
         if (with_k1 && (e = pass64(1))) return e;
         if ((e = pass64(2))) return e;
         if (all && nreduce > 1) {
@@ -470,25 +532,22 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         uint8_t* lng = tie + n;
         RCHK(hipMemsetAsync(lng, 0, n, s));
         RCHK(hipMemsetAsync(flags + 2, 0, 16, s));
-        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1);
+        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1, with_k1 ? ext : nullptr);
         if (all_runs) {  // every tied run goes to the merge sort (no per-run insertion sort)
             mark_all_ties_kernel<<<grid_for(n), 256, 0, s>>>(tie, n, lng);
             RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 2, 8, hipMemcpyDeviceToHost, s));
             RCHK(hipStreamSynchronize(s));
             *any_long = ws->h_pinned[3] != 0;
-            return *any_long ? sort_long_runs(ws, r, pa, n, lng, s) : 0;
+            return *any_long ? sort_long_runs(ws, r, pa, n, lng, ext, s) : 0;
         }
         fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, kMaxRun, flags, lng);
         RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 3, 8, hipMemcpyDeviceToHost, s));
         RCHK(hipStreamSynchronize(s));
         *any_long = ws->h_pinned[3] != 0;
-        if (*any_long && merge) return sort_long_runs(ws, r, pa, n, lng, s);
+        if (*any_long && merge) return sort_long_runs(ws, r, pa, n, lng, ext, s);
         return 0;
     };
     int e;
-    // grep keys are whole lines (> 16 bytes, often sharing their first words):
-    // sort with the k1 pass from the start
-    const bool k1_first = has_long && app != 1;
     if ((e = sort_all(k1_first))) return e;
     if (k1_first) {
         bool any_long = false;
