@@ -321,12 +321,23 @@ __global__ void collect_long_kernel(Tables t) {
         if (o >= t.out_cap || off + len > t.out.arena_n) { set_status(t.ctr, kStRecFull); continue; }
         uint32_t h = 2166136261u;
         uint64_t k0 = 0, k1 = 0;
-        for (uint64_t k = 0; k < len; k++) {
-            const uint32_t b = s.rep[k];
-            t.out.arena[off + k] = (uint8_t)b;
-            h = fnv1a32_step(h, b);
-            if (k < 8) k0 |= (uint64_t)b << (8 * k);
-            else if (k < 16) k1 |= (uint64_t)b << (8 * (k - 8));
+        // the representative's bytes by aligned 16-byte blocks (it sits at a
+        // random input offset: one load per block, not a chain of byte loads)
+        for (int64_t q = 0; q < (int64_t)len;) {
+            int64_t bi;
+            const uint4 v = block16(s.rep, q, bi);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const int64_t k = bi + j;
+                if (k < q || k >= (int64_t)len) continue;
+                const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                t.out.arena[off + k] = (uint8_t)b;
+                h = fnv1a32_step(h, b);
+                if (k < 8) k0 |= (uint64_t)b << (8 * k);
+                else if (k < 16) k1 |= (uint64_t)b << (8 * (k - 8));
+            }
+            q = bi + 16;
         }
         t.out.k0[o] = k0;
         t.out.k1[o] = k1;
