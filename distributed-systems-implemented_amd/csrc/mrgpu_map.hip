@@ -292,59 +292,84 @@ __global__ void collect_short_kernel(Tables t, const uint32_t* idx, const uint32
 
 __global__ void nrec_add_kernel(Counters* ctr, const uint32_t* d_count) { ctr->nrec += *d_count; }
 
-// LongTable (small): one wave-aggregated cursor per wave.
-__global__ void collect_long_kernel(Tables t) {
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+// One LongTable record: key bytes copied to the arena at `off` by aligned
+// 16-byte blocks (the representative sits at a random input offset: one load
+// per block, not a chain of byte loads), prefix words and partition from them.
+__device__ __forceinline__ void emit_long_rec(const Tables& t, const LongSlot& s, uint64_t o, uint64_t off, uint64_t len) {
+    if (o >= t.out_cap || off + len > t.out.arena_n) { set_status(t.ctr, kStRecFull); return; }
+    uint32_t h = 2166136261u;
+    uint64_t k0 = 0, k1 = 0;
+    for (int64_t q = 0; q < (int64_t)len;) {
+        int64_t bi;
+        const uint4 v = block16(s.rep, q, bi);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 16; j++) {
+            const int64_t k = bi + j;
+            if (k < q || k >= (int64_t)len) continue;
+            const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+            t.out.arena[off + k] = (uint8_t)b;
+            h = fnv1a32_step(h, b);
+            if (k < 8) k0 |= (uint64_t)b << (8 * k);
+            else if (k < 16) k1 |= (uint64_t)b << (8 * (k - 8));
+        }
+        q = bi + 16;
+    }
+    t.out.k0[o] = k0;
+    t.out.k1[o] = k1;
+    t.out.len[o] = (uint32_t)len;
+    t.out.cnt[o] = s.count;
+    t.out.part[o] = (h & 0x7fffffffu) % t.nreduce;
+    t.out.koff[o] = off;
+}
+
+// LongTable -> records.  Each wave takes kCollectSlots x 64 slots per step and
+// reserves their records and arena bytes with ONE pair of cursor atomics
+// (same-address device atomics serialize at the memory side: one pair per 64
+// slots of a 1 M-slot table cost ~0.6 ms).
+constexpr int kCollectSlots = 8;
+__global__ void __launch_bounds__(256) collect_long_kernel(Tables t) {
+    const uint32_t lane = threadIdx.x & 63;
     const uint64_t n = t.lo_mask + 1;
-    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x; i0 < n; i0 += stride) {
-        const uint64_t i = i0 + threadIdx.x;
-        LongSlot s{0, nullptr, 0, 0};
-        if (i < n) s = t.lo[i];
-        const bool valid = s.hash != 0 && s.rep != nullptr && s.len != 0;
-        const unsigned long long o = wave_alloc(&t.ctr->nrec, valid);
-        const uint64_t len = valid ? s.len - 1 : 0;
-        // arena bytes: exclusive wave scan of the lengths, one atomic per wave
-        uint64_t incl = len;
-        const uint32_t lane = threadIdx.x & 63;
+    constexpr uint64_t kStep = 64 * kCollectSlots;
+    const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    for (uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kStep; w0 < n; w0 += nw * kStep) {
+        LongSlot sl[kCollectSlots];
+        uint32_t c = 0;
+        uint64_t bytes = 0;
+#pragma unroll
+        for (int k = 0; k < kCollectSlots; k++) {
+            const uint64_t i = w0 + 64 * k + lane;
+            sl[k] = i < n ? t.lo[i] : LongSlot{0, nullptr, 0, 0};
+            const bool valid = sl[k].hash != 0 && sl[k].rep != nullptr && sl[k].len != 0;
+            if (!valid) sl[k].len = 0;  // len + 1 of a valid slot is >= 1
+            c += valid;
+            bytes += valid ? sl[k].len - 1 : 0;
+        }
+        // inclusive wave scans of the record and byte counts
+        uint64_t ic = c, ib = bytes;
 #pragma unroll
         for (int off = 1; off < 64; off <<= 1) {
-            const uint64_t y = __shfl_up(incl, off);
-            if (lane >= (uint32_t)off) incl += y;
+            const uint64_t yc = __shfl_up(ic, off), yb = __shfl_up(ib, off);
+            if (lane >= (uint32_t)off) { ic += yc; ib += yb; }
         }
-        unsigned long long abase = 0;
-        if (lane == 63 && incl) abase = atomicAdd(&t.ctr->arena, (unsigned long long)incl);
+        unsigned long long rbase = 0, abase = 0;
+        if (lane == 63 && ic) {
+            rbase = atomicAdd(&t.ctr->nrec, (unsigned long long)ic);
+            abase = atomicAdd(&t.ctr->arena, (unsigned long long)ib);
+            atomicAdd(&t.ctr->nlong_rec, (unsigned long long)ic);
+        }
+        rbase = __shfl(rbase, 63);
         abase = __shfl(abase, 63);
-        const uint64_t nv = __popcll(__ballot(valid));
-        if (lane == 0 && nv) atomicAdd(&t.ctr->nlong_rec, (unsigned long long)nv);
-        if (!valid) continue;
-        const unsigned long long off = abase + incl - len;
-        if (o >= t.out_cap || off + len > t.out.arena_n) { set_status(t.ctr, kStRecFull); continue; }
-        uint32_t h = 2166136261u;
-        uint64_t k0 = 0, k1 = 0;
-        // the representative's bytes by aligned 16-byte blocks (it sits at a
-        // random input offset: one load per block, not a chain of byte loads)
-        for (int64_t q = 0; q < (int64_t)len;) {
-            int64_t bi;
-            const uint4 v = block16(s.rep, q, bi);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        uint64_t o = rbase + ic - c, off = abase + ib - bytes;
 #pragma unroll
-            for (int j = 0; j < 16; j++) {
-                const int64_t k = bi + j;
-                if (k < q || k >= (int64_t)len) continue;
-                const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                t.out.arena[off + k] = (uint8_t)b;
-                h = fnv1a32_step(h, b);
-                if (k < 8) k0 |= (uint64_t)b << (8 * k);
-                else if (k < 16) k1 |= (uint64_t)b << (8 * (k - 8));
-            }
-            q = bi + 16;
+        for (int k = 0; k < kCollectSlots; k++) {
+            if (sl[k].len == 0) continue;
+            const uint64_t len = sl[k].len - 1;
+            emit_long_rec(t, sl[k], o, off, len);
+            o++;
+            off += len;
         }
-        t.out.k0[o] = k0;
-        t.out.k1[o] = k1;
-        t.out.len[o] = (uint32_t)len;
-        t.out.cnt[o] = s.count;
-        t.out.part[o] = (h & 0x7fffffffu) % t.nreduce;
-        t.out.koff[o] = off;
     }
 }
 
@@ -424,7 +449,11 @@ int launch_collect(const Tables& t, ReduceWs* ws, uint64_t base, uint64_t short_
         collect_short_kernel<<<(unsigned)g, 256, 0, s>>>(t, idx, cnt, base);
         nrec_add_kernel<<<1, 1, 0, s>>>(t.ctr, cnt);
     }
-    if (long_table) collect_long_kernel<<<256, 256, 0, s>>>(t);
+    if (long_table) {
+        const uint64_t steps = (t.lo_mask + 1 + 64 * kCollectSlots - 1) / (64 * kCollectSlots);  // wave steps
+        const uint64_t g = (steps + 3) / 4 < 2048 ? (steps + 3) / 4 : 2048;
+        collect_long_kernel<<<(unsigned)g, 256, 0, s>>>(t);
+    }
     return (int)hipGetLastError();
 }
 
