@@ -152,9 +152,31 @@ __global__ void ext_words_kernel(Recs r, uint64_t* ext) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < r.n; j += stride) {
         const uint32_t len = r.len[j];
-        const uint8_t* p = len > 16 ? r.arena + r.koff[j] : nullptr;
+        uint64_t wd[kExtWords] = {};
+        if (len > 16) {
+            // key bytes [16, min(len, 64)) by aligned 16-byte blocks of the arena
+            // (one load per block; an aligned block never crosses a page)
+            const uint8_t* p = r.arena + r.koff[j];
+            const int64_t end = len < 16 + 8 * kExtWords ? (int64_t)len : 16 + 8 * kExtWords;
+            for (int64_t q = 16; q < end;) {
+                const uintptr_t a = (uintptr_t)(p + q), ab = a & ~(uintptr_t)15;
+                const int64_t bi = q - (int64_t)(a - ab);
+                const uint4 v = *(const uint4*)ab;
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
-        for (int w = 0; w < kExtWords; w++) ext[kExtWords * j + w] = p ? key_word_be(p, 16 + 8 * w, len) : 0ull;
+                for (int b = 0; b < 16; b++) {
+                    const int64_t k = bi + b;
+                    if (k < q || k >= end) continue;
+                    const uint64_t byte = (w4[b >> 2] >> (8 * (b & 3))) & 0xFFu;
+#pragma unroll
+                    for (int w = 0; w < kExtWords; w++)  // register-indexed: select, no scratch
+                        if ((k - 16) >> 3 == w) wd[w] |= byte << (56 - 8 * ((k - 16) & 7));
+                }
+                q = bi + 16;
+            }
+        }
+#pragma unroll
+        for (int w = 0; w < kExtWords; w++) ext[kExtWords * j + w] = wd[w];
     }
 }
 
