@@ -855,6 +855,17 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         if ((rc = read_counters(c))) return rc;
         if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
         uint64_t nlist = c->h_ctr->nlist;
+        // The hits bound the distinct lines: size the LongTable for them now (one
+        // map re-run) instead of growing it 4x per overflowing lines pass (C3's
+        // first job took three).  Up to 2^26 hits; past that the grow path decides.
+        if (nlist <= (1ull << 26)) {
+            int need = c->lo_log2;
+            while ((1ull << need) * 7 < nlist * 10) need++;
+            if (need > c->lo_log2) {
+                c->lo_log2 = need;
+                continue;
+            }
+        }
         launch_grep_lines(in, len, (uint32_t)plen, t, nlist, c->s);
         HCHK(c, hipGetLastError());
         HCHK(c, hipEventRecord(c->ev[2], c->s));
