@@ -84,21 +84,19 @@ __global__ void iota_kernel(uint32_t* p, uint64_t n) {
 }
 
 // Long keys (grep lines) carry key bytes 16-63 as kExtWords big-endian words
-// (ext_words_kernel); the first two are radix passes, all of them shorten the
-// comparison sort's compares to independent 8-byte loads.
+// (ext_words_kernel): the comparison sort's compares become independent 8-byte
+// loads.
 constexpr int kExtWords = 6;
 
-// which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part, 4 / 5 = ext words 0 / 1 (key bytes 16-23 / 24-31)
-__global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32,
-                                  const uint64_t* ext) {
+// which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part
+__global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint32_t j = perm[i];
         if (which == 0) k32[i] = r.len[j];
         else if (which == 1) k64[i] = __builtin_bswap64(r.k1[j]);
         else if (which == 2) k64[i] = __builtin_bswap64(r.k0[j]);
-        else if (which == 3) k32[i] = r.part[j];
-        else k64[i] = ext[kExtWords * (uint64_t)j + (which - 4)];
+        else k32[i] = r.part[j];
     }
 }
 
@@ -146,8 +144,7 @@ __device__ int rec_cmp(const Recs& r, uint32_t a, uint32_t b) {
 }
 
 // Key bytes 16-63 of each record as kExtWords big-endian words (zero past the
-// key's end).  Words 0-1 extend the radix prefix to 32 bytes, so that only keys
-// equal in their first 32 zero-padded bytes need the comparison sort.
+// key's end), read by the tied-run comparator.
 __global__ void ext_words_kernel(Recs r, uint64_t* ext) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < r.n; j += stride) {
@@ -207,11 +204,8 @@ __device__ int rec_cmp_ext(const Recs& r, const uint64_t* ext, uint32_t a, uint3
     return (la > lb) - (la < lb);
 }
 
-__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b, bool with_k1, const uint64_t* ext) {
-    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && (!with_k1 || r.k1[a] == r.k1[b]) &&
-           (ext == nullptr ||
-            (ext[kExtWords * (uint64_t)a] == ext[kExtWords * (uint64_t)b] &&
-             ext[kExtWords * (uint64_t)a + 1] == ext[kExtWords * (uint64_t)b + 1]));
+__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b, bool with_k1) {
+    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && (!with_k1 || r.k1[a] == r.k1[b]);
 }
 
 // tie[i] = 1 when sorted position i has the same (part, prefix) as i-1, the
@@ -219,11 +213,11 @@ __device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t 
 // distinct keys with equal zero-padded prefixes are only ordered by a full
 // bytewise comparison.
 __global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8_t* tie, unsigned long long* flags,
-                                 bool with_k1, const uint64_t* ext) {
+                                 bool with_k1) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint8_t t = 0;
-        if (i > 0 && same_prefix(r, perm[i - 1], perm[i], with_k1, ext)) t = 1;
+        if (i > 0 && same_prefix(r, perm[i - 1], perm[i], with_k1)) t = 1;
         tie[i] = t;
         if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
     }
@@ -508,7 +502,9 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     uint32_t* pa = ws->perm_a.as<uint32_t>();
     uint32_t* pb = ws->perm_b.as<uint32_t>();
     // grep keys are whole lines (> 16 bytes, often sharing their first words):
-    // sort with the k1 pass and the key-byte 16-31 passes from the start
+    // sort with the k1 pass from the start; ties merge-sort on the ext words
+    // (measured: two more 64-bit radix passes over bytes 16-31 cost more, ~16
+    // launches, than the larger merge sort they save)
     const bool k1_first = has_long && app != 1;
     const uint64_t* ext = nullptr;
     if (k1_first) {
@@ -517,13 +513,13 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         ext = ws->ext.as<uint64_t>();
     }
     auto pass32 = [&](int which, unsigned bits) -> int {
-        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, nullptr, ws->key_a.as<uint32_t>(), ext);
+        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, nullptr, ws->key_a.as<uint32_t>());
         int e = sort_pass<uint32_t>(ws, ws->key_a.as<uint32_t>(), ws->key_b.as<uint32_t>(), pa, pb, n, bits, s);
         std::swap(pa, pb);
         return e;
     };
     auto pass64 = [&](int which) -> int {
-        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, ws->key_a.as<uint64_t>(), nullptr, ext);
+        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, ws->key_a.as<uint64_t>(), nullptr);
         int e = sort_pass<uint64_t>(ws, ws->key_a.as<uint64_t>(), ws->key_b.as<uint64_t>(), pa, pb, n, 64, s);
         std::swap(pa, pb);
         return e;
@@ -535,7 +531,6 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     auto sort_all = [&](bool with_k1) -> int {
         int e;
         iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
-        if (with_k1 && ext && ((e = pass64(5)) || (e = pass64(4)))) return e;
         if (with_k1 && (e = pass64(1))) return e;
         if ((e = pass64(2))) return e;
         if (all && nreduce > 1) {
@@ -554,7 +549,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         uint8_t* lng = tie + n;
         RCHK(hipMemsetAsync(lng, 0, n, s));
         RCHK(hipMemsetAsync(flags + 2, 0, 16, s));
-        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1, with_k1 ? ext : nullptr);
+        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1);
         if (all_runs) {  // every tied run goes to the merge sort (no per-run insertion sort)
             mark_all_ties_kernel<<<grid_for(n), 256, 0, s>>>(tie, n, lng);
             RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 2, 8, hipMemcpyDeviceToHost, s));
