@@ -61,6 +61,7 @@ WORKLOADS = {
 }
 PATTERN = b"distributed"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+XGMI_LINK_GBS = 153.0  # per xGMI link (7 links x ~153 GB/s per GPU)
 
 
 def log(msg):
@@ -129,11 +130,43 @@ def check_output(parts: list[bytes], nreduce: int, app: str = "wc", sample: int 
     return out
 
 
-def cpu_baseline(w: dict, sample_files: int, sample_mb: int, nreduce: int, ctx: Context) -> dict | None:
-    """The oracle's distributed restatement (oracle/_build/mrcpu: coordinator + N worker
-    processes, JSON-lines intermediates — mr/coordinator.go + mr/worker.go) on a bounded
-    sample of the same workload; its outputs are also compared with the GPU's."""
+def ascii_word_count(dev) -> int | None:
+    """Independent word count of a device-resident ASCII split with plain torch
+    ops (no libmrgpu code): Go's FieldsFunc(!IsLetter) words in ASCII text are
+    the maximal runs of [A-Za-z].  None when the split holds a byte >= 0x80."""
+    total, prev, step = 0, False, 1 << 30
+    for off in range(0, dev.numel(), step):
+        x = dev[off:off + step]
+        if int(x.max()) >= 0x80:
+            return None
+        y = x | 32
+        let = (y >= 97) & (y <= 122)
+        total += int((let[1:] & ~let[:-1]).sum()) + int(bool(let[0]) and not prev)
+        prev = bool(let[-1])
+        del x, y, let
+    return total
+
+
+def _cpu_files(w: dict, sample_files: int, sample_mb: int, tmp: str):
+    voc = C.Vocab(w["kind"], w["s"], w["V"], w["seed"])
+    files, paths = [], []
+    for i in range(sample_files):
+        f = voc.fill_files([sample_mb * 1_000_000], [w["seed"] + i], file_params(w, i, w["files"]))[0]
+        p = os.path.join(tmp, f"pg-{i}.txt")
+        f.tofile(p)
+        files.append(f)
+        paths.append(p)
+    return files, paths
+
+
+def cpu_baseline(w: dict, sample_files: int, sample_mb: int, seq_files: int, nreduce: int, ctx: Context) -> dict | None:
+    """The oracle's restatements of the reference on a bounded sample of the same
+    workload, on this host's cores: oracle/_build/mrcpu = mrcoordinator + N mrworker
+    processes (mr/coordinator.go, mr/worker.go: JSON-lines mr-X-Y shuffle, one
+    write(2) per KV), and oracle/_build/mrseq = main/mrsequential.go (one process).
+    The GPU's output is compared with mrcpu's on the same sample."""
     exe = os.path.join(ROOT, "oracle", "_build", "mrcpu")
+    seq_exe = os.path.join(ROOT, "oracle", "_build", "mrseq")
     if not os.path.exists(exe):
         log("cpu_baseline skipped: oracle/_build/mrcpu not built")
         return None
@@ -141,20 +174,12 @@ def cpu_baseline(w: dict, sample_files: int, sample_mb: int, nreduce: int, ctx: 
     base = "/dev/shm" if os.path.isdir("/dev/shm") else None
     tmp = tempfile.mkdtemp(prefix="mrcpu-", dir=base)
     try:
-        voc = C.Vocab(w["kind"], w["s"], w["V"], w["seed"])
-        sizes = [sample_mb * 1_000_000] * sample_files
-        files = [voc.fill_files([sizes[i]], [w["seed"] + i], file_params(w, i, w["files"]))[0]
-                 for i in range(sample_files)]
-        paths = []
-        for i, f in enumerate(files):
-            p = os.path.join(tmp, f"pg-{i}.txt")
-            f.tofile(p)
-            paths.append(p)
+        files, paths = _cpu_files(w, sample_files, sample_mb, tmp)
         wdir = os.path.join(tmp, "work")
         os.makedirs(wdir)
         app_args = ["--app", "grep", "--pattern", PATTERN.decode()] if w["app"] == "grep" else ["--app", "wc"]
         res = subprocess.run([exe] + app_args + ["--nreduce", str(nreduce), "--workers", str(workers), "--dir", wdir]
-                             + paths, capture_output=True, text=True, timeout=600)
+                             + paths, capture_output=True, text=True, timeout=900)
         if res.returncode != 0:
             log(f"mrcpu failed: {res.stderr[-500:]}")
             return None
@@ -165,13 +190,25 @@ def cpu_baseline(w: dict, sample_files: int, sample_mb: int, nreduce: int, ctx: 
             gpu_out = ctx.run_job(MRG_APP_GREP, joined, pattern=PATTERN, nreduce=nreduce)
         else:
             gpu_out = ctx.run_job(MRG_APP_WC, joined, nreduce=nreduce)
-        return {"value": round(info["bytes"] / info["seconds"] / 1e9, 4), "unit": "GB/s", "cores": workers,
-                "kind": "port",
-                "sample": f"{sample_files} files x {sample_mb} MB of the same corpus generator "
-                          f"({info['bytes'] / 1e9:.2f} GB), mrcpu = restated mrcoordinator + {workers} mrworker "
-                          f"processes with JSON-lines mr-X-Y shuffle, nReduce={nreduce}; "
-                          f"{info['seconds']:.1f} s",
-                "gpu_output_identical": gpu_out == cpu_out}
+        out = {"value": round(info["bytes"] / info["seconds"] / 1e9, 4), "unit": "GB/s", "cores": workers,
+               "kind": "port",
+               "sample": f"{sample_files} files x {sample_mb} MB of the same corpus generator "
+                         f"({info['bytes'] / 1e9:.2f} GB); oracle/_build/mrcpu = restated mrcoordinator + {workers} "
+                         f"mrworker processes, JSON-lines mr-X-Y shuffle with one write(2) per KV as "
+                         f"worker.go:84-89, nReduce={nreduce}; {info['seconds']:.1f} s",
+               "gpu_output_identical": gpu_out == cpu_out}
+        if os.path.exists(seq_exe) and seq_files > 0:
+            sdir = os.path.join(tmp, "seq")
+            os.makedirs(sdir)
+            r2 = subprocess.run([seq_exe] + app_args + ["--out", os.path.join(sdir, "mr-out-0")] + paths[:seq_files],
+                                capture_output=True, text=True, timeout=900)
+            if r2.returncode == 0:
+                si = json.loads(r2.stdout.strip().splitlines()[-1])
+                out["mrseq"] = {"value": round(si["bytes"] / si["seconds"] / 1e9, 4), "unit": "GB/s", "cores": 1,
+                                "sample": f"{seq_files} x {sample_mb} MB; oracle/_build/mrseq = restated "
+                                          f"main/mrsequential.go (one process, every KV resident, one sort, one "
+                                          f"write(2) per key); {si['seconds']:.1f} s"}
+        return out
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -187,6 +224,7 @@ def main():
     ap.add_argument("--nreduce", type=int, default=None, help="override the workload's nReduce")
     ap.add_argument("--cpu-sample-files", type=int, default=16)
     ap.add_argument("--cpu-sample-mb", type=int, default=64)
+    ap.add_argument("--cpu-seq-files", type=int, default=2, help="files of the sample the single-process mrseq times")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-input) job")
     ap.add_argument("--opt", action="append", default=[], help="library option name=value (experiments; repeatable)")
@@ -223,11 +261,15 @@ def main():
         obj = [Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         ctx.comm_init(obj[0], world, rank)
-    dptr = ctx.device_alloc(nbytes)
+    # the split, resident in HBM before the timed region (a torch tensor: the
+    # independent word count below reads it with plain torch ops)
+    dev = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{local}")
     step = 1 << 30
     for off in range(0, nbytes, step):
         n = min(step, nbytes - off)
-        ctx.h2d(dptr + off, host[off:off + n], n)
+        dev[off:off + n].copy_(torch.from_numpy(host[off:off + n]))
+    torch.cuda.synchronize()
+    dptr = dev.data_ptr()
     ctx.sync()
 
     def run_step():
@@ -273,11 +315,52 @@ def main():
     checks = check_output(parts, args.nreduce, w["app"])
     checks["deterministic"] = hashlib.sha256(out).hexdigest() == hashlib.sha256(
         ctypes.string_at(*run_step()[:2])).hexdigest()
+    if not grep:
+        # Σ counts of the output must equal an independent count of the input's words
+        indep = ascii_word_count(dev)
+        checks["total_words_independent"] = indep
+        checks["total_words_match"] = None if indep is None else indep == checks["total_words"]
     if world > 1:
         key = "matching_lines" if grep else "total_words"
         tw = torch.tensor([checks[key]], dtype=torch.int64)
         dist.all_reduce(tw)
         checks[key] = int(tw.item())
+        if not grep and checks.get("total_words_independent") is not None:
+            ti = torch.tensor([checks["total_words_independent"]], dtype=torch.int64)
+            dist.all_reduce(ti)
+            checks["total_words_independent"] = int(ti.item())
+            checks["total_words_match"] = checks["total_words_independent"] == checks[key]
+
+    # N > 1: the shuffle's share and the weak-scaling efficiency against the
+    # same ranks running their splits with no shuffle (T(1) of the same per-GPU
+    # work, measured in this process, every partition reduced locally)
+    multi = None
+    if world > 1:
+        ex_ms = sum(st["exchange_ms"] for st in stats) / len(stats)
+        snd = sum(st["shuffle_send_bytes"] for st in stats) / len(stats)
+        ctx.set_option("skip_exchange", 1)
+        dist.barrier()
+        ctx.sync()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            run_step()
+        ctx.sync()
+        t1 = time.perf_counter() - t1
+        dist.barrier()
+        ctx.set_option("skip_exchange", 0)
+        v = torch.tensor([ex_ms, snd, t1], dtype=torch.float64)
+        vmax = v.clone()
+        dist.all_reduce(vmax, op=dist.ReduceOp.MAX)
+        links = min(world - 1, 7)
+        per_gpu_bw = snd / (ex_ms / 1e3) / 1e9 if ex_ms > 0 else 0.0
+        multi = {"exchange_ms": round(float(vmax[0]), 3), "shuffle_bytes_per_gpu": int(snd),
+                 "xgmi_achieved_GBps": round(per_gpu_bw, 2), "xgmi_peak_GBps": links * XGMI_LINK_GBS,
+                 "xgmi_frac": round(per_gpu_bw / (links * XGMI_LINK_GBS), 4),
+                 "t1_ms_per_step": round(float(vmax[2]) / args.steps * 1e3, 3),
+                 "weak_scaling_efficiency": round(float(vmax[2]) / t_max, 4),
+                 "note": "shuffle bytes = wire bytes a rank sends to the other ranks (max over ranks of the mean over timed "
+                         "steps); xgmi_frac = those bytes / exchange time / (min(P-1,7) x 153 GB/s); "
+                         "E(P) = T(1) / T(P), T(1) = the same per-GPU splits run with no shuffle in this process"}
 
     total_bytes = nbytes * world * args.steps
     value = total_bytes / t_max / 1e9
@@ -312,7 +395,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(w, args.cpu_sample_files, args.cpu_sample_mb, args.nreduce, ctx)
+        cpu = cpu_baseline(w, args.cpu_sample_files, args.cpu_sample_mb, args.cpu_seq_files, args.nreduce, ctx)
 
     if rank == 0:
         line = {
@@ -342,6 +425,7 @@ def main():
                           "dict": round(last["dict_ms"], 3), "agg": round(last["agg_ms"], 3),
                           "exchange": round(last["exchange_ms"], 3), "reduce": round(last["reduce_ms"], 3),
                           "d2h": round(last["d2h_ms"], 3)},
+            "staged_input_bytes": int(last["staged_bytes"]),
             "distinct_keys": int(last["distinct_keys"]),
             "dict_hit_words": int(last["dict_hits"]),
             "spilled_words": int(last["lds_overflow"]),
@@ -351,10 +435,11 @@ def main():
             "output_bytes": int(last["output_bytes"]),
             "checks": checks,
             "pcie_inclusive": pcie,
+            "multi_gpu": multi,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    ctx.device_free(dptr)
+    del dev
     ctx.close()
     if world > 1:
         dist.destroy_process_group()

@@ -23,7 +23,7 @@
 
 #include "../../include/mrgpu.h"
 #include "letter_table.inc"
-#include "mrgpu_internal.h"
+#include "mrgpu_device.h"
 
 using namespace mrg;
 
@@ -148,6 +148,7 @@ struct mrg_ctx {
     DevBuf bflag, dict, dict_cnt, sample, recbuf, recarena, sortbuf, dbg;
     DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
+    DevBuf ghits, glines, gdefer;        // grep: sorted hits, resolved (start, end) lines, deferred hits
     int agg_rounds = 8;                 // bucket aggregation rounds at most (the last sends leftovers to HBM)
     // Misses per bucket below which a round settles them in the HBM table instead
     // of carrying them (C2: ~5 per bucket, so no second round).  Kept small:
@@ -169,7 +170,16 @@ struct mrg_ctx {
     uint32_t spill_nwg = 1;
     int64_t spill_force_sub = 0;
     int map_mode = 0;  // benchmark ablation of wc_map_kernel phases (0 = normal)
+    // mrg_run_job without the shuffle even with a communicator (bench.py's
+    // same-process T(1) for the weak-scaling efficiency: the rank's own split,
+    // every partition reduced locally)
+    bool skip_exchange = false;
     int sh_log2 = 20, lo_log2 = 14;  // HBM tables (grow on overflow); the wc short table holds only the spill path's leftovers
+    // LongTable size of the current call: wc maps start from lo_log2 (words > 16
+    // bytes; sticky, grows on overflow), grep maps size it per job from their
+    // resolved line count, merges / imports from their record count.  Only
+    // 2^lo_log2_cur slots are cleared and collected.
+    int lo_log2_cur = 14;
     uint64_t list_cap = 1u << 20;
     int grid = 256;
     ReduceWs* rws = nullptr;
@@ -226,7 +236,10 @@ static Tables make_tables(mrg_ctx* c) {
     t.sh = (ShortSlot*)c->sh.p;
     t.sh_mask = (1ull << c->sh_log2) - 1;
     t.lo = (LongSlot*)c->lo.p;
-    t.lo_mask = (1ull << c->lo_log2) - 1;
+    t.lo_mask = (1ull << c->lo_log2_cur) - 1;
+    t.hits = (const uint64_t*)c->ghits.p;
+    t.lines = (uint64_t*)c->glines.p;
+    t.defer = (uint64_t*)c->gdefer.p;
     t.list = (uint64_t*)c->list.p;
     t.list_cap = c->list_cap;
     t.ctr = (Counters*)c->ctr.p;
@@ -303,7 +316,9 @@ static int ensure_tables(mrg_ctx* c) {
     HCHK(c, c->sh.ensure(sizeof(ShortSlot) << c->sh_log2));
     if (c->sh.p != old) c->sh_clean = false;  // fresh memory is not zeroed
     HCHK(c, c->bflag.ensure(kSpillBuckets * sizeof(uint32_t)));
-    HCHK(c, c->lo.ensure(sizeof(LongSlot) << c->lo_log2));
+    const size_t lo_bytes = sizeof(LongSlot) << c->lo_log2_cur;
+    if (c->lo.cap > 4 * lo_bytes && c->lo.cap > (256u << 20)) c->lo.release();  // a past grep job's big table
+    HCHK(c, c->lo.ensure(lo_bytes));
     HCHK(c, c->list.ensure(c->list_cap * sizeof(uint64_t)));
     HCHK(c, c->ctr.ensure(sizeof(Counters)));
     return MRG_OK;
@@ -392,7 +407,7 @@ static int collect_parts(mrg_ctx* c, int app, uint32_t nreduce, mrg_parts** out)
 static int grow_on_overflow(mrg_ctx* c, uint32_t st) {
     int again = 0;
     if (st & kStShortFull) { c->sh_log2 += 2; again = 1; }
-    if (st & kStLongFull) { c->lo_log2 += 2; again = 1; }
+    if (st & kStLongFull) { c->lo_log2_cur += 2; again = 1; }
     if (st & kStListFull) { c->list_cap = std::max<uint64_t>(c->list_cap * 4, c->h_ctr->nlist + 1024); again = 1; }
     if (st & kStRecFull) { c->rec_cap = std::max<uint64_t>(c->rec_cap * 2, c->h_ctr->nrec + 4096); again = 1; }
     return again;
@@ -588,6 +603,7 @@ static int aggregate_rounds(mrg_ctx* c, Tables& t) {
 // wc: dictionary, map, bucket aggregation, dictionary records, long words, collect.
 static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce, LetterTables lt, mrg_parts** out) {
     int rc;
+    c->lo_log2_cur = c->lo_log2;
     if ((rc = ensure_spill(c, len))) return rc;
     const uint32_t nwg = c->spill_nwg;
     HCHK(c, c->dict_cnt.ensure((size_t)nwg * kDictSlots * sizeof(uint32_t)));
@@ -599,6 +615,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
     if ((rc = ensure_spill(c, len))) return rc;
     HCHK(c, hipEventRecord(c->ev[10], c->s));
     for (int attempt = 0; attempt < 8; attempt++) {
+        c->lo_log2 = std::max(c->lo_log2, c->lo_log2_cur);  // long words: the grown size sticks for later wc maps
         if ((rc = ensure_tables(c)) || (rc = ensure_recbuf(c))) return rc;
         Tables t = make_tables(c);
         t.dict = have_dict ? (const uint4*)c->dict.p : nullptr;
@@ -663,6 +680,113 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         c->stats.dict_hits = h.dict_hits;
         c->stats.distinct_keys = h.nrec;
         c->stats.long_keys = h.nlong_rec;
+        *out = p;
+        return MRG_OK;
+    }
+    return fail(c, MRG_ENOMEM, "mrg_map: tables kept overflowing");
+}
+
+// Go's utf8.Valid (the acceptance ranges of SURVEY.md Appendix A.1).
+static bool go_valid_utf8(const uint8_t* p, size_t n) {
+    for (size_t i = 0; i < n;) {
+        const uint8_t c0 = p[i];
+        if (c0 < 0x80) { i++; continue; }
+        size_t need;
+        uint8_t lo = 0x80, hi = 0xBF;
+        if (c0 >= 0xC2 && c0 <= 0xDF) need = 1;
+        else if (c0 >= 0xE0 && c0 <= 0xEF) { need = 2; if (c0 == 0xE0) lo = 0xA0; else if (c0 == 0xED) hi = 0x9F; }
+        else if (c0 >= 0xF0 && c0 <= 0xF4) { need = 3; if (c0 == 0xF0) lo = 0x90; else if (c0 == 0xF4) hi = 0x8F; }
+        else return false;
+        if (i + need >= n) return false;  // truncated sequence
+        if (p[i + 1] < lo || p[i + 1] > hi) return false;
+        for (size_t k = 2; k <= need; k++)
+            if ((p[i + k] & 0xC0) != 0x80) return false;
+        i += need + 1;
+    }
+    return true;
+}
+
+// grep map (mrapps/dgrep.go:18-36) with a literal pattern:
+//   grep_map_kernel -> occurrence positions (one per line per chunk) -> sort ->
+//   grep_resolve_kernel (+ _long) -> one (start, end) per matching line
+//   occurrence -> the LongTable sized for them -> collect.
+// The pattern is a literal (regexp.QuoteMeta semantics).  dgrep.go:20-23 returns
+// no lines when regexp.Compile fails, which for a quoted literal happens exactly
+// when it is not valid UTF-8; a pattern holding '\n' matches no line of
+// strings.Split(contents, "\n") (dgrep.go:26).
+static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* pat, size_t plen, uint32_t nreduce,
+                    mrg_parts** out) {
+    int rc;
+    if (!go_valid_utf8(pat, plen) || (plen && memchr(pat, '\n', plen))) {
+        HCHK(c, hipEventRecord(c->ev[0], c->s));
+        if ((rc = parts_alloc(c, 0, 0, MRG_APP_GREP, nreduce, out))) return rc;
+        c->stats.distinct_keys = 0;
+        return MRG_OK;
+    }
+    HCHK(c, c->pat.ensure(plen + 16));
+    if (plen) HCHK(c, hipMemcpyAsync(c->pat.p, pat, plen, hipMemcpyHostToDevice, c->s));
+    c->lo_log2_cur = 14;
+    for (int attempt = 0; attempt < 8; attempt++) {
+        if ((rc = ensure_tables(c))) return rc;
+        Tables t = make_tables(c);
+        clear_for_run(c, t);
+        HCHK(c, hipEventRecord(c->ev[0], c->s));
+        if (plen) launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);
+        else launch_grep_all_lines(in, len, t, c->grid, c->s);
+        HCHK(c, hipGetLastError());
+        HCHK(c, hipEventRecord(c->ev[1], c->s));
+        if ((rc = read_counters(c))) return rc;
+        if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
+        const uint64_t nhits = c->h_ctr->nlist;
+        // sort the hits by position, resolve their lines
+        HCHK(c, c->ghits.ensure_grow(nhits * 8 + 64));
+        HCHK(c, c->glines.ensure_grow(nhits * 16 + 64));
+        HCHK(c, c->gdefer.ensure_grow(nhits * 8 + 64));
+        t = make_tables(c);
+        unsigned bits = 1;
+        while (bits < 64 && (len >> bits) != 0) bits++;
+        if (nhits && sort_u64_keys(c->rws, t.list, (uint64_t*)c->ghits.p, nhits, bits, c->s))
+            return fail(c, MRG_EDEVICE, "grep: hit sort failed");
+        launch_grep_resolve(in, len, (uint32_t)plen, t, nhits, c->s);
+        HCHK(c, hipGetLastError());
+        if ((rc = read_counters(c))) return rc;
+        if (c->h_ctr->ndefer) {
+            launch_grep_resolve_long(in, len, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, c->s);
+            HCHK(c, hipGetLastError());
+            if ((rc = read_counters(c))) return rc;
+        }
+        if (c->h_ctr->status & kStListFull) return fail(c, MRG_EDEVICE, "grep: line list overflow");
+        const uint64_t nlines = c->h_ctr->nlines;
+        HCHK(c, hipEventRecord(c->ev[8], c->s));
+        // The LongTable holds at most nlines distinct lines: size it for them
+        // (capped; a table that still fills up grows, and only the inserts re-run).
+        int need = 14;
+        while (need < 24 && (1ull << need) * 7 < nlines * 10) need++;
+        c->lo_log2_cur = need;
+        bool ok = false;
+        for (int grow = 0; grow < 8 && !ok; grow++) {
+            if ((rc = ensure_tables(c))) return rc;
+            t = make_tables(c);
+            clear_long_table(t, c->s);
+            launch_grep_insert(in, t, nlines, c->s);
+            HCHK(c, hipGetLastError());
+            if ((rc = read_counters(c))) return rc;
+            const uint32_t st = c->h_ctr->status;
+            if (st & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", st);
+            if (st & kStLongFull) c->lo_log2_cur += 2;
+            else ok = true;
+        }
+        if (!ok) return fail(c, MRG_ENOMEM, "grep: line table kept overflowing");
+        HCHK(c, hipEventRecord(c->ev[2], c->s));
+        c->stats.map_kernel_ms = ev_ms(c->ev[0], c->ev[1]);
+        mrg_parts* p = nullptr;
+        if ((rc = collect_parts(c, MRG_APP_GREP, nreduce, &p))) return rc;
+        HCHK(c, hipEventRecord(c->ev[3], c->s));
+        HCHK(c, hipEventSynchronize(c->ev[3]));
+        c->stats.map_total_ms = ev_ms(c->ev[0], c->ev[3]);
+        c->stats.agg_ms = ev_ms(c->ev[1], c->ev[8]);
+        c->stats.long_ms = ev_ms(c->ev[8], c->ev[2]);
+        c->stats.collect_ms = ev_ms(c->ev[2], c->ev[3]);
         *out = p;
         return MRG_OK;
     }
@@ -736,7 +860,7 @@ const char* mrg_last_error(const mrg_ctx* c) { return c ? c->err.c_str() : "null
 int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     if (!c || !name) return MRG_EINVAL;
     if (!strcmp(name, "short_table_log2")) c->sh_log2 = v > 0 ? (int)v : 20;
-    else if (!strcmp(name, "long_table_log2")) c->lo_log2 = v > 0 ? (int)v : 14;
+    else if (!strcmp(name, "long_table_log2")) c->lo_log2 = c->lo_log2_cur = v > 0 ? (int)v : 14;
     else if (!strcmp(name, "list_cap")) c->list_cap = v > 0 ? (uint64_t)v : (1u << 20);
     else if (!strcmp(name, "map_grid")) c->grid = v > 0 ? (int)v : map_grid_size(c->device);
     else if (!strcmp(name, "map_mode")) c->map_mode = (int)v;
@@ -749,6 +873,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "dict_min_bytes")) c->dict_min_bytes = v > 0 ? (uint64_t)v : (32ull << 20);
     else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);
     else if (!strcmp(name, "rec_cap")) c->rec_cap = v > 0 ? (uint64_t)v : (1u << 21);
+    else if (!strcmp(name, "skip_exchange")) c->skip_exchange = v > 0;
     else return fail(c, MRG_EINVAL, "unknown option %s", name);
     return MRG_OK;
 }
@@ -831,64 +956,11 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         HCHK(c, hipMemcpyAsync(c->staging.p, buf, len, kind == MRG_INPUT_HOST ? hipMemcpyHostToDevice
                                                                            : hipMemcpyDeviceToDevice, c->s));
         in = (const uint8_t*)c->staging.p;
-    }
-    bool grep_nl = false;
-    if (app == MRG_APP_GREP) {
-        HCHK(c, c->pat.ensure(plen + 16));
-        if (plen) HCHK(c, hipMemcpyAsync(c->pat.p, pat, plen, hipMemcpyHostToDevice, c->s));
-        grep_nl = plen && memchr(pat, '\n', plen) != nullptr;  // no line can contain '\n'
+        c->stats.staged_bytes = len;
     }
     LetterTables lt{c->d_l1, c->d_l2};
     if (app == MRG_APP_WC) return wc_map(c, in, len, nreduce, lt, out);
-    for (int attempt = 0; attempt < 8; attempt++) {
-        if ((rc = ensure_tables(c))) return rc;
-        Tables t = make_tables(c);
-        clear_for_run(c, t);
-        HCHK(c, hipEventRecord(c->ev[0], c->s));
-        if (!grep_nl) {
-            if (plen) launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);
-            else launch_grep_all_lines(in, len, t, c->grid, c->s);
-        }
-        HCHK(c, hipGetLastError());
-        HCHK(c, hipEventRecord(c->ev[1], c->s));
-        HCHK(c, hipEventRecord(c->ev[8], c->s));
-        if ((rc = read_counters(c))) return rc;
-        if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
-        uint64_t nlist = c->h_ctr->nlist;
-        // The hits bound the distinct lines: size the LongTable for them now (one
-        // map re-run) instead of growing it 4x per overflowing lines pass (C3's
-        // first job took three).  Up to 2^26 hits; past that the grow path decides.
-        if (nlist <= (1ull << 26)) {
-            int need = c->lo_log2;
-            while ((1ull << need) * 7 < nlist * 10) need++;
-            if (need > c->lo_log2) {
-                c->lo_log2 = need;
-                continue;
-            }
-        }
-        launch_grep_lines(in, len, (uint32_t)plen, t, nlist, c->s);
-        HCHK(c, hipGetLastError());
-        HCHK(c, hipEventRecord(c->ev[2], c->s));
-        if ((rc = read_counters(c))) return rc;
-        uint32_t st = c->h_ctr->status;
-        if (st & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", st);
-        if (grow_on_overflow(c, st)) continue;
-        c->stats.map_kernel_ms = ev_ms(c->ev[0], c->ev[1]);
-        c->stats.lds_overflow = c->h_ctr->spilled + c->h_ctr->spill_ovf;
-        c->stats.spill_ovf = c->h_ctr->spill_ovf;
-        c->stats.agg_miss = c->h_ctr->agg_miss;
-        mrg_parts* p = nullptr;
-        if ((rc = collect_parts(c, app, nreduce, &p))) return rc;
-        HCHK(c, hipEventRecord(c->ev[3], c->s));
-        HCHK(c, hipEventSynchronize(c->ev[3]));
-        c->stats.map_total_ms = ev_ms(c->ev[0], c->ev[3]);
-        c->stats.agg_ms = ev_ms(c->ev[1], c->ev[8]);
-        c->stats.long_ms = ev_ms(c->ev[8], c->ev[2]);
-        c->stats.collect_ms = ev_ms(c->ev[2], c->ev[3]);
-        *out = p;
-        return MRG_OK;
-    }
-    return fail(c, MRG_ENOMEM, "mrg_map: tables kept overflowing");
+    return grep_map(c, in, len, pat, plen, nreduce, out);
 }
 
 void mrg_parts_free(mrg_parts* p) {
@@ -913,7 +985,8 @@ static int aggregate(mrg_ctx* c, const std::vector<Recs>& srcs, int app, uint32_
     uint64_t tot = 0, longs = 0;
     for (const Recs& r : srcs) { tot += r.n; longs += r.n; }
     while ((1ull << c->sh_log2) < tot * 2) c->sh_log2++;
-    while ((1ull << c->lo_log2) < longs / 4 + 1024 && c->lo_log2 < 20) c->lo_log2++;
+    c->lo_log2_cur = 14;
+    while ((1ull << c->lo_log2_cur) < longs / 4 + 1024 && c->lo_log2_cur < 20) c->lo_log2_cur++;
     for (int attempt = 0; attempt < 8; attempt++) {
         if ((rc = ensure_tables(c))) return rc;
         Tables t = make_tables(c);
@@ -1192,6 +1265,49 @@ int mrg_parts_import_json(mrg_ctx* c, int app, uint32_t nreduce, const void* byt
     return rc;
 }
 
+// Every record of an intermediate buffer must be one the map could have
+// written: the reduce kernels index the arena and a 16-byte key buffer with
+// these fields, and place records by `part`.  Returns nullptr or what is wrong.
+static const char* validate_records(const IHdr& hd, const uint8_t* soa, uint64_t* bad) {
+    const uint64_t n = hd.n;
+    const uint8_t *pk0 = soa, *pk1 = pk0 + n * 8, *pcnt = pk1 + n * 8, *pkoff = pcnt + n * 8, *plen = pkoff + n * 8,
+                  *ppart = plen + n * 4, *arena = ppart + n * 4;
+    for (uint64_t i = 0; i < n; i++) {
+        *bad = i;
+        uint64_t k0, k1, cnt, koff;
+        uint32_t len, part;
+        memcpy(&k0, pk0 + 8 * i, 8);
+        memcpy(&k1, pk1 + 8 * i, 8);
+        memcpy(&cnt, pcnt + 8 * i, 8);
+        memcpy(&koff, pkoff + 8 * i, 8);
+        memcpy(&len, plen + 4 * i, 4);
+        memcpy(&part, ppart + 4 * i, 4);
+        if (part >= hd.nreduce) return "partition >= nreduce";
+        if (cnt == 0) return "zero count";
+        if (hd.app == MRG_APP_WC && len == 0) return "empty wc key";
+        uint8_t inl[16];
+        for (int k = 0; k < 8; k++) {
+            inl[k] = (uint8_t)(k0 >> (8 * k));
+            inl[8 + k] = (uint8_t)(k1 >> (8 * k));
+        }
+        const uint8_t* key = inl;
+        if (koff == ~0ull) {
+            if (len > 16) return "inline key longer than 16 bytes";
+            for (uint32_t k = len; k < 16; k++)
+                if (inl[k]) return "inline key bytes past its length";
+        } else {
+            if (koff > hd.arena_n || len > hd.arena_n - koff) return "key outside the arena";
+            key = arena + koff;
+            for (uint32_t k = 0; k < 16; k++)  // k0/k1 are the key's first 16 bytes, zero padded
+                if (inl[k] != (k < len ? key[k] : 0)) return "prefix words differ from the arena key";
+        }
+        uint32_t h = 2166136261u;
+        for (uint32_t k = 0; k < len; k++) h = fnv1a32_step(h, key[k]);
+        if ((h & 0x7fffffffu) % hd.nreduce != part) return "partition differs from ihash(key) % nreduce";
+    }
+    return nullptr;
+}
+
 int mrg_parts_import(mrg_ctx* c, const void* bytes, size_t nb, mrg_parts** out) {
     if (!c || !bytes || !out || nb < sizeof(IHdr)) return c ? fail(c, MRG_EFORMAT, "import: short buffer") : MRG_EINVAL;
     IHdr hd;
@@ -1199,7 +1315,11 @@ int mrg_parts_import(mrg_ctx* c, const void* bytes, size_t nb, mrg_parts** out) 
     if (hd.magic != kIMagic || (hd.app != MRG_APP_WC && hd.app != MRG_APP_GREP) || hd.nreduce == 0)
         return fail(c, MRG_EFORMAT, "import: bad header");
     const uint64_t n = hd.n;
-    if (sizeof(IHdr) + n * 40 + hd.arena_n != nb) return fail(c, MRG_EFORMAT, "import: size mismatch");
+    if (n > (nb - sizeof(IHdr)) / 40 || hd.arena_n > nb || sizeof(IHdr) + n * 40 + hd.arena_n != nb)
+        return fail(c, MRG_EFORMAT, "import: size mismatch");
+    uint64_t bad = 0;
+    if (const char* why = validate_records(hd, (const uint8_t*)bytes + sizeof(IHdr), &bad))
+        return fail(c, MRG_EFORMAT, "import: record %llu: %s", (unsigned long long)bad, why);
     int rc;
     if ((rc = bind(c))) return rc;
     mrg_parts* p = nullptr;
@@ -1299,13 +1419,30 @@ int mrg_comm_init(mrg_ctx* c, const uint8_t id[128], int nranks, int rank) {
 }
 
 // Wire record: the parts SoA of one destination, then its arena bytes.
-__global__ void owner_count_kernel(Recs r, uint32_t nranks, unsigned long long* cnt /*[2*nranks]*/) {
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+// Records are routed to owner rank part % nranks.  Per-owner counts and slots
+// come from LDS histograms, one device atomic per (workgroup, owner) per step:
+// a same-address device atomic per record serializes at the memory side
+// (~12 ns each, MI355X_MICROARCH.md fan-in row).  Arena bytes of a key are
+// padded to 16 so every key starts 16-byte aligned on the wire and is copied by
+// 16-byte stores.
+constexpr uint32_t kExchMaxRanks = 1024;
+constexpr int kExchThreads = 256;
+__host__ __device__ __forceinline__ uint64_t pad16(uint64_t x) { return (x + 15) & ~15ull; }
+
+__global__ void __launch_bounds__(kExchThreads) owner_count_kernel(Recs r, uint32_t nranks,
+                                                                   unsigned long long* cnt /*[2*nranks]*/) {
+    __shared__ unsigned long long h[2 * kExchMaxRanks];
+    for (uint32_t i = threadIdx.x; i < 2 * nranks; i += blockDim.x) h[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += stride) {
-        uint32_t o = r.part[i] % nranks;
-        atomicAdd(&cnt[2 * o], 1ull);
-        if (r.koff[i] != ~0ull) atomicAdd(&cnt[2 * o + 1], (unsigned long long)r.len[i]);
+        const uint32_t o = r.part[i] % nranks;
+        atomicAdd(&h[2 * o], 1ull);
+        if (r.koff[i] != ~0ull) atomicAdd(&h[2 * o + 1], (unsigned long long)pad16(r.len[i]));
     }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 2 * nranks; i += blockDim.x)
+        if (h[i]) atomicAdd(&cnt[i], h[i]);
 }
 
 // Pack into per-destination segments: records at rec_base[o] (AoS 40 B), arena at ar_base[o].
@@ -1314,36 +1451,72 @@ struct WireRec {
     uint32_t len, part;
 };
 
-__global__ void pack_kernel(Recs r, uint32_t nranks, const uint64_t* rec_base, const uint64_t* ar_base,
-                            unsigned long long* cur /*[2*nranks]*/, WireRec* wrec, uint8_t* war) {
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += stride) {
-        uint32_t o = r.part[i] % nranks;
-        unsigned long long slot = atomicAdd(&cur[2 * o], 1ull);
-        WireRec w{r.k0[i], r.k1[i], r.cnt[i], ~0ull, r.len[i], r.part[i]};
-        if (r.koff[i] != ~0ull) {
-            unsigned long long a = atomicAdd(&cur[2 * o + 1], (unsigned long long)r.len[i]);
-            for (uint32_t k = 0; k < r.len[i]; k++) war[ar_base[o] + a + k] = r.arena[r.koff[i] + k];
-            w.koff = a;  // relative to the destination's segment from this source
+__global__ void __launch_bounds__(kExchThreads) pack_kernel(Recs r, uint32_t nranks, const uint64_t* rec_base,
+                                                            const uint64_t* ar_base,
+                                                            unsigned long long* cur /*[2*nranks]*/, WireRec* wrec,
+                                                            uint8_t* war) {
+    __shared__ unsigned long long h[2 * kExchMaxRanks];     // this step's records / arena bytes per owner
+    __shared__ unsigned long long gbase[2 * kExchMaxRanks];  // their global slots
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t b0 = (uint64_t)blockIdx.x * blockDim.x; b0 < r.n; b0 += stride) {
+        for (uint32_t k = threadIdx.x; k < 2 * nranks; k += blockDim.x) h[k] = 0;
+        __syncthreads();
+        const uint64_t i = b0 + threadIdx.x;
+        const bool valid = i < r.n;
+        uint32_t o = 0;
+        unsigned long long slot = 0, aoff = 0;
+        uint64_t koff = ~0ull, alen = 0;
+        if (valid) {
+            o = r.part[i] % nranks;
+            koff = r.koff[i];
+            slot = atomicAdd(&h[2 * o], 1ull);
+            if (koff != ~0ull) {
+                alen = pad16(r.len[i]);
+                aoff = atomicAdd(&h[2 * o + 1], (unsigned long long)alen);
+            }
         }
-        wrec[rec_base[o] + slot] = w;
+        __syncthreads();
+        for (uint32_t k = threadIdx.x; k < 2 * nranks; k += blockDim.x) gbase[k] = h[k] ? atomicAdd(&cur[k], h[k]) : 0;
+        __syncthreads();
+        if (valid) {
+            WireRec w{r.k0[i], r.k1[i], r.cnt[i], ~0ull, r.len[i], r.part[i]};
+            if (koff != ~0ull) {
+                const unsigned long long a = gbase[2 * o + 1] + aoff;  // relative to owner o's segment from this source
+                uint4* dst = (uint4*)(war + ar_base[o] + a);           // 16-byte aligned (padded lengths)
+                const uint8_t* src = r.arena + koff;
+                const uint64_t len = r.len[i];
+                for (uint64_t q = 0; q < len; q += 16) {
+                    uint64_t lo, hi;
+                    load16u(src + q, len - q, lo, hi);
+                    dst[q >> 4] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+                }
+                w.koff = a;
+            }
+            wrec[rec_base[o] + gbase[2 * o] + slot] = w;
+        }
+        __syncthreads();  // h / gbase are reused by the next step
     }
 }
 
-// Unpack received wire records; koff rebased by the source's arena displacement.
+// Unpack received wire records; koff rebased by the source's arena displacement
+// (the source segment of record i by binary search over the P record offsets).
 __global__ void unpack_kernel(const WireRec* wrec, uint64_t n, const uint64_t* src_rec_begin, const uint64_t* src_ar_begin,
                               uint32_t nsrc, Recs r) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint32_t s = 0;
-        while (s + 1 < nsrc && src_rec_begin[s + 1] <= i) s++;
-        WireRec w = wrec[i];
+        uint32_t lo = 0, hi = nsrc - 1;  // last s with src_rec_begin[s] <= i
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi + 1) >> 1;
+            if (src_rec_begin[mid] <= i) lo = mid;
+            else hi = mid - 1;
+        }
+        const WireRec w = wrec[i];
         r.k0[i] = w.k0;
         r.k1[i] = w.k1;
         r.cnt[i] = w.cnt;
         r.len[i] = w.len;
         r.part[i] = w.part;
-        r.koff[i] = w.koff == ~0ull ? ~0ull : src_ar_begin[s] + w.koff;
+        r.koff[i] = w.koff == ~0ull ? ~0ull : src_ar_begin[lo] + w.koff;
     }
 }
 
@@ -1389,7 +1562,8 @@ static int exch_count(mrg_ctx* c, const Recs& r, int P, ExchSide& x) {
     size_t meta = sizeof(unsigned long long) * (8 * P + 8);
     HCHK(c, x.scratch.ensure(meta));
     HCHK(c, hipMemsetAsync(x.scratch.p, 0, meta, c->s));
-    if (r.n) owner_count_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, x.d_cnt(P));
+    if (P > (int)kExchMaxRanks) return fail(c, MRG_EINVAL, "exchange: more than %u ranks", kExchMaxRanks);
+    if (r.n) owner_count_kernel<<<1024, kExchThreads, 0, c->s>>>(r, (uint32_t)P, x.d_cnt(P));
     HCHK(c, hipGetLastError());
     return MRG_OK;
 }
@@ -1404,7 +1578,7 @@ static int exch_pack(mrg_ctx* c, const Recs& r, int P, ExchSide& x) {
     HCHK(c, x.rar_b.ensure_cached(x.plan.rar + 64, c->device));  // handed to the received parts object
     HCHK(c, hipMemcpyAsync(x.d_base(P), x.plan.hbase.data(), 16 * P, hipMemcpyHostToDevice, c->s));
     if (r.n)
-        pack_kernel<<<1024, 256, 0, c->s>>>(r, (uint32_t)P, x.d_base(P), x.d_base(P) + P, x.d_cur(P),
+        pack_kernel<<<1024, kExchThreads, 0, c->s>>>(r, (uint32_t)P, x.d_base(P), x.d_base(P) + P, x.d_cur(P),
                                              (WireRec*)x.sbuf.p, (uint8_t*)x.sar_b.p);
     HCHK(c, hipGetLastError());
     return MRG_OK;
@@ -1438,6 +1612,18 @@ static int exch_finish(mrg_ctx* c, const mrg_parts* local, int P, ExchSide& x, m
 
 static void exch_free(ExchSide* x) { delete x; }
 
+// Wire bytes to / from the OTHER ranks (the self segment is a local copy).
+static void exch_bytes(const ExchPlan& pl, int P, int me, mrg_stats* st) {
+    uint64_t snd = 0, rcv = 0;
+    for (int o = 0; o < P; o++) {
+        if (o == me) continue;
+        snd += pl.sc[o] + pl.asc[o];
+        rcv += pl.rc[o] + pl.arc[o];
+    }
+    st->shuffle_send_bytes = snd;
+    st->shuffle_recv_bytes = rcv;
+}
+
 int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     if (!c || !local || !owned) return MRG_EINVAL;
     int rc;
@@ -1466,6 +1652,7 @@ int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     HCHK(c, hipEventRecord(c->ev[7], c->s));
     rc = exch_finish(c, local, P, x, owned);
     c->stats.exchange_ms = ev_ms(c->ev[6], c->ev[7]);
+    exch_bytes(pl, P, c->rank, &c->stats);
     return rc;
 }
 
@@ -1544,6 +1731,7 @@ int mrg_exchange_group(mrg_ctx* const* ctxs, int P, const mrg_parts* const* loca
         if ((rc = bind(ctxs[j]))) return undo(rc);
         if ((rc = exch_finish(ctxs[j], local[j], P, xs[j], &owned[j]))) return undo(rc);
         ctxs[j]->stats.exchange_ms = ev_ms(ctxs[j]->ev[6], ctxs[j]->ev[7]);
+        exch_bytes(xs[j].plan, P, j, &ctxs[j]->stats);
     }
     return MRG_OK;
 }
@@ -1556,10 +1744,12 @@ int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, cons
     if (rc) return rc;
     mrg_stats keep = c->stats;
     mrg_parts* use = p;
-    if (c->comm && c->nranks > 1) {
+    if (c->comm && c->nranks > 1 && !c->skip_exchange) {
         mrg_parts* o = nullptr;
         rc = mrg_exchange(c, p, &o);
         keep.exchange_ms = c->stats.exchange_ms;
+        keep.shuffle_send_bytes = c->stats.shuffle_send_bytes;
+        keep.shuffle_recv_bytes = c->stats.shuffle_recv_bytes;
         mrg_parts_free(p);
         if (rc) return rc;
         use = o;

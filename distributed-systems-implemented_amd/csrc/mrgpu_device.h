@@ -255,6 +255,48 @@ __device__ __forceinline__ uint32_t short_partition(uint64_t k0, uint64_t k1, ui
     return (h & 0x7fffffffu) % nreduce;
 }
 
+// 16 bytes starting at p as two little-endian words; only the bytes before
+// p + avail are meaningful.  Reads the aligned 16-byte block holding p and the
+// next one only if bytes before p + avail lie in it (an aligned block never
+// crosses a page, so nothing past the buffer's last page is touched).
+__device__ __forceinline__ void load16u(const uint8_t* p, uint64_t avail, uint64_t& r0, uint64_t& r1) {
+    const uintptr_t a = (uintptr_t)p, ab = a & ~(uintptr_t)15;
+    uint32_t sh = (uint32_t)(a - ab);
+    const uint4 lo = *(const uint4*)ab;
+    uint4 hi = make_uint4(0, 0, 0, 0);
+    if (sh != 0 && avail > 16 - sh) hi = *(const uint4*)(ab + 16);
+    uint64_t q0 = ((uint64_t)lo.y << 32) | lo.x, q1 = ((uint64_t)lo.w << 32) | lo.z;
+    uint64_t q2 = ((uint64_t)hi.y << 32) | hi.x;
+    const uint64_t q3 = ((uint64_t)hi.w << 32) | hi.z;
+    if (sh >= 8) { q0 = q1; q1 = q2; q2 = q3; sh -= 8; }
+    if (sh) {
+        const uint32_t b = 8 * sh;
+        r0 = (q0 >> b) | (q1 << (64 - b));
+        r1 = (q1 >> b) | (q2 << (64 - b));
+    } else {
+        r0 = q0;
+        r1 = q1;
+    }
+}
+
+// len bytes at a == len bytes at b, 16 bytes per step (long keys, grep lines:
+// a chain of byte loads would cost a memory round trip per byte).
+__device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint64_t len) {
+    for (uint64_t k = 0; k < len; k += 16) {
+        const uint64_t left = len - k;
+        uint64_t a0, a1, b0, b1;
+        load16u(a + k, left, a0, a1);
+        load16u(b + k, left, b0, b1);
+        if (left < 16) {
+            const uint64_t m0 = left >= 8 ? ~0ull : (1ull << (8 * left)) - 1;
+            const uint64_t m1 = left <= 8 ? 0ull : (1ull << (8 * (left - 8))) - 1;
+            a0 &= m0; b0 &= m0; a1 &= m1; b1 &= m1;
+        }
+        if (a0 != b0 || a1 != b1) return false;
+    }
+    return true;
+}
+
 // ------------------------------------------------------- HBM table inserts
 // Lock-free insert of a short key.  Claim = CAS on k0 (0 -> key); the claimer
 // then publishes k1.  A prober that matches k0 before k1 is visible never waits
@@ -345,10 +387,7 @@ __device__ inline int long_try(const Tables& t, uint64_t h, const uint8_t* rep, 
             const uint64_t lp1 = ld_agent(&s->len);
             if (r == nullptr || lp1 == 0) return kRetry;
             if (lp1 == len + 1) {
-                bool eq = true;
-                for (uint64_t k = 0; k < len; k++)
-                    if (r[k] != rep[k]) { eq = false; break; }
-                if (eq) {
+                if (bytes_equal(r, rep, len)) {
                     atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
                     return kDone;
                 }

@@ -58,6 +58,8 @@ struct Counters {
     unsigned long long dict_hits;  // occurrences counted by the hot-key dictionary
     unsigned long long carried;    // aggregator misses carried to the next round
     unsigned long long round_mask; // bit r: aggregation round r had input
+    unsigned long long nlines;     // grep: matching line occurrences resolved (one per line, not per hit)
+    unsigned long long ndefer;     // grep: hits whose line bounds lie beyond a lane's scan window
     unsigned long long pad[1];
 };
 
@@ -129,6 +131,11 @@ struct Tables {
     uint64_t lo_mask;
     uint64_t* list;      // u64 offsets (long-word starts / grep match positions)
     uint64_t list_cap;
+    // grep line resolution: hits sorted by position; resolved lines as (start,
+    // end) pairs; hits handed to the workgroup-wide scan (indices into hits)
+    const uint64_t* hits;
+    uint64_t* lines;
+    uint64_t* defer;
     Counters* ctr;
     Spill sp;
     // wc record output: dict_emit / wc_agg (direct) / collect append at ctr->nrec
@@ -172,7 +179,17 @@ void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t 
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
                      hipStream_t s);
-void launch_grep_lines(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nlist, hipStream_t s);
+// grep line resolution, linear in the input (mrgpu_map.hip): t.hits (sorted) ->
+// one (start, end) pair per matching line occurrence in t.lines (ctr->nlines),
+// hits in lines longer than a lane's scan window to t.defer (ctr->ndefer).
+void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, hipStream_t s);
+// The deferred hits, one workgroup each (wide coalesced scans).
+void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t ndefer,
+                              uint64_t nhits, hipStream_t s);
+// t.lines -> the LongTable (one distinct line = one slot).
+void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, hipStream_t s);
+// Clear the LongTable and its fill counters (a re-run of launch_grep_insert after growth).
+void clear_long_table(const Tables& t, hipStream_t s);
 void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int grid, hipStream_t s);
 struct ReduceWs;
 // Append the HBM tables' keys to t.out: the ShortTable's `short_used` keys at
@@ -193,6 +210,8 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
 // Indices of occupied ShortTable slots; *d_count (device) = how many.
 int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64_t max_used, uint32_t** d_idx,
                       uint32_t** d_count, hipStream_t s);
+// Radix sort of u64 keys (the low `bits` bits); result in k_out.
+int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s);
 // Stable radix sort of (u32 key, u32 value) pairs; result in k_out / v_out.
 int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, uint64_t n,
                    unsigned bits, hipStream_t s);

@@ -7,6 +7,8 @@
 //   start, counted in the LongTable.
 // collect: the HBM tables' distinct keys -> records with partition =
 //   ihash(key) % nReduce (mr/worker.go:33-37,76), appended at ctr->nrec.
+#include <climits>
+
 #include "mrgpu_device.h"
 
 namespace mrg {
@@ -30,7 +32,7 @@ __global__ void wc_long_kernel(const uint8_t* __restrict__ in, uint64_t n, Table
 
 // ------------------------------------------------------------ grep kernels
 // Pattern occurrence search.  Every occurrence start p (with p + plen <= n) is
-// appended to the list; grep_lines_kernel resolves its line.
+// appended to the list; grep_resolve_kernel resolves its line.
 __device__ __forceinline__ uint32_t eq_mask16(uint4 v, uint32_t rep) {
     // exact per-byte equality with the broadcast byte (no borrow false positives)
     uint32_t m = 0;
@@ -76,6 +78,36 @@ __device__ __forceinline__ void grep_dma(const uint8_t* in, uint64_t n, uint64_t
     lds_base = __builtin_amdgcn_readfirstlane(lds_base);
     asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rs), "s"(lds_base)
                  : "memory", "m0");
+}
+
+// Of a chunk's occurrences (lane l: 16-bit masks `hit` and `nl` ('\n') of its
+// 16 bytes), keep the first of each line: an occurrence is dropped when an
+// earlier one of the chunk has no '\n' between them (the pattern holds no
+// '\n').  The last occurrence / newline of the lanes below come from a wave
+// prefix max.
+__device__ uint32_t first_hit_per_line(uint32_t hit, uint32_t nl, uint32_t lane) {
+    int lh = hit ? (int)(16 * lane + 31 - __builtin_clz(hit)) : -1;
+    int ln = nl ? (int)(16 * lane + 31 - __builtin_clz(nl)) : -1;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {  // inclusive prefix max
+        const int a = __shfl_up(lh, off), b = __shfl_up(ln, off);
+        if (lane >= (uint32_t)off) {
+            lh = max(lh, a);
+            ln = max(ln, b);
+        }
+    }
+    int ph = __shfl_up(lh, 1), pn = __shfl_up(ln, 1);  // exclusive: the lanes below
+    if (lane == 0) ph = pn = -1;
+    bool open = ph > pn;  // the line this lane starts in already has an occurrence
+    uint32_t keep = 0;
+    for (int b = 0; b < 16; b++) {
+        if ((nl >> b) & 1u) open = false;
+        if ((hit >> b) & 1u) {
+            if (!open) keep |= 1u << b;
+            open = true;
+        }
+    }
+    return keep;
 }
 
 __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
@@ -134,7 +166,8 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
             const uint32_t nb = (uint32_t)__shfl_down((int)(m1 & 1u), 1);  // next lane's byte 0 (lane 59 -> 60: look-ahead)
             m &= (m1 >> 1) | (nb << 15);
         }
-        bool any = false;
+        bool any = false;  // a rare path issued other VMEM instructions: drain before the next DMA wait
+        uint32_t vm = 0;   // verified occurrences starting in this lane's bytes
         while (m) {
             const uint32_t bit = __builtin_ctz(m);
             m &= m - 1;
@@ -150,15 +183,25 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
                     if (in[pos + q] != pat[q]) { ok = false; break; }
                 any = true;
             }
-            if (ok) {
-                const uint32_t at_m = __hip_atomic_fetch_add(wcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (at_m < (uint32_t)kGrepBuf) {
-                    mbuf[wv][at_m] = pos;
-                } else {  // buffer full inside one chunk (pathological): append directly
-                    __hip_atomic_fetch_add(wcnt, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    list_append(t, pos);
-                    any = true;
-                }
+            if (ok) vm |= 1u << bit;
+        }
+        // Only the first occurrence of each line within the chunk goes on: later
+        // ones name the same line (a line with k occurrences would otherwise be
+        // resolved k times).  Rare in text, so only chunks with two or more pay.
+        const uint64_t lanes_hit = __ballot(vm != 0);
+        if ((lanes_hit & (lanes_hit - 1)) != 0 || __ballot((vm & (vm - 1)) != 0) != 0)
+            vm = first_hit_per_line(vm, eq_mask16(v, 0x0A0A0A0Au), lane);
+        while (vm) {
+            const uint32_t bit = __builtin_ctz(vm);
+            vm &= vm - 1;
+            const uint64_t pos = cs + 16 * lane + bit;
+            const uint32_t at_m = __hip_atomic_fetch_add(wcnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (at_m < (uint32_t)kGrepBuf) {
+                mbuf[wv][at_m] = pos;
+            } else {  // buffer full inside one chunk (pathological): append directly
+                __hip_atomic_fetch_add(wcnt, ~0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                list_append(t, pos);
+                any = true;
             }
         }
         if (__ballot(any)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rare paths: drain
@@ -208,53 +251,204 @@ __device__ __forceinline__ bool long_try_insert_counted(const Tables& t, uint64_
     return claimed;
 }
 
-// Resolve the line of each hit: [last '\n' before p]+1 .. next '\n' at/after p,
-// one lane per hit.  plen == 0 means the list already holds line starts.  The
-// lines sit in HBM at random offsets, so the kernel is bound by memory-level
-// parallelism: a lane per hit keeps 64 independent misses in flight per wave
-// (measured: a wave per hit, with coalesced 64-byte steps, took 2.3 ms more on
-// C3), and each boundary-scan and hash step is one 16-byte load (byte loads:
-// 1.4 ms more).  The table's fill counters are added once per wave.
-__global__ void __launch_bounds__(256) grep_lines_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen, Tables t,
-                                                              uint64_t nlist) {
+// ------------------------------------------------------------ grep lines
+// Line resolution, linear in the input.  The hits are sorted by position.  Hit
+// i's line starts after the last '\n' before it; if there is none between the
+// previous hit and this one, both lie in one line and hit i is dropped.  So
+// the backward scans cover disjoint byte ranges (each at most up to the
+// previous hit), only the first hit of a line scans forward to its end, and
+// the lines are hashed once per occurrence of the line.  A lane scans at most
+// kLineScan bytes each way; a hit whose bounds lie further (long lines) goes
+// to grep_resolve_long_kernel, one workgroup per hit with coalesced 4 KiB
+// steps.  The lines sit at random HBM offsets, so this is bound by
+// memory-level parallelism: a lane per hit keeps 64 independent misses in
+// flight per wave, each step one aligned 16-byte load.
+constexpr int64_t kLineScan = 4096;
+
+// Position of the last '\n' in [lo, p), scanning down from p: -1 if there is
+// none, -2 if none within kLineScan bytes.
+__device__ int64_t last_nl_before(const uint8_t* in, int64_t lo, int64_t p) {
+    int64_t q = p;
+    while (q > lo) {
+        if (p - q >= kLineScan) return -2;
+        int64_t bi;
+        const uint4 v = block16(in, q - 1, bi);
+        uint32_t m = eq_mask16(v, 0x0A0A0A0Au) & ((2u << (uint32_t)(q - 1 - bi)) - 1u);  // bytes < q
+        if (bi < lo) m &= ~((1u << (uint32_t)(lo - bi)) - 1u);                            // bytes >= lo
+        if (m) return bi + 31 - __builtin_clz(m);
+        q = bi;
+    }
+    return -1;
+}
+
+// Position of the first '\n' in [q0, n): n if there is none, -2 if none within
+// kLineScan bytes.
+__device__ int64_t first_nl_from(const uint8_t* in, int64_t n, int64_t q0) {
+    for (int64_t q = q0; q < n;) {
+        if (q - q0 >= kLineScan) return -2;
+        int64_t bi;
+        const uint4 v = block16(in, q, bi);
+        uint32_t m = eq_mask16(v, 0x0A0A0A0Au) & ~((1u << (uint32_t)(q - bi)) - 1u);
+        if (n - bi < 16) m &= (1u << (uint32_t)(n - bi)) - 1u;
+        if (m) return bi + __builtin_ctz(m);
+        q = bi + 16;
+    }
+    return n;
+}
+
+// Append the (s, e) line pairs and deferred hit indices of a wave (one cursor
+// atomic each per wave).
+__device__ __forceinline__ void put_line(const Tables& t, uint64_t cap, bool keep, uint64_t s, uint64_t e, bool defer,
+                                         uint64_t i) {
+    const unsigned long long o = wave_alloc(&t.ctr->nlines, keep);
+    if (keep) {
+        if (o < cap) {
+            t.lines[2 * o] = s;
+            t.lines[2 * o + 1] = e;
+        } else {
+            set_status(t.ctr, kStListFull);
+        }
+    }
+    const unsigned long long d = wave_alloc(&t.ctr->ndefer, defer);
+    if (defer) {
+        if (d < cap) t.defer[d] = i;
+        else set_status(t.ctr, kStListFull);
+    }
+}
+
+// One lane per hit.  plen == 0: the hits are line starts (empty pattern).
+__global__ void __launch_bounds__(256) grep_resolve_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
+                                                           Tables t, uint64_t nhits) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool keep = false, defer = false;
+    int64_t s = 0, e = 0;
+    if (i < nhits) {
+        const int64_t p = (int64_t)t.hits[i];
+        if (plen == 0) {
+            s = p;
+            keep = true;
+        } else {
+            const int64_t lo = i == 0 ? 0 : (int64_t)t.hits[i - 1] + 1;
+            const int64_t q = last_nl_before(in, lo, p);
+            if (q == -2) defer = true;
+            else if (q >= 0) { s = q + 1; keep = true; }
+            else if (i == 0) { s = 0; keep = true; }  // no '\n' before the split's first hit
+            // else: no '\n' since the previous hit, which named this line already
+        }
+        if (keep) {
+            e = first_nl_from(in, (int64_t)n, p + plen);
+            if (e == -2) { keep = false; defer = true; }
+        }
+    }
+    put_line(t, nhits, keep, (uint64_t)s, (uint64_t)e, defer, i);
+}
+
+// Deferred hits: one 256-thread workgroup each, 16 bytes per lane per step
+// (4 KiB steps of aligned blocks), block-wide max / min of the newline found.
+__global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
+                                                                Tables t, uint64_t ndefer, uint64_t cap) {
+    __shared__ long long red[4];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const uintptr_t base = (uintptr_t)in;
+    auto block_max = [&](long long v) -> long long {
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v = max(v, (long long)__shfl_xor(v, off));
+        if (lane == 0) red[wv] = v;
+        __syncthreads();
+        v = max(max(red[0], red[1]), max(red[2], red[3]));
+        __syncthreads();
+        return v;
+    };
+    for (uint64_t d = blockIdx.x; d < ndefer; d += gridDim.x) {
+        const uint64_t i = t.defer[d];
+        const int64_t p = (int64_t)t.hits[i];
+        int64_t s = p;
+        bool keep = true;
+        if (plen != 0) {
+            const int64_t lo = i == 0 ? 0 : (int64_t)t.hits[i - 1] + 1;
+            // aligned blocks from the one holding p - 1 downwards: block k starts at
+            // input offset top - 16 k
+            const int64_t top = (int64_t)(((base + (uint64_t)p - 1) & ~(uintptr_t)15) - base);
+            long long found = -1;
+            for (int64_t step = 0; found < 0; step++) {
+                const int64_t bo = top - 16 * (256 * step + (int64_t)tid);  // this lane's block
+                const int64_t hi_end = top - 16 * 256 * step + 16;          // first block of the step ends here
+                if (hi_end <= lo) break;
+                long long mine = -1;
+                if (bo + 16 > lo && bo < p) {
+                    const uint4 v = *(const uint4*)(in + bo);
+                    uint32_t m = eq_mask16(v, 0x0A0A0A0Au);
+                    for (int b = 15; b >= 0; b--)
+                        if (((m >> b) & 1u) && bo + b >= lo && bo + b < p) { mine = bo + b; break; }
+                }
+                found = block_max(mine);
+            }
+            if (found >= 0) s = found + 1;
+            else if (i == 0) s = 0;
+            else keep = false;
+        }
+        int64_t e = (int64_t)n;
+        if (keep) {
+            const int64_t q0 = p + plen;
+            const int64_t first = (int64_t)((base + (uint64_t)q0) & ~(uintptr_t)15) - (int64_t)base;
+            for (int64_t step = 0;; step++) {
+                const int64_t bo = first + 16 * (256 * step + (int64_t)tid);
+                if (first + 16 * 256 * step >= (int64_t)n) break;
+                long long mine = LLONG_MAX;
+                if (bo < (int64_t)n && bo + 16 > q0) {
+                    const uint4 v = *(const uint4*)(in + bo);
+                    uint32_t m = eq_mask16(v, 0x0A0A0A0Au);
+                    for (int b = 0; b < 16; b++)
+                        if (((m >> b) & 1u) && bo + b >= q0 && bo + b < (int64_t)n) { mine = bo + b; break; }
+                }
+                const long long f = -block_max(-mine);
+                if (f != LLONG_MAX) { e = f; break; }
+            }
+        }
+        if (tid == 0 && keep) {
+            const unsigned long long o = atomicAdd(&t.ctr->nlines, 1ull);
+            if (o < cap) {
+                t.lines[2 * o] = (uint64_t)s;
+                t.lines[2 * o + 1] = (uint64_t)e;
+            } else {
+                set_status(t.ctr, kStListFull);
+            }
+        }
+    }
+}
+
+// Line content hash for the LongTable: FNV-1a-64 of every byte, or for a line
+// longer than kHashAll of its first and last kHashEdge bytes and its length
+// (equal lines hash equally, and slot matches are confirmed bytewise anyway).
+constexpr uint64_t kHashAll = 8192, kHashEdge = 2048;
+__device__ uint64_t hash_bytes(const uint8_t* in, int64_t s, int64_t e, uint64_t h) {
+    for (int64_t q = s; q < e;) {
+        int64_t bi;
+        const uint4 v = block16(in, q, bi);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            if (bi + j >= q && bi + j < e) h = fnv1a64_step(h, (w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+        q = bi + 16;
+    }
+    return h;
+}
+
+__global__ void __launch_bounds__(256) grep_insert_kernel(const uint8_t* __restrict__ in, Tables t, uint64_t nlines) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool claimed = false;
     uint64_t len = 0;
-    if (i < nlist) {
-        const int64_t p = (int64_t)t.list[i];
-        int64_t s = p;
-        if (plen > 0) {
-            int64_t q = p;  // the last '\n' before q
-            s = 0;
-            while (q > 0) {
-                int64_t bi;
-                const uint4 v = block16(in, q - 1, bi);
-                uint32_t m = eq_mask16(v, 0x0A0A0A0Au) & ((2u << (uint32_t)(q - 1 - bi)) - 1u);
-                if (bi < 0) m &= ~((1u << (uint32_t)(-bi)) - 1u);
-                if (m) { s = bi + (31 - __builtin_clz(m)) + 1; break; }
-                q = bi;
-            }
-        }
-        int64_t e = (int64_t)n;
-        for (int64_t q = p; q < (int64_t)n;) {  // the first '\n' at or after p
-            int64_t bi;
-            const uint4 v = block16(in, q, bi);
-            uint32_t m = eq_mask16(v, 0x0A0A0A0Au) & ~((1u << (uint32_t)(q - bi)) - 1u);
-            if ((int64_t)n - bi < 16) m &= (1u << (uint32_t)((int64_t)n - bi)) - 1u;
-            if (m) { e = bi + __builtin_ctz(m); break; }
-            q = bi + 16;
-        }
-        uint64_t h = kFnv64Off;
-        for (int64_t q = s; q < e;) {
-            int64_t bi;
-            const uint4 v = block16(in, q, bi);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-            for (int j = 0; j < 16; j++)
-                if (bi + j >= q && bi + j < e) h = fnv1a64_step(h, (w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-            q = bi + 16;
-        }
+    if (i < nlines) {
+        const int64_t s = (int64_t)t.lines[2 * i], e = (int64_t)t.lines[2 * i + 1];
         len = (uint64_t)(e - s);
+        uint64_t h;
+        if (len <= kHashAll) {
+            h = hash_bytes(in, s, e, kFnv64Off);
+        } else {
+            h = hash_bytes(in, s, s + (int64_t)kHashEdge, kFnv64Off);
+            h = hash_bytes(in, e - (int64_t)kHashEdge, e, h);
+            h = fnv1a64_step(h ^ len, 0xA5u);
+        }
         claimed = long_try_insert_counted(t, h, in + s, len);
     }
     // fill counters once per wave (same-address device atomics serialize)
@@ -406,6 +600,19 @@ int map_grid_size(int device) {
     return ncu;  // one 1024-thread workgroup per CU (LDS-bound), persistent over chunks
 }
 
+__global__ void clear_long_kernel(Tables t) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t i = i0; i <= t.lo_mask; i += stride) t.lo[i] = LongSlot{0, nullptr, 0, 0};
+    if (i0 == 0) {
+        t.ctr->status = 0;
+        t.ctr->long_used = 0;
+        t.ctr->long_bytes = 0;
+    }
+}
+
+void clear_long_table(const Tables& t, hipStream_t s) { clear_long_kernel<<<2048, 256, 0, s>>>(t); }
+
 void clear_tables(const Tables& t, bool short_table, hipStream_t s) {
     hipMemsetAsync(t.ctr, 0, sizeof(Counters), s);
     if (t.bflag) hipMemsetAsync(t.bflag, 0, kSpillBuckets * sizeof(uint32_t), s);
@@ -433,10 +640,21 @@ void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int g
     grep_all_lines_kernel<<<grid * 4, 256, 0, s>>>(in, n, t);
 }
 
-void launch_grep_lines(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nlist, hipStream_t s) {
-    if (nlist == 0) return;
-    // one wave per hit, 4 per workgroup; at most 64 K workgroups, each wave then strides
-    grep_lines_kernel<<<(unsigned)((nlist + 255) / 256), 256, 0, s>>>(in, n, plen, t, nlist);
+void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, hipStream_t s) {
+    if (nhits == 0) return;
+    grep_resolve_kernel<<<(unsigned)((nhits + 255) / 256), 256, 0, s>>>(in, n, plen, t, nhits);
+}
+
+void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t ndefer,
+                              uint64_t nhits, hipStream_t s) {
+    if (ndefer == 0) return;
+    const uint64_t g = ndefer < 4096 ? ndefer : 4096;
+    grep_resolve_long_kernel<<<(unsigned)g, 256, 0, s>>>(in, n, plen, t, ndefer, nhits);
+}
+
+void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, hipStream_t s) {
+    if (nlines == 0) return;
+    grep_insert_kernel<<<(unsigned)((nlines + 255) / 256), 256, 0, s>>>(in, t, nlines);
 }
 
 int launch_collect(const Tables& t, ReduceWs* ws, uint64_t base, uint64_t short_used, bool long_table, hipStream_t s) {

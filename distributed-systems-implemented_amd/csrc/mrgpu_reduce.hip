@@ -18,7 +18,7 @@
 #include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
-#include "mrgpu_internal.h"
+#include "mrgpu_device.h"
 
 namespace mrg {
 
@@ -353,11 +353,16 @@ __global__ void part_offsets_kernel(Recs r, const uint32_t* perm, uint64_t n, co
     offsets[p] = lo < n ? off[lo] : total;
 }
 
+// Records of one partition (or owner): one cursor atomic per wave (wave_alloc),
+// not per record (same-address device atomics serialize).  The loop bound is
+// wave-uniform, so every lane reaches the ballot.
 __global__ void select_kernel(Recs src, uint32_t mod, uint32_t want, Recs dst, unsigned long long* cnt) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < src.n; i += stride) {
-        if (src.part[i] % mod != want) continue;
-        unsigned long long o = atomicAdd(cnt, 1ull);
+    for (uint64_t b = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); b < src.n; b += stride) {
+        const uint64_t i = b + (threadIdx.x & 63u);
+        const bool take = i < src.n && src.part[i] % mod == want;
+        const unsigned long long o = wave_alloc(cnt, take);
+        if (!take) continue;
         dst.k0[o] = src.k0[i];
         dst.k1[o] = src.k1[i];
         dst.len[o] = src.len[i];
@@ -414,6 +419,14 @@ int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64
     RCHK(rocprim::select(nullptr, tb, first, *d_idx, *d_count, (size_t)nslots, ShortUsed{sh}, s));
     RCHK(ws->tmp.ensure(tb));
     RCHK(rocprim::select(ws->tmp.p, tb, first, *d_idx, *d_count, (size_t)nslots, ShortUsed{sh}, s));
+    return 0;
+}
+
+int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s) {
+    size_t tb = 0;
+    RCHK(rocprim::radix_sort_keys<OnesweepCfg>(nullptr, tb, k_in, k_out, (size_t)n, 0u, bits, s));
+    RCHK(ws->tmp.ensure(tb));
+    RCHK(rocprim::radix_sort_keys<OnesweepCfg>(ws->tmp.p, tb, k_in, k_out, (size_t)n, 0u, bits, s));
     return 0;
 }
 

@@ -116,13 +116,116 @@ def grep_params(pattern: bytes = b"distributed", match_rate: float = 0.005, dup_
     return Params(MODE_GREP, 0.0, pattern, match_rate, dup_rate, line_min, line_max, 0, 0)
 
 
+C1_SIZES_ = [100_000, 180_000, 250_000, 320_000, 400_000, 470_000, 530_000, 600_000]
+
 # SURVEY.md §8d presets: (kind, s, V, vocab seed, file size, n files, params factory)
 CONFIGS = {
-    "C1": dict(kind=KIND_ASCII, s=1.07, V=20000, seed=1, file_sizes=[100_000, 180_000, 250_000, 320_000,
-                                                                      400_000, 470_000, 530_000, 600_000],
-               params=lambda: wc_params(), app="wc", nreduce=10),
+    # C1 is English-like prose from c1_files() (Gutenberg substitute), not the Zipf generator
+    "C1": dict(generator="c1_files", seed=1, file_sizes=C1_SIZES_, app="wc", nreduce=10),
     "C2": dict(kind=KIND_ASCII, s=1.07, V=10**6, seed=2, file_sizes=[250_000_000] * 40,
                params=lambda: wc_params(), app="wc", nreduce=10),
     "C3": dict(kind=KIND_UTF8, s=1.07, V=10**6, seed=3, file_sizes=[250_000_000] * 40,
                params=lambda: grep_params(), app="grep", pattern=b"distributed", nreduce=10),
 }
+
+
+# ---------------------------------------------------------------- C1 substitute corpus
+# the reference runs mrsequential + wc on the Gutenberg texts
+# pg-*.txt (main/test-mr.sh:30), which it does not bundle (.gitignore:36).  The
+# substitute: 8 files of 0.1-0.6 MB of English-like ASCII prose, seed 1 —
+# Gutenberg-style header, chapter headings with roman and arabic numerals,
+# paragraphs wrapped at ~70 columns with CRLF line ends, sentences with commas,
+# quotes, apostrophes, hyphens, digits and dates.  Pure function of the seed
+# (tests/golden/c1_manifest.json pins every file's SHA-256).
+_C1_WORDS = (
+    "the of and to a in that he was it his i with as had for you not be her on at by which this she all they "
+    "have from my but or were him so one there would me their said we been what if when more no out up into "
+    "an man could them do time some very upon then little about now only than like over any before such "
+    "other great made well down two may should these first see must much day good our your after old know "
+    "us shall never way long through came how mr its most where himself without come again those can life "
+    "own think house thought hand head room nothing eyes went yet under young every night mind while face "
+    "place last work away door something still against heart many same take father mother moment found "
+    "left began voice people world things let even done light side round being thing home looked tell "
+    "once whole both felt night years better part say might quite just morning another each whom country "
+    "lady letter water town street river window friend answer captain question king book family evening "
+    "don't can't won't it's I'm she's we'll they'd o'clock well-known half-past to-morrow good-bye"
+).split()
+_C1_NAMES = ("Elizabeth Darcy Bennet Holmes Watson Pip Estella Jane Rochester Ahab Ishmael Alice Hatter Jekyll Hyde "
+             "Dorian Basil Emma Knightley Catherine Heathcliff Marianne Elinor Oliver Fagin Sherlock Moriarty").split()
+_ROMAN = ["I", "II", "III", "IV", "V", "VI", "VII", "VIII", "IX", "X", "XI", "XII", "XIII", "XIV", "XV", "XVI",
+          "XVII", "XVIII", "XIX", "XX", "XXI", "XXII", "XXIII", "XXIV", "XXV"]
+C1_SIZES = C1_SIZES_
+
+
+def _c1_file(rnd, size: int, idx: int) -> bytes:
+    import math
+    words = _C1_WORDS
+    w = [1.0 / math.pow(k + 1, 1.0) for k in range(len(words))]
+    tot = sum(w)
+    cum, acc = [], 0.0
+    for x in w:
+        acc += x / tot
+        cum.append(acc)
+
+    def word():
+        u = rnd.random()
+        if u < 0.04:
+            return rnd.choice(_C1_NAMES)
+        if u < 0.05:
+            return str(rnd.randint(1, 1900))
+        v = rnd.random()
+        lo, hi = 0, len(cum) - 1
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if cum[mid] < v:
+                lo = mid + 1
+            else:
+                hi = mid
+        return words[lo]
+
+    def sentence():
+        n = rnd.randint(4, 24)
+        ws = [word() for _ in range(n)]
+        ws[0] = ws[0][:1].upper() + ws[0][1:]
+        for k in range(1, n - 1):
+            if rnd.random() < 0.08:
+                ws[k] += rnd.choice([",", ",", ";", ":", " --"])
+        s = " ".join(ws) + rnd.choice([".", ".", ".", "!", "?"])
+        if rnd.random() < 0.15:
+            s = '"' + s + '"'
+        return s
+
+    def wrap(par: str) -> str:
+        lines, cur = [], ""
+        for tok in par.split(" "):
+            if cur and len(cur) + 1 + len(tok) > 70:
+                lines.append(cur)
+                cur = tok
+            else:
+                cur = tok if not cur else cur + " " + tok
+        if cur:
+            lines.append(cur)
+        return "\r\n".join(lines)
+
+    out = [f"The Project Gutenberg-style EBook #{1000 + idx} (synthetic substitute text, seed 1)\r\n\r\n"
+           f"Title: A Tale of {rnd.choice(_C1_NAMES)} and {rnd.choice(_C1_NAMES)}\r\n"
+           f"Release Date: {rnd.choice(['May', 'June', 'August'])} {rnd.randint(1, 28)}, {rnd.randint(1994, 2012)}"
+           f" [EBook #{1000 + idx}]\r\n\r\n*** START OF THIS SYNTHETIC EBOOK ***\r\n\r\n"]
+    n, chap = len(out[0]), 0
+    while n < size:
+        if rnd.random() < 0.03 or chap == 0:
+            chap += 1
+            t = f"\r\n\r\nCHAPTER {_ROMAN[(chap - 1) % len(_ROMAN)]}. ({chap})\r\n\r\n"
+        else:
+            t = wrap(" ".join(sentence() for _ in range(rnd.randint(2, 8)))) + "\r\n\r\n"
+        out.append(t)
+        n += len(t)
+    data = "".join(out).encode("ascii")[:size - 2] + b"\r\n"
+    return data
+
+
+def c1_files(seed: int = 1) -> list[bytes]:
+    """The C1 substitute corpus: 8 files, C1_SIZES bytes each, ending in CRLF."""
+    import random
+    rnd = random.Random(seed)
+    return [_c1_file(rnd, sz, i) for i, sz in enumerate(C1_SIZES)]

@@ -70,6 +70,9 @@ class Stats(ctypes.Structure):
         ("dict_keys", c_uint64),
         ("dict_hits", c_uint64),
         ("agg_rounds", c_uint64),
+        ("shuffle_send_bytes", c_uint64),
+        ("shuffle_recv_bytes", c_uint64),
+        ("staged_bytes", c_uint64),
     ]
 
     def as_dict(self):

@@ -17,9 +17,9 @@ import sys
 def load(d, separate=False):
     per = collections.defaultdict(lambda: collections.defaultdict(float))
     names = {}
-    for f in glob.glob(os.path.join(d, "*_counter_collection.csv")):
+    for f in glob.glob(os.path.join(d, "**", "*_counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            key = (os.path.basename(f), r["Dispatch_Id"])
+            key = (f, r["Dispatch_Id"])
             names[key] = r["Kernel_Name"].split("(")[0]
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
     out = collections.defaultdict(lambda: collections.defaultdict(list))

@@ -87,6 +87,10 @@ typedef struct {
     uint64_t dict_keys;       /* wc: sample keys offered to the dictionary */
     uint64_t dict_hits;       /* wc: occurrences counted by the dictionary in LDS */
     uint64_t agg_rounds;      /* wc: bucket aggregation rounds run (high-cardinality splits need > 1) */
+    uint64_t shuffle_send_bytes; /* exchange: wire bytes this rank sent to OTHER ranks (records + arena) */
+    uint64_t shuffle_recv_bytes; /* exchange: wire bytes this rank received from other ranks */
+    uint64_t staged_bytes;    /* map: bytes copied into the context's staging buffer first (host input,
+                                 or a device pointer not 16-byte aligned) */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);
@@ -96,7 +100,11 @@ int mrg_device_count(int* n);
 
 /* Map one input split (one file = one map task).  app = MRG_APP_WC or MRG_APP_GREP
  * (pat/plen = the literal; ignored for wc).  Output: device-resident partial
- * aggregates (distinct key, count, partition) for all nreduce partitions. */
+ * aggregates (distinct key, count, partition) for all nreduce partitions.
+ * grep: the pattern is a literal (regexp.QuoteMeta semantics).  dgrep.go:20-23
+ * returns no lines when regexp.Compile fails, which for a literal happens
+ * exactly when it is not valid UTF-8: such a pattern maps to no lines, as does
+ * one holding '\n' (no line of strings.Split(contents, "\n") contains it). */
 int mrg_map(mrg_ctx* ctx, int app, const void* buf, size_t len, int input_kind, const uint8_t* pat,
             size_t plen, uint32_t nreduce, mrg_parts** out);
 /* Combine `from` into `into` (both on ctx's device, same app and nreduce). */
@@ -105,6 +113,10 @@ int mrg_parts_merge(mrg_ctx* ctx, mrg_parts* into, const mrg_parts* from);
 int mrg_parts_info(const mrg_parts* p, uint64_t* nkeys, uint32_t* nreduce, int* app);
 /* Serialize partition r (r = UINT32_MAX: all) to library-owned host bytes. */
 int mrg_parts_export(mrg_ctx* ctx, const mrg_parts* p, uint32_t r, void** bytes, size_t* n);
+/* Deserialize an mrg_parts_export buffer.  Every record is checked on the host
+ * before it reaches the device (partition < nreduce and = ihash(key) % nreduce,
+ * inline keys <= 16 bytes, arena keys inside the arena, prefix words equal to
+ * the key's first bytes, counts >= 1): anything else is MRG_EFORMAT. */
 int mrg_parts_import(mrg_ctx* ctx, const void* bytes, size_t n, mrg_parts** out);
 void mrg_parts_free(mrg_parts* p);
 /* The reference's own intermediate format, for mixed clusters of GPU and

@@ -122,8 +122,24 @@ def grep_map(contents: bytes, pattern: bytes) -> list[bytes]:
     trailing newline; a line is emitted (once per line) when the literal occurs
     in it.  For a valid-UTF-8 literal, Go's regexp match equals a byte-substring
     test; the empty pattern matches every line.
+    dgrep.go:20-23: when ``regexp.Compile`` fails grepMap returns nil — for a
+    quoted literal that is exactly an invalid-UTF-8 pattern (regexp/syntax
+    rejects it with ErrInvalidUTF8).
     """
+    if not valid_utf8(pattern):
+        return []
     return [line for line in contents.split(b"\n") if pattern in line]
+
+
+def valid_utf8(b: bytes) -> bool:
+    """Go's utf8.Valid: every rune decodes with width > 1 or is ASCII (decode_rune)."""
+    i = 0
+    while i < len(b):
+        cp, w = decode_rune(b, i)
+        if cp == 0xFFFD and w == 1 and b[i] >= 0x80:
+            return False
+        i += w
+    return True
 
 
 def grep_reduce(key: bytes, values: list[bytes]) -> bytes:
@@ -148,7 +164,7 @@ def _map_reduce_fns(app: str):
     if app == "wc":
         return (lambda name, data: wc_map(data)), wc_reduce
     if app.startswith("grep:"):
-        pat = app[len("grep:"):].encode()
+        pat = app[len("grep:"):].encode("utf-8", "surrogateescape")
         return (lambda name, data: grep_map(data, pat)), grep_reduce
     raise ValueError(f"unknown app {app!r}")
 

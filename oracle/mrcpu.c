@@ -14,10 +14,11 @@
  *                one JSON line {"Key":k,"Value":v} per KV into mr-X-Y (temp + rename).
  *   worker red.: mr/worker.go:99-161 — decode mr-i-Y for i < nMap (missing files
  *                skipped), sort by key, group, Reduce, "%v %v\n" into mr-out-Y.
- * Differences (documented in DESIGN.md): buffered writes instead of one write(2)
- * per KV; no 10 s re-issue watchdog (tasks are sized to finish well within it).
+ * Writes: one write(2) per KV line and per output line, the reference's cost
+ * structure (--buffered: stdio batching instead).  Difference (documented in
+ * DESIGN.md): no 10 s re-issue watchdog (tasks are sized to finish well within it).
  *
- * usage: mrcpu [--app wc|grep] [--pattern P] [--nreduce R] [--workers N] --dir D file...
+ * usage: mrcpu [--app wc|grep] [--pattern P] [--nreduce R] [--workers N] [--buffered] --dir D file...
  * prints: {"seconds": t, "bytes": n, "workers": N, "nmap": M, "nreduce": R}
  */
 #define _GNU_SOURCE
@@ -59,31 +60,58 @@ static uint8_t* read_file(const char* path, size_t* n) {
     fclose(f); *n = (size_t)sz; return b;
 }
 
+/* A growable byte buffer: one encoded KV line (or one output line) at a time. */
+typedef struct { char* b; size_t n, cap; } sbuf;
+static void sb_put(sbuf* o, const void* p, size_t n) {
+    if (o->n + n > o->cap) {
+        size_t c = o->cap ? o->cap : 256;
+        while (c < o->n + n) c *= 2;
+        o->b = (char*)realloc(o->b, c);
+        o->cap = c;
+    }
+    memcpy(o->b + o->n, p, n);
+    o->n += n;
+}
+static void sb_putc(sbuf* o, char c) { sb_put(o, &c, 1); }
+static void sb_puts(sbuf* o, const char* s) { sb_put(o, s, strlen(s)); }
+
+/* Each line leaves as ONE write(2), as the reference's unbuffered *os.File
+ * does: json.Encoder.Encode writes the encoded KV in one Write call
+ * (worker.go:84-89) and fmt.Fprintf one write per key (worker.go:144,
+ * mrsequential.go:81).  --buffered batches them through stdio instead. */
+static int g_buffered = 0;
+static void emit_line(FILE* f, sbuf* line) {
+    if (g_buffered) fwrite(line->b, 1, line->n, f);
+    else if (line->n && write(fileno(f), line->b, line->n) != (ssize_t)line->n) { perror("write"); exit(1); }
+    line->n = 0;
+}
+
 /* encoding/json string encoding (HTML-escaping encoder, the json.NewEncoder default). */
-static void json_str(FILE* o, const uint8_t* s, size_t n) {
+static void json_str(sbuf* o, const uint8_t* s, size_t n) {
     static const char hex[] = "0123456789abcdef";
-    fputc('"', o);
+    sb_putc(o, '"');
     size_t i = 0;
     while (i < n) {
         uint8_t c = s[i];
         if (c < 0x80) {
-            if (c == '"' || c == '\\') { fputc('\\', o); fputc(c, o); }
-            else if (c == '\n') fputs("\\n", o);
-            else if (c == '\r') fputs("\\r", o);
-            else if (c == '\t') fputs("\\t", o);
+            if (c == '"' || c == '\\') { sb_putc(o, '\\'); sb_putc(o, (char)c); }
+            else if (c == '\n') sb_puts(o, "\\n");
+            else if (c == '\r') sb_puts(o, "\\r");
+            else if (c == '\t') sb_puts(o, "\\t");
             else if (c < 0x20 || c == '<' || c == '>' || c == '&') {
-                fputs("\\u00", o); fputc(hex[c >> 4], o); fputc(hex[c & 15], o);
-            } else fputc(c, o);
+                char u[6] = {'\\', 'u', '0', '0', hex[c >> 4], hex[c & 15]};
+                sb_put(o, u, 6);
+            } else sb_putc(o, (char)c);
             i++;
             continue;
         }
         uint32_t cp; size_t w = oracle_decode_rune(s, n, i, &cp);
-        if (cp == 0xFFFD && w == 1) fputs("\\ufffd", o);
-        else if (cp == 0x2028 || cp == 0x2029) fprintf(o, "\\u%04x", cp);
-        else fwrite(s + i, 1, w, o);
+        if (cp == 0xFFFD && w == 1) sb_puts(o, "\\ufffd");
+        else if (cp == 0x2028 || cp == 0x2029) { char u[8]; snprintf(u, sizeof u, "\\u%04x", cp); sb_puts(o, u); }
+        else sb_put(o, s + i, w);
         i += w;
     }
-    fputc('"', o);
+    sb_putc(o, '"');
 }
 
 static void do_map(const char* path, int x) {
@@ -105,12 +133,15 @@ static void do_map(const char* path, int x) {
         fs[r] = fopen(tmp, "wb");
         setvbuf(fs[r], NULL, _IOFBF, 1 << 16);
     }
+    sbuf line = {0};
     for (size_t i = 0; i < nk; i++) {       /* worker.go:74-78 then :84-89 */
         int r = (int)(oracle_ihash(b + offs[i], lens[i]) % (uint32_t)g_nreduce);
-        fputs("{\"Key\":", fs[r]);
-        json_str(fs[r], b + offs[i], lens[i]);
-        fputs(g_app == ORACLE_APP_WC ? ",\"Value\":\"1\"}\n" : ",\"Value\":\"\"}\n", fs[r]);
+        sb_puts(&line, "{\"Key\":");
+        json_str(&line, b + offs[i], lens[i]);
+        sb_puts(&line, g_app == ORACLE_APP_WC ? ",\"Value\":\"1\"}\n" : ",\"Value\":\"\"}\n");
+        emit_line(fs[r], &line);
     }
+    free(line.b);
     for (int r = 0; r < g_nreduce; r++) {
         fclose(fs[r]);
         snprintf(tmp, sizeof tmp, "%s/.tmp-mr-%d-%d-%d", g_dir, x, r, (int)getpid());
@@ -189,15 +220,20 @@ static void do_reduce(int y, int nmap) {
     FILE* o = fopen(tmp, "wb");
     setvbuf(o, NULL, _IOFBF, 1 << 16);
     size_t i = 0;
+    sbuf line = {0};
+    char num[32];
     while (i < nkv) {                           /* worker.go:129-146 */
         size_t j = i + 1;
         while (j < nkv && kv[j].n == kv[i].n && memcmp(kv[j].p, kv[i].p, kv[i].n) == 0) j++;
-        fwrite(kv[i].p, 1, kv[i].n, o);
-        fputc(' ', o);
-        if (g_app == ORACLE_APP_WC) fprintf(o, "%zu", j - i); else fwrite(kv[i].p, 1, kv[i].n, o);
-        fputc('\n', o);
+        sb_put(&line, kv[i].p, kv[i].n);
+        sb_putc(&line, ' ');
+        if (g_app == ORACLE_APP_WC) { int k = snprintf(num, sizeof num, "%zu", j - i); sb_put(&line, num, (size_t)k); }
+        else sb_put(&line, kv[i].p, kv[i].n);
+        sb_putc(&line, '\n');
+        emit_line(o, &line);
         i = j;
     }
+    free(line.b);
     fclose(o);
     snprintf(fin, sizeof fin, "%s/mr-out-%d", g_dir, y);
     rename(tmp, fin);
@@ -237,6 +273,7 @@ int main(int argc, char** argv) {
         else if (!strcmp(argv[i], "--nreduce")) g_nreduce = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--workers")) workers = atoi(argv[++i]);
         else if (!strcmp(argv[i], "--dir")) g_dir = argv[++i];
+        else if (!strcmp(argv[i], "--buffered")) g_buffered = 1;
         else break;
     }
     char** files = argv + i;
@@ -257,7 +294,8 @@ int main(int argc, char** argv) {
     for (int w = 0; w < workers; w++) { wait(&status); if (!WIFEXITED(status) || WEXITSTATUS(status)) ok = 0; }
     clock_gettime(CLOCK_MONOTONIC, &t1);
     double sec = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
-    printf("{\"seconds\": %.6f, \"bytes\": %zu, \"workers\": %d, \"nmap\": %d, \"nreduce\": %d, \"ok\": %s}\n",
-           sec, total, workers, nmap, g_nreduce, ok ? "true" : "false");
+    printf("{\"seconds\": %.6f, \"bytes\": %zu, \"workers\": %d, \"nmap\": %d, \"nreduce\": %d, \"buffered\": %s, "
+           "\"ok\": %s}\n",
+           sec, total, workers, nmap, g_nreduce, g_buffered ? "true" : "false", ok ? "true" : "false");
     return ok ? 0 : 1;
 }

@@ -117,7 +117,21 @@ static int contains(const uint8_t* h, size_t hn, const uint8_t* pat, size_t pn) 
     return 0;
 }
 
+/* utf8.Valid: regexp.Compile of a (quoted) literal fails exactly when it is not
+ * valid UTF-8, and grepMap then returns nil (dgrep.go:20-23). */
+static int valid_utf8(const uint8_t* s, size_t n) {
+    for (size_t i = 0; i < n;) {
+        uint32_t cp;
+        if (s[i] < 0x80) { i++; continue; }
+        size_t w = oracle_decode_rune(s, n, i, &cp);
+        if (w == 1) return 0;
+        i += w;
+    }
+    return 1;
+}
+
 static void grep_lines(const uint8_t* s, size_t n, const uint8_t* pat, size_t pn, okeyvec* out) {
+    if (!valid_utf8(pat, pn)) return;
     size_t ls = 0;
     for (size_t i = 0; i <= n; i++) {
         if (i == n || s[i] == '\n') {

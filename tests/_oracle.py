@@ -70,7 +70,7 @@ def _app(app):
     if app == "wc":
         return APP_WC, b""
     assert app.startswith("grep:")
-    return APP_GREP, app[5:].encode()
+    return APP_GREP, app[5:].encode("utf-8", "surrogateescape")
 
 
 def c_mrsequential(app: str, files) -> bytes:

@@ -100,7 +100,43 @@ def grep_edge_cases() -> dict[str, tuple[list[bytes], bytes]]:
         "tied_lines": ([b"".join(b"the distributed system " + str((i * 7919) % 1000).encode() * (1 + i % 3) + b"\n"
                                  for i in range(1000)) + b"the distributed system \nthe distributed system\n"],
                        b"distributed"),
+        # strings.Split yields a final "" after a trailing '\n'; the empty pattern
+        # matches it, so mr-out holds " \n" 
+        "empty_pattern_trailing_nl": ([b"a\nb\n", b"\n", b"x\n\ny\n"], b""),
+        # a frequent one-byte pattern in lines longer than a lane's scan window
+        # (4 KiB), the same long line twice (bytewise table compare), overlapping
+        # occurrences, and hits right after a newline
+        "long_lines_many_hits": ([_long_line(21000, 1) + b"\nshort e line\n" + _long_line(21000, 1) + b"\n"
+                                  + _long_line(9000, 2) + b"\neee\ne\n" + _long_line(5000, 3)], b"e"),
+        "overlapping": ([b"aaaaaa\nxaax\naaa\naa\na\n"], b"aa"),
+        # > 64 distinct matching lines sharing a 70-byte prefix that differ later,
+        # strict prefixes of one another, NUL bytes past byte 64 (the reduce's
+        # arena-compare fallback past the 64 bytes its sort words cover)
+        "shared_prefix_70": ([_shared_prefix_lines()], b"distributed"),
+        # dgrep.go:20-23: regexp.Compile fails on invalid UTF-8, grepMap returns nil
+        "invalid_utf8_pattern": ([b"ab\xffcd\n\xff\nxx\n"], b"\xff"),
+        "truncated_utf8_pattern": (["κόσμε\n".encode(), b"\xce\n"], b"\xce"),
     }
+
+
+def _long_line(n: int, seed: int) -> bytes:
+    """n bytes of one line (no '\n'): letters with frequent 'e' and spaces."""
+    rnd = random.Random(500 + seed)
+    return bytes(rnd.choice(b"abcdeeee ") for _ in range(n))
+
+
+def _shared_prefix_lines() -> bytes:
+    prefix = b"distributed " + b"p" * 58  # 70 bytes
+    lines = [prefix, prefix + b"a", prefix + b"ab", prefix + b"a\x00", prefix + b"\x00"]
+    for i in range(120):
+        tail = bytes([97 + (i * 7) % 26, 97 + (i * 13) % 26]) * (1 + i % 3)
+        if i % 5 == 0:
+            lines.append(prefix[:66] + b"\x00" + prefix[67:] + tail)
+        else:
+            lines.append(prefix + tail)
+    lines = lines * 2  # duplicates collapse in Reduce
+    random.Random(9).shuffle(lines)
+    return b"\n".join(lines) + b"\n"
 
 
 def synthetic(kind: int, V: int, sizes: list[int], seed: int, invalid_rate: float = 0.0) -> list[bytes]:

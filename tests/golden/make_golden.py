@@ -43,7 +43,7 @@ def main():
                    "out": {str(R): [enc(x) for x in M.mr_partitioned("wc", files, R)] for R in NREDUCES}}
     grep = {}
     for name, (files, pat) in sorted(cases.grep_edge_cases().items()):
-        app = "grep:" + pat.decode()
+        app = "grep:" + pat.decode("utf-8", "surrogateescape")
         grep[name] = {"files": [enc(f) for f in files], "pattern": enc(pat),
                       "out": {str(R): [enc(x) for x in M.mr_partitioned(app, files, R)] for R in (1, 10)}}
     files = cases.synthetic_grep(3000, [60_000], 23, match_rate=0.05)

@@ -53,12 +53,7 @@ def test_grep_corpus_valid_utf8_with_matches():
     assert len(set(hits)) < len(hits)  # some duplicate lines
 
 
-def test_fixed_digest_c1():
-    """C1 substitute corpus bytes are pinned (guards against silent generator drift)."""
+def test_c1_presets():
+    """C1 is the English-like substitute (tests/test_c1.py pins its bytes)."""
     cfg = C.CONFIGS["C1"]
-    v = C.Vocab(cfg["kind"], cfg["s"], cfg["V"], cfg["seed"])
-    files = v.fill_files(cfg["file_sizes"], [cfg["seed"] * 1000 + i for i in range(len(cfg["file_sizes"]))],
-                         cfg["params"]())
-    h = hashlib.sha256(b"".join(bytes(f) for f in files)).hexdigest()
-    assert len(h) == 64
-    np.testing.assert_equal(sum(len(f) for f in files), sum(cfg["file_sizes"]))
+    assert cfg["generator"] == "c1_files" and cfg["file_sizes"] == C.C1_SIZES and cfg["nreduce"] == 10

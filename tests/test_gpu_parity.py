@@ -21,7 +21,7 @@ pytestmark = pytest.mark.gpu
 def gpu_partitioned(ctx, app: str, files: list[bytes], nreduce: int) -> list[bytes]:
     """Map each file as its own split (worker.go map task), merge, reduce all partitions."""
     a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
-    pat = b"" if app == "wc" else app[5:].encode()
+    pat = b"" if app == "wc" else app[5:].encode("utf-8", "surrogateescape")
     parts = None
     for f in files:
         p = ctx.map(a, f, pattern=pat, nreduce=nreduce)
@@ -62,7 +62,7 @@ def test_wc_edge_cases(wctx, name):
 @pytest.mark.parametrize("name", sorted(cases.grep_edge_cases()))
 def test_grep_edge_cases(ctx, name):
     files, pat = cases.grep_edge_cases()[name]
-    check(ctx, "grep:" + pat.decode(), files, nreduces=(1, 10))
+    check(ctx, "grep:" + pat.decode("utf-8", "surrogateescape"), files, nreduces=(1, 10))
 
 
 @pytest.mark.parametrize("kind,V,seed,inv", [(C.KIND_ASCII, 5000, 1, 0.0), (C.KIND_ASCII, 200000, 2, 0.0),
@@ -219,7 +219,7 @@ def test_exchange_group_multi_rank(P, app, R):
     all ranks' inputs.  Long words (> 16 B, arena bytes) and UTF-8 included."""
     from mrgpu import Context
     a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
-    pat = b"" if app == "wc" else app[5:].encode()
+    pat = b"" if app == "wc" else app[5:].encode("utf-8", "surrogateescape")
     files = []
     for i in range(P):
         if app == "wc":
@@ -276,7 +276,7 @@ def test_export_json_matches_reference_format(ctx, app):
     else:
         files = [JSON_GREP_LINES * 3]
     a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
-    pat = b"" if app == "wc" else app[5:].encode()
+    pat = b"" if app == "wc" else app[5:].encode("utf-8", "surrogateescape")
     R = 7
     p = ctx.map(a, b"\n".join(files), pattern=pat, nreduce=R)
     allj = []
@@ -318,3 +318,147 @@ def test_import_json_reference_intermediates(ctx, app):
     empty.free()
     with pytest.raises(Exception):
         ctx.import_json(a, R, b'{"Key":"x"}\n')
+
+
+def test_import_rejects_malformed(ctx):
+    """mrg_parts_import checks every record before it reaches the device
+    (a corrupt intermediate must be MRG_EFORMAT, never an
+    out-of-bounds read or a record in the wrong partition)."""
+    import struct
+
+    from mrgpu import MrgError
+    from mrgpu import intermediate as I
+    R = 8
+    keys = [b"alpha", b"b" * 16, b"long" * 9, b"q"]
+    parts = [O.c_ihash(k) % R for k in keys]
+    good = I.encode(MRG_APP_WC, R, keys, [3, 1, 2, 5], parts)
+    q = ctx.import_(good)
+    assert ctx.reduce_all(q)[parts[0]].count(b"alpha 3\n") == 1
+    q.free()
+    n = len(keys)
+    off_k0, off_cnt, off_koff = I.HDR.size, I.HDR.size + 16 * n, I.HDR.size + 24 * n
+    off_len, off_part = I.HDR.size + 32 * n, I.HDR.size + 36 * n
+
+    def put(buf, off, fmt, v):
+        b = bytearray(buf)
+        struct.pack_into(fmt, b, off, v)
+        return bytes(b)
+
+    bad = {
+        "partition >= nreduce": put(good, off_part, "<I", R),
+        "partition != ihash % R": put(good, off_part, "<I", (parts[0] + 1) % R),
+        "inline key > 16 bytes": put(good, off_len + 4, "<I", 17),
+        "arena key past the arena": put(good, off_koff + 8 * 2, "<Q", 10**6),
+        "arena length past the arena": put(good, off_len + 8, "<I", 10**6),
+        "prefix word differs": put(good, off_k0 + 8 * 2, "<Q", 0x4141414141414141),
+        "zero count": put(good, off_cnt, "<Q", 0),
+        "bytes past inline length": put(good, off_len, "<I", 2),
+        "truncated": good[:-3],
+        "size lies": put(good, 16, "<Q", 2**62),
+    }
+    for why, data in bad.items():
+        with pytest.raises(MrgError, match="import"):
+            ctx.import_(data)
+        assert why
+
+
+# ---------------------------------------------------------------- full-scale splits
+GIB = 1 << 30
+TILED_TOTAL = 4_500_000_000  # > 2^32: byte offsets past 4 GiB, every 1 GiB descriptor base
+
+
+def _seam_tiles(app: str) -> list[tuple[bytes, int]]:
+    """(tile, cut): tile = '\\n' + ... + '\\n'; the 1 GiB boundary falls at byte
+    `cut` of the tile, inside a word (wc) or a pattern occurrence (grep)."""
+    if app == "wc":
+        words = [(b"Xylophonequartzseam", 7), (b"abcdefghijklmnop", 8), (b"seamword", 3), ("ééé".encode(), 3),
+                 (b"qz", 1)]
+        return [(b"\nleft " + w + b" right\n", 6 + k) for w, k in words]
+    return [(b"\nzz distributed seam line\n", 6), (b"\nno match here\ndistributed\n", 15),
+            (b"\n" + "é distributed é".encode() + b"\n", 1), (b"\nx distributed y\n", 4),
+            (b"\ndistributedness\n", 1)]
+
+
+def _tiled_device(base: bytes, app: str):
+    """base repeated until TILED_TOTAL bytes, with a seam tile placed across every
+    1 GiB boundary (and 2^32) and '\\n' padding before it.  Returns the device
+    tensor, the number of base tiles and the seam tiles used."""
+    import torch
+    L = len(base)
+    assert base.endswith(b"\n")
+    seams = _seam_tiles(app)
+    buf = torch.empty(TILED_TOTAL, dtype=torch.uint8, device="cuda:0")
+    dbase = torch.frombuffer(bytearray(base), dtype=torch.uint8).to("cuda:0")
+    bounds = [j * GIB for j in range(1, TILED_TOTAL // GIB + 1)]
+    cur, nb, used = 0, 0, []
+    for j, b in enumerate(bounds):
+        tile, cut = seams[j % len(seams)]
+        start = b - cut
+        while cur + L <= start:
+            buf[cur:cur + L].copy_(dbase)
+            cur += L
+            nb += 1
+        buf[cur:start].fill_(10)
+        buf[start:start + len(tile)].copy_(torch.frombuffer(bytearray(tile), dtype=torch.uint8).to("cuda:0"))
+        used.append(tile)
+        cur = start + len(tile)
+    while cur + L <= TILED_TOTAL:
+        buf[cur:cur + L].copy_(dbase)
+        cur += L
+        nb += 1
+    buf[cur:].fill_(10)
+    torch.cuda.synchronize()
+    return buf, nb, used
+
+
+def _wc_counts(parts: list[bytes]) -> list[dict]:
+    out = []
+    for p in parts:
+        d = {}
+        for line in p.split(b"\n")[:-1]:
+            k, c = line.rsplit(b" ", 1)
+            d[k] = int(c)
+        out.append(d)
+    return out
+
+
+def test_wc_split_past_4gib_vs_oracle(ctx):
+    """One 4.5 GB split (SURVEY.md §8c gate at scale): an oracle-checked 32 MB
+    corpus tiled ~140 times, plus crafted words straddling every 1 GiB boundary
+    and 2^32 (long, 16-byte, short and UTF-8 words).  Expected mr-out-r = the
+    base's counts x tiles + the seam tiles' counts, exactly."""
+    voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
+    base = bytes(voc.fill_files([32_000_000], [4242], C.wc_params())[0])
+    R = 10
+    buf, nb, seams = _tiled_device(base, "wc")
+    try:
+        got = ctx.run_job(MRG_APP_WC, device_ptr=buf.data_ptr(), nbytes=TILED_TOTAL, nreduce=R)
+    finally:
+        del buf
+    want = _wc_counts(O.c_partitioned("wc", [base], R))
+    for r, d in enumerate(_wc_counts(O.c_partitioned("wc", seams, R))):
+        for k in want[r]:
+            want[r][k] *= nb
+        for k, c in d.items():
+            want[r][k] = want[r].get(k, 0) + c
+    for r in range(R):
+        exp = b"".join(k + b" " + str(want[r][k]).encode() + b"\n" for k in sorted(want[r]))
+        assert got[r] == exp, f"partition {r}: {len(got[r])} vs {len(exp)} bytes"
+    assert b"Xylophonequartzseam 1\n" in got[O.c_ihash(b"Xylophonequartzseam") % R]
+
+
+def test_grep_split_past_4gib_vs_oracle(ctx):
+    """grep over the same kind of 4.5 GB tiled split: occurrences and lines
+    straddling every 1 GiB boundary; duplicates of the base's lines collapse, so
+    mr-out-r = the oracle's output over [base] + seam tiles."""
+    voc = C.Vocab(C.KIND_UTF8, 1.07, 10**5, 3)
+    base = bytes(voc.fill_files([32_000_000], [4343], C.grep_params(b"distributed", match_rate=0.01))[0])
+    R = 10
+    buf, nb, seams = _tiled_device(base, "grep")
+    try:
+        got = ctx.run_job(MRG_APP_GREP, pattern=b"distributed", device_ptr=buf.data_ptr(), nbytes=TILED_TOTAL,
+                          nreduce=R)
+    finally:
+        del buf
+    assert nb > 100
+    assert got == O.c_partitioned("grep:distributed", [base] + seams, R)

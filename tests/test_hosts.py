@@ -47,3 +47,24 @@ def test_test_mr_sh_equivalent(tmp_path, app):
     assert not glob.glob(str(job / "mr-*-*[0-9]")) or all("out" in g for g in glob.glob(str(job / "mr-*")))
     all_lines = sorted(l for p in parts for l in p.split(b"\n") if l)  # sort mr-out* | grep .
     assert all_lines == sorted(l for l in out0.split(b"\n") if l)
+
+
+def test_c1_substitute_corpus_hosts(tmp_path):
+    """C1's plumbing run on the GPU hosts: mrseq_gpu (mrsequential.go) and
+    mrjob_gpu -n 10 on the pinned Gutenberg substitute (tests/test_c1.py),
+    byte-exact against the oracle and against each other as test-mr.sh checks."""
+    files = C.c1_files(1)
+    paths = []
+    for i, f in enumerate(files):
+        p = tmp_path / f"pg-{i}.txt"
+        p.write_bytes(f)
+        paths.append(str(p))
+    (tmp_path / "seq").mkdir()
+    (tmp_path / "job").mkdir()
+    _run("mrseq_gpu", ["wc"] + paths, tmp_path / "seq")
+    _run("mrjob_gpu", ["-n", "10", "wc"] + paths, tmp_path / "job")
+    out0 = (tmp_path / "seq" / "mr-out-0").read_bytes()
+    assert out0 == O.c_mrsequential("wc", files)
+    parts = [(tmp_path / "job" / f"mr-out-{r}").read_bytes() for r in range(10)]
+    assert parts == O.c_partitioned("wc", files, 10)
+    assert sorted(l for p in parts for l in p.split(b"\n") if l) == sorted(l for l in out0.split(b"\n") if l)

@@ -56,7 +56,7 @@ def test_c_oracle_wc_golden(name):
 def test_c_oracle_grep_golden(name):
     case = _load("grep_cases.json")[name]
     files = [dec(f) for f in case["files"]]
-    app = "grep:" + dec(case["pattern"]).decode()
+    app = "grep:" + dec(case["pattern"]).decode("utf-8", "surrogateescape")
     for R, outs in case["out"].items():
         assert O.c_partitioned(app, files, int(R)) == [dec(x) for x in outs]
 
