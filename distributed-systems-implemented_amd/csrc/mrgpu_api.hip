@@ -267,6 +267,7 @@ static Tables make_tables(mrg_ctx* c) {
     t.bflag = (uint32_t*)c->bflag.p;
     t.dict = nullptr;
     t.dict_cnt = (uint32_t*)c->dict_cnt.p;
+    t.dict_hot = c->dict.p ? (const uint32_t*)((const uint4*)c->dict.p + kDictSets) : nullptr;
     t.dbg = c->debug_times && c->dbg.ensure(2 * kMaxMapWGs * 8 * 4) == hipSuccess ? (unsigned long long*)c->dbg.p : nullptr;
     return t;
 }
@@ -506,7 +507,8 @@ static int dict_from_recs(mrg_ctx* c, uint64_t nrec) {
     launch_dict_keys(r, keys, idx, c->s);
     if (sort_u32_pairs(c->rws, keys, keys2, idx, idx2, nrec, 16, c->s))
         return fail(c, MRG_EDEVICE, "dictionary sort failed");
-    launch_dict_build(r, idx2, nrec, cand, (uint4*)c->dict.p, c->s);
+    launch_dict_build(r, idx2, nrec, cand, (uint4*)c->dict.p, (uint32_t*)((uint4*)c->dict.p + kDictSets),
+                      (c->map_mode & 0x20000) ? 1 : 2, c->s);
     HCHK(c, hipGetLastError());
     return MRG_OK;
 }
@@ -516,7 +518,7 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
     uint64_t win = 256u << 10;
     if (len < 2 * win) win = (len / 2) & ~15ull;
     if (win < 4096) return MRG_OK;
-    HCHK(c, c->dict.ensure(sizeof(uint4) * kDictSets));
+    HCHK(c, c->dict.ensure(sizeof(uint4) * kDictSets + 16));  // + the 4 hot slots
     const uint64_t target = std::min<uint64_t>(c->dict_sample_bytes, std::max<uint64_t>(len / 64, 4u << 20));
     const uint64_t small = std::min<uint64_t>(target, 2u << 20);
     int rc;

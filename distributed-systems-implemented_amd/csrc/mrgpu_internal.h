@@ -145,6 +145,7 @@ struct Tables {
     uint32_t* bflag;        // [kSpillBuckets] nonzero: a key of the bucket went to the HBM table
     const uint4* dict;      // dictionary image [kDictSets] (nullptr: no dictionary)
     uint32_t* dict_cnt;     // [nwg][kDictSlots] per-map-workgroup dictionary counts
+    const uint32_t* dict_hot;  // [4] count slots of the 4 hottest dictionary keys (~0u: none)
     unsigned long long* dbg;  // diagnostics (MRG_DEBUG_TIMES): per-workgroup s_memrealtime stamps, or nullptr
 };
 
@@ -173,7 +174,9 @@ void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s);
 void launch_sample_gather(const uint8_t* in, uint64_t n, uint64_t win, uint64_t stride, uint32_t nwin, uint8_t* dst,
                           hipStream_t s);
 // Build the dictionary image from sample records ordered by descending count.
-void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s);
+// hot: the count slots of the 4 hottest placed keys; choices: 1 or 2 candidate sets per key.
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, uint32_t* hot,
+                       int choices, hipStream_t s);
 // Sort keys for the dictionary build: ~count (u32) of each record.
 void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t s);
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);

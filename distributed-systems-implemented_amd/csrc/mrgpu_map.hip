@@ -85,7 +85,7 @@ __device__ __forceinline__ void grep_dma(const uint8_t* in, uint64_t n, uint64_t
 // earlier one of the chunk has no '\n' between them (the pattern holds no
 // '\n').  The last occurrence / newline of the lanes below come from a wave
 // prefix max.
-__device__ uint32_t first_hit_per_line(uint32_t hit, uint32_t nl, uint32_t lane) {
+__device__ __attribute__((noinline)) uint32_t first_hit_per_line(uint32_t hit, uint32_t nl, uint32_t lane) {
     int lh = hit ? (int)(16 * lane + 31 - __builtin_clz(hit)) : -1;
     int ln = nl ? (int)(16 * lane + 31 - __builtin_clz(nl)) : -1;
 #pragma unroll

@@ -158,8 +158,12 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
     // 1 = stream input only, 2 = tokenize only (no per-word work), 4 = per-word
     // key extraction without the dictionary, 16 = no spill append (misses dropped),
-    // 32 = spill cursors but no stores; 0x100 / 0x4000 / 0x8000 (exact) = input
-    // loads with the default policy / sc1 / sc0 sc1 instead of nt
+    // 32 = spill cursors but no stores, 8 = dictionary counters not updated;
+    // 0x100 / 0x4000 / 0x8000 (exact) = input loads with the default policy /
+    // sc1 / sc0 sc1 instead of nt.  Exact variants: 0x20000 = single-choice
+    // dictionary lookup (one set read; the dictionary is then built single
+    // choice), 0x40000 = the 4 hottest keys counted by ballots into SGPRs,
+    // 0x80000 = key bytes by three aligned 8-byte LDS reads (not five dword reads)
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -196,6 +200,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         0x00020000);
     uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
     const uint32_t ring0 = lds_addr(L.ring[wv][0]);
+    // mode 0x40000: dictionary slots of the hottest keys, counted in SGPRs (never a real slot: ~0u)
+    uint32_t hot_slot[4] = {~0u, ~0u, ~0u, ~0u}, hot_cnt[4] = {0, 0, 0, 0};
+    if constexpr ((mode & 0x40000) != 0)
+        if (use_dict && t.dict_hot)
+            for (int k = 0; k < 4; k++) hot_slot[k] = __builtin_amdgcn_readfirstlane(t.dict_hot[k]);
 
     // prologue: chunk c0 landed before the loop, chunk c0 + stride in flight
     // byte offsets advance by addition (64-bit scalar multiplies per iteration are not free)
@@ -283,8 +292,21 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     u32x4 km[kBatch];  // the key's byte mask, from the length (same round trip)
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        const lds_u32* p4 = (const lds_u32*)(buf + ((e[u] & 0x3FFu) & ~3u));
-                        g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
+                        if constexpr ((mode & 0x80000) != 0) {
+                            // three aligned 8-byte reads [s & ~7, +24): the lanes' addresses
+                            // rise with the lane, so a 32-lane group spans < 64 banks
+                            const lds_u64* p8 = (const lds_u64*)(buf + ((e[u] & 0x3FFu) & ~7u));
+                            const uint64_t q0 = p8[0], q1 = p8[1], q2 = p8[2];
+                            const bool odd = (e[u] & 4u) != 0;
+                            g0[u] = odd ? (uint32_t)(q0 >> 32) : (uint32_t)q0;
+                            g1[u] = odd ? (uint32_t)q1 : (uint32_t)(q0 >> 32);
+                            g2[u] = odd ? (uint32_t)(q1 >> 32) : (uint32_t)q1;
+                            g3[u] = odd ? (uint32_t)q2 : (uint32_t)(q1 >> 32);
+                            g4[u] = odd ? (uint32_t)(q2 >> 32) : (uint32_t)q2;
+                        } else {
+                            const lds_u32* p4 = (const lds_u32*)(buf + ((e[u] & 0x3FFu) & ~3u));
+                            g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
+                        }
                         km[u] = kmask4[min(e[u] >> 10, 16u)];
                     }
                     uint64_t k0[kBatch], k1[kBatch];
@@ -330,7 +352,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         for (int u = 0; u < kBatch; u++) {
                             dict_sets(hh[u], k1[u] != 0, s1[u], s2[u]);
                             A[u] = dset[s1[u]];
-                            B[u] = dset[s2[u]];
+                            if constexpr ((mode & 0x20000) == 0) B[u] = dset[s2[u]];
+                            else B[u] = (u32x4){0, 0, 0, 0};  // single choice: the second set is never read
                         }
                         __builtin_amdgcn_sched_barrier(0);  // all 2 * kBatch set reads in flight before the compares
         #pragma unroll
@@ -358,7 +381,22 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             const uint32_t wa = __builtin_amdgcn_inverse_ballot_w64(~mMid & ~mA0) ? 1u : 0u;
                             const uint32_t wb = __builtin_amdgcn_inverse_ballot_w64(~mMid & ~mB0) ? 1u : 0u;
                             const uint32_t slot = __builtin_amdgcn_inverse_ballot_w64(mHa) ? 2 * s1[u] + wa : 2 * s2[u] + wb;
-                            const uint32_t ci = hit[u] ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
+                            bool cnt_lds = hit[u];
+                            if constexpr ((mode & 0x40000) != 0) {
+                                // the hottest keys ("the" alone is ~10 % of C2's words) are counted
+                                // with ballots into SGPRs: in an LDS add, lanes of one address serialize
+                                const uint64_t mSlot0 = __ballot(slot == hot_slot[0]) & mHit[u];
+                                const uint64_t mSlot1 = __ballot(slot == hot_slot[1]) & mHit[u];
+                                const uint64_t mSlot2 = __ballot(slot == hot_slot[2]) & mHit[u];
+                                const uint64_t mSlot3 = __ballot(slot == hot_slot[3]) & mHit[u];
+                                hot_cnt[0] += (uint32_t)__popcll(mSlot0);
+                                hot_cnt[1] += (uint32_t)__popcll(mSlot1);
+                                hot_cnt[2] += (uint32_t)__popcll(mSlot2);
+                                hot_cnt[3] += (uint32_t)__popcll(mSlot3);
+                                cnt_lds = __builtin_amdgcn_inverse_ballot_w64(mHit[u] & ~(mSlot0 | mSlot1 | mSlot2 | mSlot3));
+                            }
+                            if constexpr ((mode & 8) != 0) cnt_lds = false;  // ablation: counters not updated
+                            const uint32_t ci = cnt_lds ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
                             __hip_atomic_fetch_add(&dcnt[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     } else {
@@ -470,6 +508,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         dma_for_chunk<dma_policy(mode)>(in, n, cs + 2 * cstep, lane, ring0 + kf * kSlotBytes);
     }
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
+    if constexpr ((mode & 0x40000) != 0)
+        if (lane == 0)
+            for (int k = 0; k < 4; k++)
+                if (hot_cnt[k]) __hip_atomic_fetch_add(&dcnt[hot_slot[k]], hot_cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 
     __syncthreads();
     unsigned long long spilled = 0, hits = 0;
@@ -1065,7 +1107,8 @@ __global__ void dict_cands_kernel(Recs r, const uint32_t* order, uint64_t lim, u
 // One workgroup places the candidates in order, 1024 at a time, each into the
 // first of its two sets with a free way; a key whose two sets are full stays out
 // (it is then counted through the spill path).
-__global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uint64_t lim, uint4* dict) {
+__global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uint64_t lim, uint4* dict, uint32_t* hot,
+                                                            int choices) {
     __shared__ uint4 S[kDictSets];
     __shared__ uint32_t fill[kDictSets];
     const uint32_t tid = threadIdx.x;
@@ -1073,6 +1116,7 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uin
         S[i] = make_uint4(0, 0, 0, 0);
         fill[i] = 0;
     }
+    if (hot && tid < 4) hot[tid] = ~0u;
     __syncthreads();
     uint4 nx = tid < lim ? cand[tid] : make_uint4(0, 0, 0, 0);
     for (uint64_t base = 0; base < lim; base += 1024) {
@@ -1086,11 +1130,13 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uin
             dict_sets(fold32(c.x, c.y, c.z, c.w), mid, s1, s2);
             const uint32_t ways = mid ? 1u : 2u;
             uint32_t s = s1, w = atomicAdd(&fill[s1], 1u);
-            if (w >= ways) { s = s2; w = atomicAdd(&fill[s2], 1u); }
+            if (w >= ways && choices > 1) { s = s2; w = atomicAdd(&fill[s2], 1u); }
             if (w < ways) {
                 if (mid) S[s] = c;
                 else if (w == 0) { S[s].x = c.x; S[s].y = c.y; }
                 else { S[s].z = c.x; S[s].w = c.y; }
+                // the 4 hottest candidates' count slots (way w of set s: slot 2 s + w)
+                if (base == 0 && tid < 4 && hot) hot[tid] = 2 * s + w;
             }
         }
         __syncthreads();
@@ -1120,8 +1166,9 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     switch (mode) {
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
-        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(16) MRG_MAP_MODE(32) MRG_MAP_MODE(0x100)
-        MRG_MAP_MODE(0x4000) MRG_MAP_MODE(0x8000)
+        MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(8) MRG_MAP_MODE(16) MRG_MAP_MODE(32)
+        MRG_MAP_MODE(0x100) MRG_MAP_MODE(0x4000) MRG_MAP_MODE(0x8000) MRG_MAP_MODE(0x20000) MRG_MAP_MODE(0x40000)
+        MRG_MAP_MODE(0x60000) MRG_MAP_MODE(0x80000) MRG_MAP_MODE(0xE0000)
 #undef MRG_MAP_MODE
         // occupancy benchmark: 8 or 12 waves per workgroup (results stay exact)
         case 0x1000: wc_map_kernel<0, 8><<<(unsigned)g, 8 * kWave, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
@@ -1163,10 +1210,11 @@ void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t 
 }
 
 // cand: scratch for kDictCands uint4
-void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s) {
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, uint32_t* hot,
+                       int choices, hipStream_t s) {
     const uint64_t lim = n < kDictCands ? n : kDictCands;
     if (lim) dict_cands_kernel<<<(unsigned)((lim + 255) / 256), 256, 0, s>>>(r, order, lim, cand);
-    dict_build_kernel<<<1, 1024, 0, s>>>(cand, lim, dict);
+    dict_build_kernel<<<1, 1024, 0, s>>>(cand, lim, dict, hot, choices);
 }
 
 }  // namespace mrg

@@ -1,0 +1,75 @@
+// mrhost_util.h — shared helpers of the C++ hosts over the C ABI (mrhost.cpp,
+// mrcoord.cpp): file I/O with the reference's error behaviour (log.Fatalf ->
+// message + exit 1, worker.go:60-64), temp + rename outputs (worker.go:83,91),
+// and the APP argument ("wc" | "grep:<literal>"), the plugin choice of
+// main/mrworker.go:34-51.
+#pragma once
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mrgpu.h"
+
+namespace mrhost {
+
+[[noreturn]] inline void fatalf(const char* fmt, const char* a, const char* b = "") {
+    fprintf(stderr, fmt, a, b);
+    fputc('\n', stderr);
+    exit(1);
+}
+
+inline std::vector<uint8_t> read_file(const char* path) {
+    FILE* f = fopen(path, "rb");
+    if (!f) fatalf("cannot open %s", path);
+    std::vector<uint8_t> b;
+    uint8_t tmp[1 << 16];
+    size_t n;
+    while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) b.insert(b.end(), tmp, tmp + n);
+    if (ferror(f)) fatalf("cannot read %s", path);
+    fclose(f);
+    return b;
+}
+
+inline bool read_file_opt(const std::string& path, std::vector<uint8_t>* out) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    fclose(f);
+    *out = read_file(path.c_str());
+    return true;
+}
+
+inline void write_file_atomic(const std::string& name, const void* p, size_t n) {
+    std::string tmp = name + ".tmp";  // temp + rename, as worker.go:83,91
+    FILE* f = fopen(tmp.c_str(), "wb");
+    if (!f) fatalf("cannot create %s", tmp.c_str());
+    if (n && fwrite(p, 1, n, f) != n) fatalf("cannot write into %s", name.c_str());
+    fclose(f);
+    if (rename(tmp.c_str(), name.c_str()) != 0) fatalf("cannot rename %s", tmp.c_str());
+}
+
+struct App {
+    int id;
+    std::string pat;
+};
+
+inline App parse_app(const char* a) {
+    if (!strcmp(a, "wc")) return {MRG_APP_WC, ""};
+    if (!strncmp(a, "grep:", 5)) return {MRG_APP_GREP, std::string(a + 5)};
+    fatalf("unknown app %s (want wc or grep:<literal>)", a);
+}
+
+inline void check(mrg_ctx* c, int rc, const char* what) {
+    if (rc != MRG_OK) fatalf("%s failed: %s", what, mrg_last_error(c));
+}
+
+inline mrg_parts* map_split(mrg_ctx* c, const App& app, const std::vector<uint8_t>& data, uint32_t nreduce) {
+    mrg_parts* p = nullptr;
+    check(c, mrg_map(c, app.id, data.data(), data.size(), MRG_INPUT_HOST, (const uint8_t*)app.pat.data(),
+                     app.pat.size(), nreduce, &p),
+          "mrg_map");
+    return p;
+}
+
+}  // namespace mrhost

@@ -42,7 +42,7 @@ def main():
     res = []
     for g in [int(x) for x in a.grids.split(",")]:
         ctx.set_option("map_grid", g)
-        for m in [int(x) for x in a.modes.split(",")]:
+        for m in [int(x, 0) for x in a.modes.split(",")]:
             ctx.set_option("map_mode", m)
             ts = []
             for _ in range(a.reps):

@@ -462,3 +462,67 @@ def test_grep_split_past_4gib_vs_oracle(ctx):
         del buf
     assert nb > 100
     assert got == O.c_partitioned("grep:distributed", [base] + seams, R)
+
+
+def _merge_partitioned_wc(outs: list[list[bytes]], R: int) -> list[bytes]:
+    """Σ of several oracle wc outputs (same R) -> the oracle output of the union."""
+    merged = [dict() for _ in range(R)]
+    for out in outs:
+        for r, d in enumerate(_wc_counts(out)):
+            m = merged[r]
+            for k, c in d.items():
+                m[k] = m.get(k, 0) + c
+    return [b"".join(k + b" " + str(m[k]).encode() + b"\n" for k in sorted(m)) for m in merged]
+
+
+def _group_job(files: list[bytes], R: int) -> list[list[bytes]]:
+    """Rank i maps files[i] on its own context, the P-context shuffle, then every
+    owner reduces; returns each rank's mr-out-r list."""
+    from mrgpu import Context
+    P = len(files)
+    ctxs = [Context(0) for _ in range(P)]
+    try:
+        local = [ctxs[i].map(MRG_APP_WC, files[i], nreduce=R) for i in range(P)]
+        owned = Context.exchange_group(ctxs, local)
+        outs = [ctxs[i].reduce_all(owned[i]) for i in range(P)]
+        st = [c.stats() for c in ctxs]
+        for q in local + owned:
+            q.free()
+        assert all(s["shuffle_send_bytes"] > 0 for s in st)
+        return outs
+    finally:
+        for c in ctxs:
+            c.close()
+
+
+def test_exchange_group_c4_shape():
+    """C4's shape (8 ranks, nReduce = 64, C2 generator, 64 MB per rank, seed 4+g):
+    owner r % 8 of every partition equals the oracle over all ranks' inputs."""
+    from concurrent.futures import ThreadPoolExecutor
+    P, R = 8, 64
+    voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 4)
+    files = [bytes(f) for f in voc.fill_files([64_000_000] * P, [4 + g for g in range(P)], C.wc_params())]
+    with ThreadPoolExecutor(P) as ex:  # the C oracle releases the GIL
+        per = list(ex.map(lambda f: O.c_partitioned("wc", [f], R), files))
+    want = _merge_partitioned_wc(per, R)
+    outs = _group_job(files, R)
+    for i in range(P):
+        for r in range(R):
+            assert outs[i][r] == (want[r] if r % P == i else b""), f"rank {i} partition {r}"
+
+
+def test_exchange_group_c5_shape():
+    """C5's shape (high cardinality): 4 ranks, each emitting its 3 M-word share of
+    a Zipf(0.8, 1.2e7) vocabulary once up front plus sampled words (>= 3 M
+    distinct keys per rank), nReduce = 64 — multi-round aggregation on every rank
+    and millions of records through the shuffle."""
+    P, R, V = 4, 64, 12_000_000
+    voc = C.Vocab(C.KIND_ASCII, 0.8, V, 5)
+    files = [bytes(voc.fill_files([32_000_000], [5 + g], C.wc_params(vocab_lo=3_000_000 * g,
+                                                                      vocab_hi=3_000_000 * (g + 1)))[0])
+             for g in range(P)]
+    want = O.c_partitioned("wc", files, R)
+    outs = _group_job(files, R)
+    for i in range(P):
+        for r in range(R):
+            assert outs[i][r] == (want[r] if r % P == i else b""), f"rank {i} partition {r}"
