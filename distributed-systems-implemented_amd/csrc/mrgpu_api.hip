@@ -17,7 +17,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
+#include <chrono>
 #include <mutex>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -164,6 +167,8 @@ struct mrg_ctx {
     uint64_t rec_cap = 1u << 21;       // record output buffer capacity (grows on overflow)
     bool sh_clean = false;             // ShortTable known to be empty (skip its clear)
     int dict_mode = 0;                 // <0: never build the hot-key dictionary
+    bool dict_warm = true;             // level-1 dictionary = the previous map task's (see build_dict)
+    bool dict_valid = false;           // c->dict holds a dictionary built by an earlier call
     uint64_t dict_min_bytes = 32ull << 20;
     uint64_t dict_sample_bytes = 16ull << 20;  // C2: 16 vs 64 MB loses 0.13% of dictionary hits, halves the build
     uint64_t spill_sub_keys = 0, spill_sub8 = 0;
@@ -174,6 +179,14 @@ struct mrg_ctx {
     // same-process T(1) for the weak-scaling efficiency: the rank's own split,
     // every partition reduced locally)
     bool skip_exchange = false;
+    // Host-input splits of at least ingest_min bytes are copied in pieces of
+    // ~ingest_piece bytes on a second stream, each piece mapped as soon as it and
+    // the next one (look-ahead) are resident.
+    uint64_t ingest_piece = 256ull << 20, ingest_min = 64ull << 20;
+    hipStream_t cs = nullptr;            // copy stream (created on first use)
+    std::vector<hipEvent_t> piece_ev;    // one per piece, reused
+    uint8_t* h_sample = nullptr;         // pinned: dictionary sample gathered from host input
+    size_t h_sample_cap = 0;
     int sh_log2 = 20, lo_log2 = 14;  // HBM tables (grow on overflow); the wc short table holds only the spill path's leftovers
     // LongTable size of the current call: wc maps start from lo_log2 (words > 16
     // bytes; sticky, grows on overflow), grep maps size it per job from their
@@ -267,7 +280,6 @@ static Tables make_tables(mrg_ctx* c) {
     t.bflag = (uint32_t*)c->bflag.p;
     t.dict = nullptr;
     t.dict_cnt = (uint32_t*)c->dict_cnt.p;
-    t.dict_hot = c->dict.p ? (const uint32_t*)((const uint4*)c->dict.p + kDictSets) : nullptr;
     t.dbg = c->debug_times && c->dbg.ensure(2 * kMaxMapWGs * 8 * 4) == hipSuccess ? (unsigned long long*)c->dbg.p : nullptr;
     return t;
 }
@@ -468,11 +480,26 @@ static void print_stamps(mrg_ctx* c, const char* what, uint32_t nblocks, uint32_
 // become the records the final dictionary is built from.  Only speed depends
 // on the dictionary: every key it misses is counted exactly through the spill.
 static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win, uint32_t nwin, LetterTables lt,
-                       bool with_dict, uint64_t* nrec_out, double* spill_rate = nullptr) {
+                       bool with_dict, uint64_t* nrec_out, double* spill_rate = nullptr, const uint8_t* host = nullptr) {
     const uint64_t stride = ((len - win) / nwin) & ~15ull;
     const uint64_t sn = (uint64_t)nwin * (win + 16);
     HCHK(c, c->sample.ensure(sn + 64));
-    launch_sample_gather(in, len, win, stride, nwin, (uint8_t*)c->sample.p, c->s);
+    if (host) {  // host input still in flight: the same sample bytes, gathered on the host
+        if (c->h_sample_cap < sn) {
+            if (c->h_sample) hipHostFree(c->h_sample);
+            c->h_sample = nullptr;
+            c->h_sample_cap = 0;
+            HCHK(c, hipHostMalloc((void**)&c->h_sample, sn, hipHostMallocDefault));
+            c->h_sample_cap = sn;
+        }
+        for (uint32_t w = 0; w < nwin; w++) {  // window w, then 16 '\n' (sample_gather_kernel's layout)
+            memcpy(c->h_sample + w * (win + 16), host + w * stride, win);
+            memset(c->h_sample + w * (win + 16) + win, '\n', 16);
+        }
+        HCHK(c, hipMemcpyAsync(c->sample.p, c->h_sample, sn, hipMemcpyHostToDevice, c->s));
+    } else {
+        launch_sample_gather(in, len, win, stride, nwin, (uint8_t*)c->sample.p, c->s);
+    }
     int rc;
     if ((rc = ensure_tables(c)) || (rc = ensure_recbuf(c))) return rc;
     Tables t = make_tables(c);
@@ -507,28 +534,38 @@ static int dict_from_recs(mrg_ctx* c, uint64_t nrec) {
     launch_dict_keys(r, keys, idx, c->s);
     if (sort_u32_pairs(c->rws, keys, keys2, idx, idx2, nrec, 16, c->s))
         return fail(c, MRG_EDEVICE, "dictionary sort failed");
-    launch_dict_build(r, idx2, nrec, cand, (uint4*)c->dict.p, (uint32_t*)((uint4*)c->dict.p + kDictSets),
-                      (c->map_mode & 0x20000) ? 1 : 2, c->s);
+    launch_dict_build(r, idx2, nrec, cand, (uint4*)c->dict.p, c->s);
     HCHK(c, hipGetLastError());
     return MRG_OK;
 }
 
-static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables lt, bool* have) {
+static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables lt, bool* have,
+                      const uint8_t* host = nullptr) {
     *have = false;
     uint64_t win = 256u << 10;
     if (len < 2 * win) win = (len / 2) & ~15ull;
     if (win < 4096) return MRG_OK;
-    HCHK(c, c->dict.ensure(sizeof(uint4) * kDictSets + 16));  // + the 4 hot slots
+    HCHK(c, c->dict.ensure(sizeof(uint4) * kDictSets));
     const uint64_t target = std::min<uint64_t>(c->dict_sample_bytes, std::max<uint64_t>(len / 64, 4u << 20));
     const uint64_t small = std::min<uint64_t>(target, 2u << 20);
     int rc;
     uint64_t nrec = 0;
-    if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, small / win), lt, false, &nrec))) return rc;
-    if (nrec == 0) return MRG_OK;
-    if ((rc = dict_from_recs(c, nrec))) return rc;
+    // Warm start: a context that already built a dictionary (its previous map
+    // task) maps the full sample with that one instead of first building a
+    // level-1 dictionary from a small sample.  The final dictionary still comes
+    // from this split's own sample; only speed depends on either.
+    const bool warm = c->dict_warm && c->dict_valid && target > small;
+    if (!warm) {
+        if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, small / win), lt, false, &nrec, nullptr,
+                              host)))
+            return rc;
+        if (nrec == 0) return MRG_OK;
+        if ((rc = dict_from_recs(c, nrec))) return rc;
+    }
     if (target > small) {
         double rate = 0;
-        if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, target / win), lt, true, &nrec, &rate)))
+        if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, target / win), lt, true, &nrec, &rate,
+                              host)))
             return rc;
         if (nrec && (rc = dict_from_recs(c, nrec))) return rc;
         // Spill streams hold 0.094 8-byte records per input byte at scale 1 (C2
@@ -539,6 +576,7 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
         if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
     }
     c->stats.dict_keys = nrec;
+    c->dict_valid = true;
     *have = true;
     return MRG_OK;
 }
@@ -602,23 +640,115 @@ static int aggregate_rounds(mrg_ctx* c, Tables& t) {
     return MRG_OK;
 }
 
+// ---------------------------------------------------------------- streamed ingest
+// A host-input split is copied to the staging buffer in pieces by a helper
+// thread (copy stream, one event per piece) while this thread launches the map
+// over each piece as soon as the piece and the next one (the chunk windows'
+// 64-byte look-ahead) are resident.  Pieces are multiples of both map chunk
+// sizes, so the chunk grid — and every result — is that of one whole-split map.
+struct Ingest {
+    mrg_ctx* c = nullptr;
+    std::thread th;
+    std::atomic<int> recorded{0};  // events recorded so far
+    std::atomic<int> err{0};
+    uint64_t piece = 0;
+    int npieces = 0;
+    ~Ingest() {  // every early return still joins the copy thread
+        if (th.joinable()) th.join();
+    }
+};
+
+static int ingest_start(mrg_ctx* c, Ingest& g, const uint8_t* host, uint8_t* dev, uint64_t len) {
+    constexpr uint64_t kUnit = 56640;  // lcm(kWcChunkBytes, kGrepChunkBytes)
+    static_assert(kUnit % kWcChunkBytes == 0 && kUnit % kGrepChunkBytes == 0, "piece unit");
+    g.c = c;
+    g.piece = std::max<uint64_t>(kUnit, c->ingest_piece / kUnit * kUnit);
+    g.npieces = (int)((len + g.piece - 1) / g.piece);
+    if (!c->cs) HCHK(c, hipStreamCreateWithFlags(&c->cs, hipStreamNonBlocking));
+    while ((int)c->piece_ev.size() < g.npieces) {
+        hipEvent_t e;
+        HCHK(c, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        c->piece_ev.push_back(e);
+    }
+    const int dev_id = c->device;
+    hipStream_t cs = c->cs;
+    hipEvent_t* ev = c->piece_ev.data();
+    g.th = std::thread([&g, host, dev, len, dev_id, cs, ev]() {
+        if (hipSetDevice(dev_id) != hipSuccess) g.err = 1;
+        for (int k = 0; k < g.npieces && !g.err; k++) {
+            const uint64_t off = (uint64_t)k * g.piece, n = std::min<uint64_t>(g.piece, len - off);
+            if (hipMemcpyAsync(dev + off, host + off, n, hipMemcpyHostToDevice, cs) != hipSuccess ||
+                hipEventRecord(ev[k], cs) != hipSuccess)
+                g.err = 1;
+            g.recorded.store(k + 1);
+        }
+        g.recorded.store(g.npieces);
+    });
+    return MRG_OK;
+}
+
+// Make c->s wait until pieces [0, k] are resident; false on a copy error.
+static bool ingest_wait(Ingest& g, int k) {
+    while (g.recorded.load() <= k) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    if (g.err) return false;
+    return hipStreamWaitEvent(g.c->s, g.c->piece_ev[k], 0) == hipSuccess;
+}
+
+static int ingest_finish(mrg_ctx* c, Ingest& g) {
+    if (g.th.joinable()) g.th.join();
+    if (g.err) return fail(c, MRG_EDEVICE, "host input copy failed");
+    return MRG_OK;
+}
+
+// Map chunk range [b, e) of piece-aligned host input: launch(cb, ce, resume)
+// per piece once the piece and its successor are resident.
+template <class F>
+static int ingest_map(mrg_ctx* c, Ingest& g, uint64_t chunk_bytes, uint64_t len, F launch) {
+    const uint64_t per = g.piece / chunk_bytes;  // chunks per piece
+    const uint64_t nch = (len + chunk_bytes - 1) / chunk_bytes;
+    for (int k = 0; k < g.npieces; k++) {
+        if (!ingest_wait(g, std::min(k + 1, g.npieces - 1))) {
+            ingest_finish(c, g);
+            return fail(c, MRG_EDEVICE, "host input copy failed");
+        }
+        const uint64_t cb = (uint64_t)k * per, ce = std::min<uint64_t>(nch, cb + per);
+        if (!launch(cb, ce, k > 0)) {
+            ingest_finish(c, g);
+            return fail(c, MRG_EINVAL, "split too large for 32-bit chunk indices (%llu bytes)", (unsigned long long)len);
+        }
+    }
+    return ingest_finish(c, g);
+}
+
 // wc: dictionary, map, bucket aggregation, dictionary records, long words, collect.
-static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce, LetterTables lt, mrg_parts** out) {
+static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce, LetterTables lt, mrg_parts** out,
+                  const uint8_t* host = nullptr) {
     int rc;
     c->lo_log2_cur = c->lo_log2;
+    Ingest ing;
+    if (host && (rc = ingest_start(c, ing, host, (uint8_t*)in, len))) return rc;
     if ((rc = ensure_spill(c, len))) return rc;
     const uint32_t nwg = c->spill_nwg;
     HCHK(c, c->dict_cnt.ensure((size_t)nwg * kDictSlots * sizeof(uint32_t)));
     HCHK(c, hipEventRecord(c->ev[9], c->s));
     bool have_dict = false;
-    if (c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict))) return rc;
+    if (c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict, host))) {
+        ingest_finish(c, ing);
+        return rc;
+    }
     // the sample may have raised spill_scale: size the streams for this split now,
     // not only from the next call on (overflowing streams merge through HBM: slow)
-    if ((rc = ensure_spill(c, len))) return rc;
+    if ((rc = ensure_spill(c, len))) {
+        ingest_finish(c, ing);
+        return rc;
+    }
     HCHK(c, hipEventRecord(c->ev[10], c->s));
     for (int attempt = 0; attempt < 8; attempt++) {
         c->lo_log2 = std::max(c->lo_log2, c->lo_log2_cur);  // long words: the grown size sticks for later wc maps
-        if ((rc = ensure_tables(c)) || (rc = ensure_recbuf(c))) return rc;
+        if ((rc = ensure_tables(c)) || (rc = ensure_recbuf(c))) {
+            ingest_finish(c, ing);
+            return rc;
+        }
         Tables t = make_tables(c);
         t.dict = have_dict ? (const uint4*)c->dict.p : nullptr;
         t.nreduce = nreduce;
@@ -626,8 +756,15 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         t.out_cap = c->rec_cap;
         clear_for_run(c, t);
         HCHK(c, hipEventRecord(c->ev[0], c->s));
-        if (!launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s))
+        if (ing.npieces && attempt == 0) {  // the first pass runs while the host input streams in
+            rc = ingest_map(c, ing, kWcChunkBytes, len, [&](uint64_t cb, uint64_t ce, bool resume) {
+                return launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s, cb, ce, resume);
+            });
+            if (rc) return rc;
+        } else if (!launch_wc_map(in, len, t, lt, c->grid, c->map_mode, c->s)) {
+            ingest_finish(c, ing);
             return fail(c, MRG_EINVAL, "split too large for 32-bit chunk indices (%llu bytes)", (unsigned long long)len);
+        }
         HCHK(c, hipEventRecord(c->ev[1], c->s));
         print_stamps(c, "map", nwg, kSpillBuckets);
         if ((rc = aggregate_rounds(c, t))) return rc;
@@ -717,9 +854,10 @@ static bool go_valid_utf8(const uint8_t* p, size_t n) {
 // when it is not valid UTF-8; a pattern holding '\n' matches no line of
 // strings.Split(contents, "\n") (dgrep.go:26).
 static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* pat, size_t plen, uint32_t nreduce,
-                    mrg_parts** out) {
+                    mrg_parts** out, const uint8_t* host = nullptr) {
     int rc;
     if (!go_valid_utf8(pat, plen) || (plen && memchr(pat, '\n', plen))) {
+        if (host) HCHK(c, hipMemcpyAsync((void*)in, host, len, hipMemcpyHostToDevice, c->s));  // no map: plain copy
         HCHK(c, hipEventRecord(c->ev[0], c->s));
         if ((rc = parts_alloc(c, 0, 0, MRG_APP_GREP, nreduce, out))) return rc;
         c->stats.distinct_keys = 0;
@@ -728,13 +866,28 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
     HCHK(c, c->pat.ensure(plen + 16));
     if (plen) HCHK(c, hipMemcpyAsync(c->pat.p, pat, plen, hipMemcpyHostToDevice, c->s));
     c->lo_log2_cur = 14;
+    Ingest ing;
+    if (host && plen && (rc = ingest_start(c, ing, host, (uint8_t*)in, len))) return rc;
+    if (host && !plen) HCHK(c, hipMemcpyAsync((void*)in, host, len, hipMemcpyHostToDevice, c->s));
     for (int attempt = 0; attempt < 8; attempt++) {
-        if ((rc = ensure_tables(c))) return rc;
+        if ((rc = ensure_tables(c))) {
+            ingest_finish(c, ing);
+            return rc;
+        }
         Tables t = make_tables(c);
         clear_for_run(c, t);
         HCHK(c, hipEventRecord(c->ev[0], c->s));
-        if (plen) launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);
-        else launch_grep_all_lines(in, len, t, c->grid, c->s);
+        if (plen && ing.npieces && attempt == 0) {  // the first pass runs while the host input streams in
+            rc = ingest_map(c, ing, kGrepChunkBytes, len, [&](uint64_t cb, uint64_t ce, bool) {
+                launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s, cb, ce);
+                return true;
+            });
+            if (rc) return rc;
+        } else if (plen) {
+            launch_grep_map(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->grid, c->s);
+        } else {
+            launch_grep_all_lines(in, len, t, c->grid, c->s);
+        }
         HCHK(c, hipGetLastError());
         HCHK(c, hipEventRecord(c->ev[1], c->s));
         if ((rc = read_counters(c))) return rc;
@@ -849,6 +1002,9 @@ void mrg_close(mrg_ctx* c) {
     if (c->h_ctr) hipHostFree(c->h_ctr);
     if (c->h_scr) hipHostFree(c->h_scr);
     if (c->h_out) hipHostFree(c->h_out);
+    if (c->h_sample) hipHostFree(c->h_sample);
+    for (hipEvent_t e : c->piece_ev) hipEventDestroy(e);
+    if (c->cs) hipStreamDestroy(c->cs);
     reduce_ws_free(c->rws);
     for (auto& e : c->ev)
         if (e) hipEventDestroy(e);
@@ -872,10 +1028,13 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "agg_big0")) c->agg_big0 = v >= 0;  // -1: off
     else if (!strcmp(name, "agg_carry_min")) c->agg_carry_min = v > 0 ? (uint32_t)v : v < 0 ? 0u : 64u;  // -1: always carry
     else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
+    else if (!strcmp(name, "dict_warm")) c->dict_warm = v >= 0;  // -1: always build the level-1 dictionary
     else if (!strcmp(name, "dict_min_bytes")) c->dict_min_bytes = v > 0 ? (uint64_t)v : (32ull << 20);
     else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);
     else if (!strcmp(name, "rec_cap")) c->rec_cap = v > 0 ? (uint64_t)v : (1u << 21);
     else if (!strcmp(name, "skip_exchange")) c->skip_exchange = v > 0;
+    else if (!strcmp(name, "ingest_piece")) c->ingest_piece = v > 0 ? (uint64_t)v : (256ull << 20);
+    else if (!strcmp(name, "ingest_min")) c->ingest_min = v > 0 ? (uint64_t)v : (64ull << 20);
     else return fail(c, MRG_EINVAL, "unknown option %s", name);
     return MRG_OK;
 }
@@ -953,16 +1112,18 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
     c->stats = mrg_stats{};
     c->stats.input_bytes = len;
     const uint8_t* in = (const uint8_t*)buf;
+    const uint8_t* host = nullptr;  // host input streamed in pieces, overlapped with the map
     if (kind == MRG_INPUT_HOST || (((uintptr_t)buf) & 15)) {
         HCHK(c, c->staging.ensure(len + 64));
-        HCHK(c, hipMemcpyAsync(c->staging.p, buf, len, kind == MRG_INPUT_HOST ? hipMemcpyHostToDevice
-                                                                           : hipMemcpyDeviceToDevice, c->s));
+        if (kind == MRG_INPUT_HOST && len >= c->ingest_min) host = (const uint8_t*)buf;
+        else HCHK(c, hipMemcpyAsync(c->staging.p, buf, len, kind == MRG_INPUT_HOST ? hipMemcpyHostToDevice
+                                                                                 : hipMemcpyDeviceToDevice, c->s));
         in = (const uint8_t*)c->staging.p;
         c->stats.staged_bytes = len;
     }
     LetterTables lt{c->d_l1, c->d_l2};
-    if (app == MRG_APP_WC) return wc_map(c, in, len, nreduce, lt, out);
-    return grep_map(c, in, len, pat, plen, nreduce, out);
+    if (app == MRG_APP_WC) return wc_map(c, in, len, nreduce, lt, out, host);
+    return grep_map(c, in, len, pat, plen, nreduce, out, host);
 }
 
 void mrg_parts_free(mrg_parts* p) {

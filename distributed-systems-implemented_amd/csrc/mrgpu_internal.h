@@ -145,7 +145,6 @@ struct Tables {
     uint32_t* bflag;        // [kSpillBuckets] nonzero: a key of the bucket went to the HBM table
     const uint4* dict;      // dictionary image [kDictSets] (nullptr: no dictionary)
     uint32_t* dict_cnt;     // [nwg][kDictSlots] per-map-workgroup dictionary counts
-    const uint32_t* dict_hot;  // [4] count slots of the 4 hottest dictionary keys (~0u: none)
     unsigned long long* dbg;  // diagnostics (MRG_DEBUG_TIMES): per-workgroup s_memrealtime stamps, or nullptr
 };
 
@@ -158,8 +157,12 @@ struct LetterTables {
 void clear_tables(const Tables& t, bool short_table, hipStream_t s);
 // ---- wc pipeline (mrgpu_wc.hip) ----
 uint32_t wc_map_grid(uint64_t n, int grid);
+// Chunks [cbeg, cend) of the split (kOwn = 944 input bytes each; default: all);
+// resume: a previous launch of this map already ran over chunks < cbeg.
 bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode,
-                   hipStream_t s);
+                   hipStream_t s, uint64_t cbeg = 0, uint64_t cend = ~0ull, bool resume = false);
+constexpr uint64_t kWcChunkBytes = 944;   // input bytes a wc map chunk owns
+constexpr uint64_t kGrepChunkBytes = 960; // input bytes a grep map chunk owns
 // emit: 0 = flush every bucket table into the HBM table (legacy),
 //       1 = emit records directly unless the bucket overflowed (then merge through HBM),
 //       2 = sample mode: emit table keys, drop misses (approximate counts for the dictionary)
@@ -174,14 +177,12 @@ void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s);
 void launch_sample_gather(const uint8_t* in, uint64_t n, uint64_t win, uint64_t stride, uint32_t nwin, uint8_t* dst,
                           hipStream_t s);
 // Build the dictionary image from sample records ordered by descending count.
-// hot: the count slots of the 4 hottest placed keys; choices: 1 or 2 candidate sets per key.
-void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, uint32_t* hot,
-                       int choices, hipStream_t s);
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s);
 // Sort keys for the dictionary build: ~count (u32) of each record.
 void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t s);
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
-                     hipStream_t s);
+                     hipStream_t s, uint64_t cbeg = 0, uint64_t cend = ~0ull);
 // grep line resolution, linear in the input (mrgpu_map.hip): t.hits (sorted) ->
 // one (start, end) pair per matching line occurrence in t.lines (ctr->nlines),
 // hits in lines longer than a lane's scan window to t.defer (ctr->ndefer).

@@ -110,8 +110,9 @@ __device__ __attribute__((noinline)) uint32_t first_hit_per_line(uint32_t hit, u
     return keep;
 }
 
-__global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t nchunks,
-                                                            const uint8_t* __restrict__ pat, uint32_t plen, Tables t) {
+__global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t cbeg,
+                                                            uint64_t nchunks, const uint8_t* __restrict__ pat,
+                                                            uint32_t plen, Tables t) {
     __shared__ uint4 ring[kWavesPerWG][2][kChunk / 16];
     __shared__ uint8_t P[kAhead + 16];
     __shared__ unsigned long long mbuf[kWavesPerWG][kGrepBuf];  // buffered match positions
@@ -141,7 +142,7 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
     const uint32_t p0 = P[0], p1 = plen > 1 ? P[1] : 0u;
     const uint32_t rep0 = p0 * 0x01010101u, rep1 = p1 * 0x01010101u;
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
-    const uint64_t c0 = (uint64_t)blockIdx.x * kWavesPerWG + wv;
+    const uint64_t c0 = cbeg + (uint64_t)blockIdx.x * kWavesPerWG + wv;
     const uint32_t slot0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ring[wv][0];
     const uint64_t cstep = stride * kGrepOwn;
     grep_dma(in, n, c0 * kGrepOwn, lane, slot0);
@@ -584,13 +585,22 @@ __global__ void insert_recs_kernel(Recs src, Tables t) {
     }
 }
 
+// Zero everything a map run accumulates into, in one launch (each separate
+// hipMemsetAsync is its own ~4 us dispatch): the counters, the bucket flags,
+// the spill stream lengths, the LongTable, and the ShortTable unless known clean.
 __global__ void clear_tables_kernel(Tables t, bool short_table) {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i0 < sizeof(Counters) / 8) reinterpret_cast<unsigned long long*>(t.ctr)[i0] = 0;
+    if (t.bflag)
+        for (uint64_t i = i0; i < (uint64_t)kSpillBuckets; i += stride) t.bflag[i] = 0;
+    if (t.sp.counts) {  // counts and counts8 are contiguous (make_tables)
+        const uint64_t nc = 2ull * kSpillBuckets * t.sp.nwg;
+        for (uint64_t i = i0; i < nc; i += stride) t.sp.counts[i] = 0;
+    }
     if (short_table)
-        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= t.sh_mask; i += stride)
-            t.sh[i] = ShortSlot{0, kUnwritten, 0, 0};
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= t.lo_mask; i += stride)
-        t.lo[i] = LongSlot{0, nullptr, 0, 0};
+        for (uint64_t i = i0; i <= t.sh_mask; i += stride) t.sh[i] = ShortSlot{0, kUnwritten, 0, 0};
+    for (uint64_t i = i0; i <= t.lo_mask; i += stride) t.lo[i] = LongSlot{0, nullptr, 0, 0};
 }
 
 // ------------------------------------------------------------ launchers
@@ -614,10 +624,7 @@ __global__ void clear_long_kernel(Tables t) {
 void clear_long_table(const Tables& t, hipStream_t s) { clear_long_kernel<<<2048, 256, 0, s>>>(t); }
 
 void clear_tables(const Tables& t, bool short_table, hipStream_t s) {
-    hipMemsetAsync(t.ctr, 0, sizeof(Counters), s);
-    if (t.bflag) hipMemsetAsync(t.bflag, 0, kSpillBuckets * sizeof(uint32_t), s);
-    // spill stream lengths: a map launch writes those of its own workgroups only
-    if (t.sp.counts) hipMemsetAsync(t.sp.counts, 0, (size_t)2 * kSpillBuckets * t.sp.nwg * sizeof(uint32_t), s);
+    static_assert(sizeof(Counters) % 8 == 0 && sizeof(Counters) / 8 <= 256, "counters cleared by the first threads");
     clear_tables_kernel<<<2048, 256, 0, s>>>(t, short_table);
 }
 
@@ -627,13 +634,15 @@ void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables
 }
 
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
-                     hipStream_t s) {
-    const uint64_t nchunks = (n + kGrepOwn - 1) / kGrepOwn;
-    if (nchunks == 0 || plen == 0) return;
-    uint64_t g = (nchunks + kWavesPerWG - 1) / kWavesPerWG;
+                     hipStream_t s, uint64_t cbeg, uint64_t cend) {
+    static_assert(kGrepOwn == kGrepChunkBytes, "chunk size");
+    uint64_t nchunks = (n + kGrepOwn - 1) / kGrepOwn;
+    if (cend < nchunks) nchunks = cend;
+    if (nchunks <= cbeg || plen == 0) return;
+    uint64_t g = (nchunks - cbeg + kWavesPerWG - 1) / kWavesPerWG;
     const uint64_t gmax = (uint64_t)grid * 2;
     if (g > gmax) g = gmax;
-    grep_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, d_pat, plen, t);
+    grep_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, cbeg, nchunks, d_pat, plen, t);
 }
 
 void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int grid, hipStream_t s) {

@@ -153,17 +153,17 @@ __device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uin
 constexpr int dma_policy(uint32_t mode) { return (mode & 0x100) ? 0 : (mode & 0x4000) ? 2 : (mode & 0x8000) ? 3 : 1; }
 
 template <uint32_t mode, int NW = kWavesPerWG>
-__global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t nchunks,
-                                                          uint32_t ctail, Tables t, LetterTables lt) {
+__global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t cbeg,
+                                                          uint32_t cend, uint32_t ctail, int resume, Tables t,
+                                                          LetterTables lt) {
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
     // 1 = stream input only, 2 = tokenize only (no per-word work), 4 = per-word
     // key extraction without the dictionary, 16 = no spill append (misses dropped),
     // 32 = spill cursors but no stores, 8 = dictionary counters not updated;
     // 0x100 / 0x4000 / 0x8000 (exact) = input loads with the default policy /
-    // sc1 / sc0 sc1 instead of nt.  Exact variants: 0x20000 = single-choice
-    // dictionary lookup (one set read; the dictionary is then built single
-    // choice), 0x40000 = the 4 hottest keys counted by ballots into SGPRs,
-    // 0x80000 = key bytes by three aligned 8-byte LDS reads (not five dword reads)
+    // sc1 / sc0 sc1 instead of nt.  (Measured and removed, DESIGN.md §6: the 4
+    // hottest keys counted by ballots into SGPRs; key bytes by three aligned
+    // 8-byte reads; a single-choice dictionary lookup.)
     __shared__ MapLds L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
@@ -178,8 +178,17 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // NW (waves per workgroup) < kWavesPerWG only for the occupancy benchmark (map_mode 0x1000 / 0x2000)
     constexpr uint32_t kT = NW * kWave;
     for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kT) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
-    for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kT) dcnt[i] = 0;
-    for (uint32_t b = tid; b < 2u * kSpillBuckets + kWave; b += kT) curs[b] = 0;
+    // chunks [cbeg, cend) of the split; resume: an earlier launch mapped chunks
+    // before cbeg (host input streamed piece by piece), so this workgroup's spill
+    // cursors and dictionary counts continue from what it wrote
+    for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kT)
+        dcnt[i] = resume && use_dict && i < (uint32_t)kDictSlots ? t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i] : 0u;
+    for (uint32_t b = tid; b < 2u * kSpillBuckets + kWave; b += kT) {
+        uint32_t v = 0;
+        if (resume && b < (uint32_t)kSpillBuckets) v = t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
+        else if (resume && b < 2u * kSpillBuckets) v = t.sp.counts[(uint64_t)(b - kSpillBuckets) * t.sp.nwg + blockIdx.x];
+        curs[b] = v;
+    }
     if (tid < 17 * 4) {  // byte masks: dword d of kmask[len] keeps clamp(len - 4d, 0, 4) bytes
         const int nb = min(max((int)(tid >> 2) - 4 * (int)(tid & 3), 0), 4);
         ((uint32_t*)L.kmask)[tid] = nb == 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
@@ -188,7 +197,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 
     // chunk indices are 32-bit (the launcher checks): scalar compares, no 64-bit VALU ones
     const uint32_t stride = gridDim.x * NW;
-    const uint32_t c0 = blockIdx.x * NW + wv;
+    const uint32_t c0 = cbeg + blockIdx.x * NW + wv;
     const uint32_t sub = (uint32_t)t.sp.sub_keys, sub8 = (uint32_t)t.sp.sub8;
     // this workgroup's spill streams: [g][bucket][sub] (a workgroup's stores stay
     // within a few MiB, so they hit few TLB pages; mrgpu_internal.h Spill)
@@ -200,11 +209,6 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         0x00020000);
     uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
     const uint32_t ring0 = lds_addr(L.ring[wv][0]);
-    // mode 0x40000: dictionary slots of the hottest keys, counted in SGPRs (never a real slot: ~0u)
-    uint32_t hot_slot[4] = {~0u, ~0u, ~0u, ~0u}, hot_cnt[4] = {0, 0, 0, 0};
-    if constexpr ((mode & 0x40000) != 0)
-        if (use_dict && t.dict_hot)
-            for (int k = 0; k < 4; k++) hot_slot[k] = __builtin_amdgcn_readfirstlane(t.dict_hot[k]);
 
     // prologue: chunk c0 landed before the loop, chunk c0 + stride in flight
     // byte offsets advance by addition (64-bit scalar multiplies per iteration are not free)
@@ -214,7 +218,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn + cstep, lane, ring0 + kSlotBytes);
     uint32_t k = 0;  // ring slot of the current chunk
     uint64_t cs = (uint64_t)c0 * kOwn;  // the current chunk's first own byte = slot byte 16 (slot byte i = input cs - 16 + i)
-    for (uint32_t c = c0; c < nchunks; c += stride, cs += cstep, k = k == kRing - 1 ? 0 : k + 1) {
+    for (uint32_t c = c0; c < cend; c += stride, cs += cstep, k = k == kRing - 1 ? 0 : k + 1) {
         wait_vmem_iter();  // chunk c's DMA (issued two iterations ago) has landed
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
         lds_uint4* b4 = (lds_uint4*)buf;
@@ -292,21 +296,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     u32x4 km[kBatch];  // the key's byte mask, from the length (same round trip)
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        if constexpr ((mode & 0x80000) != 0) {
-                            // three aligned 8-byte reads [s & ~7, +24): the lanes' addresses
-                            // rise with the lane, so a 32-lane group spans < 64 banks
-                            const lds_u64* p8 = (const lds_u64*)(buf + ((e[u] & 0x3FFu) & ~7u));
-                            const uint64_t q0 = p8[0], q1 = p8[1], q2 = p8[2];
-                            const bool odd = (e[u] & 4u) != 0;
-                            g0[u] = odd ? (uint32_t)(q0 >> 32) : (uint32_t)q0;
-                            g1[u] = odd ? (uint32_t)q1 : (uint32_t)(q0 >> 32);
-                            g2[u] = odd ? (uint32_t)(q1 >> 32) : (uint32_t)q1;
-                            g3[u] = odd ? (uint32_t)q2 : (uint32_t)(q1 >> 32);
-                            g4[u] = odd ? (uint32_t)(q2 >> 32) : (uint32_t)q2;
-                        } else {
-                            const lds_u32* p4 = (const lds_u32*)(buf + ((e[u] & 0x3FFu) & ~3u));
-                            g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
-                        }
+                        const lds_u32* p4 = (const lds_u32*)(buf + ((e[u] & 0x3FFu) & ~3u));
+                        g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
                         km[u] = kmask4[min(e[u] >> 10, 16u)];
                     }
                     uint64_t k0[kBatch], k1[kBatch];
@@ -352,8 +343,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         for (int u = 0; u < kBatch; u++) {
                             dict_sets(hh[u], k1[u] != 0, s1[u], s2[u]);
                             A[u] = dset[s1[u]];
-                            if constexpr ((mode & 0x20000) == 0) B[u] = dset[s2[u]];
-                            else B[u] = (u32x4){0, 0, 0, 0};  // single choice: the second set is never read
+                            B[u] = dset[s2[u]];
                         }
                         __builtin_amdgcn_sched_barrier(0);  // all 2 * kBatch set reads in flight before the compares
         #pragma unroll
@@ -382,19 +372,6 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             const uint32_t wb = __builtin_amdgcn_inverse_ballot_w64(~mMid & ~mB0) ? 1u : 0u;
                             const uint32_t slot = __builtin_amdgcn_inverse_ballot_w64(mHa) ? 2 * s1[u] + wa : 2 * s2[u] + wb;
                             bool cnt_lds = hit[u];
-                            if constexpr ((mode & 0x40000) != 0) {
-                                // the hottest keys ("the" alone is ~10 % of C2's words) are counted
-                                // with ballots into SGPRs: in an LDS add, lanes of one address serialize
-                                const uint64_t mSlot0 = __ballot(slot == hot_slot[0]) & mHit[u];
-                                const uint64_t mSlot1 = __ballot(slot == hot_slot[1]) & mHit[u];
-                                const uint64_t mSlot2 = __ballot(slot == hot_slot[2]) & mHit[u];
-                                const uint64_t mSlot3 = __ballot(slot == hot_slot[3]) & mHit[u];
-                                hot_cnt[0] += (uint32_t)__popcll(mSlot0);
-                                hot_cnt[1] += (uint32_t)__popcll(mSlot1);
-                                hot_cnt[2] += (uint32_t)__popcll(mSlot2);
-                                hot_cnt[3] += (uint32_t)__popcll(mSlot3);
-                                cnt_lds = __builtin_amdgcn_inverse_ballot_w64(mHit[u] & ~(mSlot0 | mSlot1 | mSlot2 | mSlot3));
-                            }
                             if constexpr ((mode & 8) != 0) cnt_lds = false;  // ablation: counters not updated
                             const uint32_t ci = cnt_lds ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
                             __hip_atomic_fetch_add(&dcnt[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -508,24 +485,23 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         dma_for_chunk<dma_policy(mode)>(in, n, cs + 2 * cstep, lane, ring0 + kf * kSlotBytes);
     }
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
-    if constexpr ((mode & 0x40000) != 0)
-        if (lane == 0)
-            for (int k = 0; k < 4; k++)
-                if (hot_cnt[k]) __hip_atomic_fetch_add(&dcnt[hot_slot[k]], hot_cnt[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
 
     __syncthreads();
     unsigned long long spilled = 0, hits = 0;
-    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kT) {
+    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kT) {  // (this launch's share: minus the resumed values)
         const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[kSpillBuckets + b], sub);
-        t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x] = k;
-        t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x] = k8;
-        spilled += k + k8;
+        uint32_t* p16 = &t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x];
+        uint32_t* p8 = &t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
+        spilled += k + k8 - (resume ? *p16 + *p8 : 0u);
+        *p16 = k;
+        *p8 = k8;
     }
     if (use_dict)
         for (uint32_t i = tid; i < (uint32_t)kDictSlots; i += kT) {
             const uint32_t v = dcnt[i];
-            t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i] = v;
-            hits += v;
+            uint32_t* pd = &t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i];
+            hits += v - (resume ? *pd : 0u);
+            *pd = v;
         }
     if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
     block_add4<NW>(&t.ctr->spilled, &t.ctr->dict_hits, &t.ctr->spill_ovf, &t.ctr->chunks_utf8, spilled, hits,
@@ -1107,8 +1083,7 @@ __global__ void dict_cands_kernel(Recs r, const uint32_t* order, uint64_t lim, u
 // One workgroup places the candidates in order, 1024 at a time, each into the
 // first of its two sets with a free way; a key whose two sets are full stays out
 // (it is then counted through the spill path).
-__global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uint64_t lim, uint4* dict, uint32_t* hot,
-                                                            int choices) {
+__global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uint64_t lim, uint4* dict) {
     __shared__ uint4 S[kDictSets];
     __shared__ uint32_t fill[kDictSets];
     const uint32_t tid = threadIdx.x;
@@ -1116,7 +1091,6 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uin
         S[i] = make_uint4(0, 0, 0, 0);
         fill[i] = 0;
     }
-    if (hot && tid < 4) hot[tid] = ~0u;
     __syncthreads();
     uint4 nx = tid < lim ? cand[tid] : make_uint4(0, 0, 0, 0);
     for (uint64_t base = 0; base < lim; base += 1024) {
@@ -1130,13 +1104,11 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uin
             dict_sets(fold32(c.x, c.y, c.z, c.w), mid, s1, s2);
             const uint32_t ways = mid ? 1u : 2u;
             uint32_t s = s1, w = atomicAdd(&fill[s1], 1u);
-            if (w >= ways && choices > 1) { s = s2; w = atomicAdd(&fill[s2], 1u); }
+            if (w >= ways) { s = s2; w = atomicAdd(&fill[s2], 1u); }
             if (w < ways) {
                 if (mid) S[s] = c;
                 else if (w == 0) { S[s].x = c.x; S[s].y = c.y; }
                 else { S[s].z = c.x; S[s].w = c.y; }
-                // the 4 hottest candidates' count slots (way w of set s: slot 2 s + w)
-                if (base == 0 && tid < 4 && hot) hot[tid] = 2 * s + w;
             }
         }
         __syncthreads();
@@ -1153,11 +1125,15 @@ uint32_t wc_map_grid(uint64_t n, int grid) {
     return (uint32_t)(g ? g : 1);
 }
 
-bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode, hipStream_t s) {
+bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode, hipStream_t s,
+                   uint64_t cbeg, uint64_t cend, bool resume) {
     const uint64_t nch = (n + kOwn - 1) / kOwn;
     if (nch == 0) return true;
     if (nch + (uint64_t)kMaxMapWGs * kWavesPerWG * 3 >= (1ull << 32)) return false;  // 32-bit chunk indices
-    const uint32_t nchunks = (uint32_t)nch;
+    if (cend > nch) cend = nch;
+    if (cbeg >= cend) return true;
+    const uint32_t cb = (uint32_t)cbeg, ce = (uint32_t)cend;
+    const int rs = resume ? 1 : 0;
     // first chunk whose window [cs - 16, cs + 1008) reaches the dword holding the
     // split's last n % 4 bytes (the range check zero-fills that partial dword)
     const uint64_t n4 = n & ~3ull, reach = kSlotBytes - kBack;
@@ -1165,15 +1141,14 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     const uint64_t g = wc_map_grid(n, grid);
     switch (mode) {
 #define MRG_MAP_MODE(M) \
-    case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
+    case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;
         MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(8) MRG_MAP_MODE(16) MRG_MAP_MODE(32)
-        MRG_MAP_MODE(0x100) MRG_MAP_MODE(0x4000) MRG_MAP_MODE(0x8000) MRG_MAP_MODE(0x20000) MRG_MAP_MODE(0x40000)
-        MRG_MAP_MODE(0x60000) MRG_MAP_MODE(0x80000) MRG_MAP_MODE(0xE0000)
+        MRG_MAP_MODE(0x100) MRG_MAP_MODE(0x4000) MRG_MAP_MODE(0x8000)
 #undef MRG_MAP_MODE
         // occupancy benchmark: 8 or 12 waves per workgroup (results stay exact)
-        case 0x1000: wc_map_kernel<0, 8><<<(unsigned)g, 8 * kWave, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
-        case 0x2000: wc_map_kernel<0, 12><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
-        default: wc_map_kernel<0><<<(unsigned)g, kThreads, 0, s>>>(in, n, nchunks, ctail, t, lt); break;
+        case 0x1000: wc_map_kernel<0, 8><<<(unsigned)g, 8 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;
+        case 0x2000: wc_map_kernel<0, 12><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;
+        default: wc_map_kernel<0><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;
     }
     return true;
 }
@@ -1210,11 +1185,10 @@ void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t 
 }
 
 // cand: scratch for kDictCands uint4
-void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, uint32_t* hot,
-                       int choices, hipStream_t s) {
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s) {
     const uint64_t lim = n < kDictCands ? n : kDictCands;
     if (lim) dict_cands_kernel<<<(unsigned)((lim + 255) / 256), 256, 0, s>>>(r, order, lim, cand);
-    dict_build_kernel<<<1, 1024, 0, s>>>(cand, lim, dict, hot, choices);
+    dict_build_kernel<<<1, 1024, 0, s>>>(cand, lim, dict);
 }
 
 }  // namespace mrg

@@ -526,3 +526,29 @@ def test_exchange_group_c5_shape():
     for i in range(P):
         for r in range(R):
             assert outs[i][r] == (want[r] if r % P == i else b""), f"rank {i} partition {r}"
+
+
+@pytest.mark.parametrize("app", ["wc", "grep:distributed"])
+def test_host_input_streamed_in_pieces(ctx, app):
+    """Host input copied piece by piece on a second stream while the map runs
+    over the resident pieces: 1 MiB-ish pieces over a
+    ~24 MB split (dictionary on, words / lines across every piece seam) equal the
+    oracle, as does the same split as device input."""
+    if app == "wc":
+        files = cases.synthetic(C.KIND_UTF8, 50000, [9_000_001, 8_000_000, 7_000_003], 71, 0.001)
+    else:
+        files = cases.synthetic_grep(50000, [9_000_001, 8_000_000, 7_000_003], 72, match_rate=0.02)
+    joined = b"\n".join(files)
+    a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
+    pat = b"" if app == "wc" else b"distributed"
+    want = O.c_partitioned(app, files, 10)
+    ctx.set_option("ingest_piece", 1 << 20)
+    ctx.set_option("ingest_min", 1 << 20)
+    ctx.set_option("dict_min_bytes", 1)
+    try:
+        assert ctx.run_job(a, joined, pattern=pat, nreduce=10) == want
+        assert ctx.stats()["staged_bytes"] == len(joined)
+    finally:
+        ctx.set_option("ingest_piece", 0)
+        ctx.set_option("ingest_min", 0)
+        ctx.set_option("dict_min_bytes", 0)
