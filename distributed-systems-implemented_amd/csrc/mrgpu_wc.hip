@@ -741,6 +741,23 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
             if (jj < js) part_range(sid, b0);
             row = jj < js ? gbase[sid % kAggSegs] + b0 : 0ull;
         }
+        if constexpr (!kMid && (kAggUnroll % 2) == 0) {
+            if (!gbase) {
+                // round 0's 8-byte records: two per 16-byte load (a map stream starts
+                // 16-byte aligned and a block at a multiple of kAggBlock records);
+                // 8-byte loads run at ~0.6x the 16-byte rate (MI355X_MICROARCH.md)
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll / 2; u++) {
+                    const uint32_t i = o + 2 * (u * kWave + lane);
+                    uint4 v = make_uint4(0, 0, 0, 0);
+                    if (jj < js && i < c) v = ((const uint4*)((const uint64_t*)pool_b + row + o))[u * kWave + lane];
+                    if (i + 1 >= c) v.z = v.w = 0;  // the odd record past the stream's end
+                    r[2 * u] = make_uint4(v.x, v.y, 0, 0);
+                    r[2 * u + 1] = make_uint4(v.z, v.w, 0, 0);
+                }
+                return;
+            }
+        }
 #pragma unroll
         for (uint32_t u = 0; u < kAggUnroll; u++) {
             const uint32_t i = o + u * kWave + lane;
