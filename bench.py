@@ -441,6 +441,7 @@ def main():
             "spill_region_full_words": int(last["spill_ovf"]),
             "aggregator_miss_words": int(last["agg_miss"]),
             "aggregation_rounds": int(last["agg_rounds"]),
+            "spill_buckets": int(last["spill_buckets"]),
             "output_bytes": int(last["output_bytes"]),
             "checks": checks,
             "pcie_inclusive": pcie,

@@ -173,6 +173,13 @@ struct mrg_ctx {
     uint64_t dict_sample_bytes = 16ull << 20;  // C2: 16 vs 64 MB loses 0.13% of dictionary hits, halves the build
     uint64_t spill_sub_keys = 0, spill_sub8 = 0;
     uint32_t spill_nwg = 1;
+    // Spill buckets of the current layout and of the next wc split.  2048 when
+    // the previous split's aggregated keys would not fit 512 buckets' LDS tables
+    // in one round (C5-like splits: 1e7 keys), else 512; option spill_buckets
+    // fixes it (0 = this feedback rule).
+    uint32_t spill_nb = kSpillBuckets, next_nb = kSpillBuckets;
+    int spill_buckets_opt = 0;
+    uint64_t spill_hi_keys = 6000ull * kSpillBuckets;  // aggregated keys above which the next split uses 2048
     int64_t spill_force_sub = 0;
     int map_mode = 0;  // benchmark ablation of wc_map_kernel phases (0 = normal)
     // mrg_run_job without the shuffle even with a communicator (bench.py's
@@ -259,11 +266,12 @@ static Tables make_tables(mrg_ctx* c) {
     t.sp.pool = (uint4*)c->spool.p;
     t.sp.sub_keys = c->spill_sub_keys;
     t.sp.sub8 = c->spill_sub8;
-    t.sp.pool8 = c->spool.p ? (uint64_t*)((uint4*)c->spool.p + c->spill_sub_keys * kSpillBuckets * c->spill_nwg)
+    t.sp.pool8 = c->spool.p ? (uint64_t*)((uint4*)c->spool.p + c->spill_sub_keys * c->spill_nb * c->spill_nwg)
                             : nullptr;
     t.sp.nwg = c->spill_nwg;
+    t.sp.nb = c->spill_nb;
     t.sp.counts = (uint32_t*)c->spmeta.p;
-    t.sp.counts8 = c->spmeta.p ? t.sp.counts + (size_t)kSpillBuckets * c->spill_nwg : nullptr;
+    t.sp.counts8 = c->spmeta.p ? t.sp.counts + (size_t)c->spill_nb * c->spill_nwg : nullptr;
     t.sp.seg_off8 = t.sp.seg_off16 = nullptr;
     t.sp.seg_n_in = nullptr;
     t.sp.seg_n_out = nullptr;
@@ -302,25 +310,28 @@ static Recs rec_view(mrg_ctx* c) {
 }
 
 // Spill pool for dictionary misses: 1.5 bytes of pool per input byte (C2
-// spills ~0.5 bytes of records per input byte), split into kSpillBuckets x nwg
+// spills ~0.5 bytes of records per input byte), split into spill_nb x nwg
 // streams of 16-byte records (0.75 B/B) and as many of 8-byte records (0.75 B/B),
 // times c->spill_scale when the dictionary sample shows a higher miss rate.
 // A stream that fills up sends the rest of its keys to the HBM table, so the
 // size only affects speed, never results.
 static int ensure_spill(mrg_ctx* c, uint64_t n) {
     const uint32_t nwg = wc_map_grid(n, c->grid);
-    uint64_t sub = (uint64_t)((double)((n - n / 4) / 16 / ((uint64_t)kSpillBuckets * nwg)) * c->spill_scale) + 64;
+    const uint64_t nb = c->spill_nb;
+    uint64_t sub = (uint64_t)((double)((n - n / 4) / 16 / (nb * nwg)) * c->spill_scale) + 64;
     sub = (sub + 63) & ~63ull;
     uint64_t sub8 = 2 * sub;
     if (c->spill_force_sub > 0) sub = sub8 = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
-    // stream offsets are 24-bit products in the map kernel (b * sub): 2^23 records per
-    // (workgroup, bucket) stream is a 1 TB split at 8 B per record and 512 streams
-    if (sub8 >= (1ull << 23)) return fail(c, MRG_EINVAL, "split too large for the spill layout (%llu bytes)", (unsigned long long)n);
+    // a workgroup's streams are addressed by 32-bit byte offsets in the map kernel
+    // ((b * sub + pos) * 16 < 2^32): 2^32 bytes of 16-byte and as many of 8-byte
+    // streams per workgroup is a ~1 TB split at scale 1 with 512 workgroups
+    if (nb * std::max(sub * 16, sub8 * 8) >= (1ull << 32))
+        return fail(c, MRG_EINVAL, "split too large for the spill layout (%llu bytes)", (unsigned long long)n);
     c->spill_nwg = nwg;
     c->spill_sub_keys = sub;
     c->spill_sub8 = sub8;
-    HCHK(c, c->spool.ensure_grow((sub * sizeof(uint4) + sub8 * sizeof(uint64_t)) * kSpillBuckets * nwg));
-    HCHK(c, c->spmeta.ensure((size_t)2 * kSpillBuckets * nwg * sizeof(uint32_t)));
+    HCHK(c, c->spool.ensure_grow((sub * sizeof(uint4) + sub8 * sizeof(uint64_t)) * nb * nwg));
+    HCHK(c, c->spmeta.ensure((size_t)2 * nb * nwg * sizeof(uint32_t)));
     return MRG_OK;
 }
 
@@ -328,7 +339,7 @@ static int ensure_tables(mrg_ctx* c) {
     const void* old = c->sh.p;
     HCHK(c, c->sh.ensure(sizeof(ShortSlot) << c->sh_log2));
     if (c->sh.p != old) c->sh_clean = false;  // fresh memory is not zeroed
-    HCHK(c, c->bflag.ensure(kSpillBuckets * sizeof(uint32_t)));
+    HCHK(c, c->bflag.ensure(kSpillBucketsHi * sizeof(uint32_t)));
     const size_t lo_bytes = sizeof(LongSlot) << c->lo_log2_cur;
     if (c->lo.cap > 4 * lo_bytes && c->lo.cap > (256u << 20)) c->lo.release();  // a past grep job's big table
     HCHK(c, c->lo.ensure(lo_bytes));
@@ -457,15 +468,16 @@ static void print_stamps(mrg_ctx* c, const char* what, uint32_t nblocks, uint32_
     fprintf(stderr, "\n");
     if (off == 0 && c->spmeta.p) {  // bucket sizes (aggregator stamps)
         const uint32_t nwg = c->spill_nwg;
-        std::vector<uint32_t> cnt((size_t)2 * kSpillBuckets * nwg);
+        const uint32_t nb = c->spill_nb;
+        std::vector<uint32_t> cnt((size_t)2 * nb * nwg);
         hipMemcpy(cnt.data(), c->spmeta.p, cnt.size() * 4, hipMemcpyDeviceToHost);
-        std::vector<uint64_t> tot(kSpillBuckets, 0);
-        for (uint32_t b = 0; b < kSpillBuckets; b++)
-            for (uint32_t g = 0; g < nwg; g++) tot[b] += cnt[(size_t)b * nwg + g] + cnt[(size_t)(kSpillBuckets + b) * nwg + g];
+        std::vector<uint64_t> tot(nb, 0);
+        for (uint32_t b = 0; b < nb; b++)
+            for (uint32_t g = 0; g < nwg; g++) tot[b] += cnt[(size_t)b * nwg + g] + cnt[(size_t)(nb + b) * nwg + g];
         std::vector<uint64_t> so(tot);
         std::sort(so.begin(), so.end());
         fprintf(stderr, "[mrg stamps]   bucket records min %llu p50 %llu max %llu; slowest buckets' records:",
-                (unsigned long long)so[0], (unsigned long long)so[kSpillBuckets / 2], (unsigned long long)so.back());
+                (unsigned long long)so[0], (unsigned long long)so[nb / 2], (unsigned long long)so.back());
         for (uint32_t k = 0; k < 5; k++) fprintf(stderr, " %llu", (unsigned long long)tot[ends[nblocks - 1 - k].second]);
         fprintf(stderr, "\n");
     }
@@ -513,7 +525,7 @@ static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win
     launch_wc_agg(t, c->map_mode & 512, 2, false, c->s);
     if (with_dict) launch_dict_emit(t, g, c->s);
     HCHK(c, hipGetLastError());
-    print_stamps(c, with_dict ? "sample agg (level 2)" : "sample agg (level 1)", kSpillBuckets);
+    print_stamps(c, with_dict ? "sample agg (level 2)" : "sample agg (level 1)", c->spill_nb);
     if ((rc = read_counters(c))) return rc;
     *nrec_out = std::min<uint64_t>(c->h_ctr->nrec, c->rec_cap);
     if (spill_rate) *spill_rate = (double)(c->h_ctr->spilled + c->h_ctr->spill_ovf) / (double)sn;
@@ -588,7 +600,7 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
 // in the HBM table.  Typical splits finish in round 0; 1e7-key splits need a
 // few rounds, each re-reading only the keys still unsettled.
 static int aggregate_rounds(mrg_ctx* c, Tables& t) {
-    constexpr uint64_t E = (uint64_t)kSpillBuckets * kAggSegs;
+    const uint64_t E = (uint64_t)c->spill_nb * kAggSegs;
     const size_t meta = 2 * E * 4 + 2 * (E + 1) * 8 + 2 * (2 * E * 4) + 64;
     HCHK(c, c->segmeta.ensure(meta));
     uint32_t* tmp = (uint32_t*)c->segmeta.p;
@@ -725,6 +737,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
                   const uint8_t* host = nullptr) {
     int rc;
     c->lo_log2_cur = c->lo_log2;
+    c->spill_nb = c->spill_buckets_opt ? (uint32_t)c->spill_buckets_opt : c->next_nb;
     Ingest ing;
     if (host && (rc = ingest_start(c, ing, host, (uint8_t*)in, len))) return rc;
     if ((rc = ensure_spill(c, len))) return rc;
@@ -766,9 +779,9 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             return fail(c, MRG_EINVAL, "split too large for 32-bit chunk indices (%llu bytes)", (unsigned long long)len);
         }
         HCHK(c, hipEventRecord(c->ev[1], c->s));
-        print_stamps(c, "map", nwg, kSpillBuckets);
+        print_stamps(c, "map", nwg, c->spill_nb);
         if ((rc = aggregate_rounds(c, t))) return rc;
-        print_stamps(c, "agg", kSpillBuckets);
+        print_stamps(c, "agg", c->spill_nb);
         if (have_dict) launch_dict_emit(t, nwg, c->s);
         HCHK(c, hipEventRecord(c->ev[8], c->s));
         HCHK(c, hipGetLastError());
@@ -783,6 +796,15 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         if (nlist && (rc = read_counters(c))) return rc;
         Counters h = *c->h_ctr;
         if (h.status & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", h.status);
+        {
+            // Bucket count for the next split (a worker's map tasks are alike):
+            // the aggregated keys (records minus the dictionary's) against what
+            // 512 buckets' round-0 tables hold (AggLdsBig: ~8 K short + 2 K mid
+            // keys each), with hysteresis.
+            const uint64_t agg_keys = h.nrec > (uint64_t)kDictSlots ? h.nrec - kDictSlots : 0;
+            if (agg_keys > c->spill_hi_keys) c->next_nb = kSpillBucketsHi;
+            else if (agg_keys < c->spill_hi_keys / 3 * 2) c->next_nb = kSpillBuckets;
+        }
         if (grow_on_overflow(c, h.status & (kStShortFull | kStLongFull | kStRecFull))) continue;
         if (h.long_bytes + 16 > c->recarena.cap) {  // the arena is written by collect below
             HCHK(c, c->recarena.ensure_cached(h.long_bytes + 16, c->device));
@@ -816,6 +838,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         c->stats.spill_ovf = h.spill_ovf;
         c->stats.agg_miss = h.agg_miss;
         c->stats.agg_rounds = (uint64_t)__builtin_popcountll(h.round_mask);
+        c->stats.spill_buckets = c->spill_nb;
         c->stats.dict_hits = h.dict_hits;
         c->stats.distinct_keys = h.nrec;
         c->stats.long_keys = h.nlong_rec;
@@ -1029,6 +1052,10 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "agg_carry_min")) c->agg_carry_min = v > 0 ? (uint32_t)v : v < 0 ? 0u : 64u;  // -1: always carry
     else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
     else if (!strcmp(name, "dict_warm")) c->dict_warm = v >= 0;  // -1: always build the level-1 dictionary
+    else if (!strcmp(name, "spill_buckets")) {  // 0: chosen per split (feedback), else 512 or 2048
+        if (v != 0 && v != kSpillBuckets && v != kSpillBucketsHi) return fail(c, MRG_EINVAL, "spill_buckets: 0, 512 or 2048");
+        c->spill_buckets_opt = (int)v;
+    } else if (!strcmp(name, "spill_hi_keys")) c->spill_hi_keys = v > 0 ? (uint64_t)v : 6000ull * kSpillBuckets;
     else if (!strcmp(name, "dict_min_bytes")) c->dict_min_bytes = v > 0 ? (uint64_t)v : (32ull << 20);
     else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);
     else if (!strcmp(name, "rec_cap")) c->rec_cap = v > 0 ? (uint64_t)v : (1u << 21);

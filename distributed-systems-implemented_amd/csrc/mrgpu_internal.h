@@ -63,34 +63,38 @@ struct Counters {
     unsigned long long pad[1];
 };
 
-// Spill of dictionary misses, hash-partitioned into kSpillBuckets buckets.
+// Spill of dictionary misses, hash-partitioned into nb buckets (kSpillBuckets,
+// or kSpillBucketsHi for high-cardinality splits whose distinct keys would not
+// fit a bucket's LDS table in one aggregation round).
 // Every (map workgroup g, bucket b) pair owns a fixed stream of `sub_keys`
-// 16-B keys {k0,k1} at pool[(g*kSpillBuckets + b)*sub_keys] (a workgroup's
+// 16-B keys {k0,k1} at pool[(g*nb + b)*sub_keys] (a workgroup's
 // streams are contiguous: its scattered appends touch few TLB pages); the
 // workgroup appends with an LDS cursor (no HBM atomics, no barriers) and
 // records the stream length in counts[b*nwg + g].  Keys beyond sub_keys go to
 // the HBM table instead.
 constexpr int kSpillBuckets = 512;
+constexpr int kSpillBucketsHi = 2048;
 constexpr int kMaxMapWGs = 512;   // map workgroups (spill streams per bucket) at most
 constexpr int kAggSegs = 8;       // aggregator waves per bucket = miss segments per bucket
 // Keys of at most 8 bytes (k1 == 0) are spilled as 8-byte records into pool8,
 // longer ones as 16-byte records into pool: the combiner's misses are mostly
 // tail words, and most words are short, so this roughly halves spill traffic.
 struct Spill {
-    uint4* pool;                     // [nwg][kSpillBuckets][sub_keys] 16-byte records (k0, k1)
-    uint64_t* pool8;                 // [nwg][kSpillBuckets][sub8] 8-byte records (k0; k1 == 0)
+    uint4* pool;                     // [nwg][nb][sub_keys] 16-byte records (k0, k1)
+    uint64_t* pool8;                 // [nwg][nb][sub8] 8-byte records (k0; k1 == 0)
     uint64_t sub_keys, sub8;         // stream capacities (records)
-    uint32_t* counts;                // [kSpillBuckets * nwg] records in each 16-byte stream
-    uint32_t* counts8;               // [kSpillBuckets * nwg] records in each 8-byte stream
+    uint32_t* counts;                // [nb * nwg] records in each 16-byte stream
+    uint32_t* counts8;               // [nb * nwg] records in each 8-byte stream
     uint32_t nwg;
+    uint32_t nb;                     // buckets: kSpillBuckets or kSpillBucketsHi
     // Multi-round bucket aggregation (high-cardinality buckets): the keys a round
     // could not hold in LDS are the next round's input.  Misses are appended to
     // per-(bucket, aggregator wave) segments; a segment's capacity is the records
     // that wave read in round 0 (a wave only ever re-reads its own segment), so the
     // offsets seg_off* are fixed over the rounds and the buffers ping-pong.
-    const uint64_t* seg_off8;        // [kSpillBuckets * kAggSegs + 1] 8-byte segment offsets (records)
-    const uint64_t* seg_off16;       // [kSpillBuckets * kAggSegs + 1] 16-byte segment offsets
-    const uint32_t* seg_n_in;        // [2][kSpillBuckets * kAggSegs] records in each input segment (8-B, 16-B)
+    const uint64_t* seg_off8;        // [nb * kAggSegs + 1] 8-byte segment offsets (records)
+    const uint64_t* seg_off16;       // [nb * kAggSegs + 1] 16-byte segment offsets
+    const uint32_t* seg_n_in;        // [2][nb * kAggSegs] records in each input segment (8-B, 16-B)
     uint32_t* seg_n_out;             // same layout: records appended this round
     const uint64_t* seg8_in;
     uint64_t* seg8_out;
@@ -142,7 +146,7 @@ struct Tables {
     Recs out;
     uint64_t out_cap;
     uint32_t nreduce;
-    uint32_t* bflag;        // [kSpillBuckets] nonzero: a key of the bucket went to the HBM table
+    uint32_t* bflag;        // [nb] nonzero: a key of the bucket went to the HBM table
     const uint4* dict;      // dictionary image [kDictSets] (nullptr: no dictionary)
     uint32_t* dict_cnt;     // [nwg][kDictSlots] per-map-workgroup dictionary counts
     unsigned long long* dbg;  // diagnostics (MRG_DEBUG_TIMES): per-workgroup s_memrealtime stamps, or nullptr
@@ -169,7 +173,7 @@ constexpr uint64_t kGrepChunkBytes = 960; // input bytes a grep map chunk owns
 // big: 1024-thread workgroups with twice the LDS table (later rounds)
 void launch_wc_agg(const Tables& t, int mode, int emit, bool big, hipStream_t s);
 // Segment layout of the multi-round aggregation (Spill::seg_off*) from the map's
-// stream counts; off8[E] / off16[E] (E = kSpillBuckets * kAggSegs) are the totals.
+// stream counts; off8[E] / off16[E] (E = nb * kAggSegs) are the totals.
 // tmp: 2 * E u32 of scratch.
 void launch_seg_layout(const Tables& t, uint32_t* tmp, uint64_t* off8, uint64_t* off16, hipStream_t s);
 void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s);

@@ -593,9 +593,9 @@ __global__ void clear_tables_kernel(Tables t, bool short_table) {
     const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i0 < sizeof(Counters) / 8) reinterpret_cast<unsigned long long*>(t.ctr)[i0] = 0;
     if (t.bflag)
-        for (uint64_t i = i0; i < (uint64_t)kSpillBuckets; i += stride) t.bflag[i] = 0;
+        for (uint64_t i = i0; i < (uint64_t)t.sp.nb; i += stride) t.bflag[i] = 0;
     if (t.sp.counts) {  // counts and counts8 are contiguous (make_tables)
-        const uint64_t nc = 2ull * kSpillBuckets * t.sp.nwg;
+        const uint64_t nc = 2ull * t.sp.nb * t.sp.nwg;
         for (uint64_t i = i0; i < nc; i += stride) t.sp.counts[i] = 0;
     }
     if (short_table)

@@ -45,16 +45,21 @@ constexpr uint64_t kOwn = 16 * kOwnLanes;  // 944
 constexpr int kRing = 3;                    // LDS slots per wave: current, in flight, free (the word list)
 static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot");
 
-struct alignas(16) MapLds {
+// NW waves per workgroup, NB spill buckets.  16 waves x 512 buckets is the
+// default; high-cardinality splits use 2048 buckets, whose cursors take the
+// LDS of 4 waves' rings (12 waves per workgroup).
+template <int NW, int NB>
+struct alignas(16) MapLdsT {
     uint4 dset[kDictSets];                      // dictionary image
     uint32_t dcnt[kDictSlots + kWave];          // dictionary counts of this workgroup (+ per-lane miss dummies)
-    uint8_t ring[kWavesPerWG][kRing][kSlotBytes];
-    // spill cursors: [0, 512) 8-byte streams, [512, 1024) 16-byte streams, then per-lane dummies for hits
-    uint32_t curs[2 * kSpillBuckets + kWave];
+    uint8_t ring[NW][kRing][kSlotBytes];
+    // spill cursors: [0, NB) 8-byte streams, [NB, 2 NB) 16-byte streams, then per-lane dummies for hits
+    uint32_t curs[2 * NB + kWave];
     unsigned long long red[4 * kWavesPerWG];    // block_add4 scratch
     uint4 kmask[17];                            // kmask[len]: the first len of 16 key bytes
 };
-static_assert(sizeof(MapLds) <= 160 * 1024, "map LDS budget");
+static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBuckets>) <= 160 * 1024, "map LDS budget");
+static_assert(sizeof(MapLdsT<12, kSpillBucketsHi>) <= 160 * 1024, "map LDS budget (high-cardinality)");
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
@@ -73,9 +78,10 @@ __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, ui
 
 // Spill bucket of a key: bits 11..19 of its hash (the bucket aggregator's table
 // indexes by the top bits, so a bucket's keys still spread over all its sets).
+template <int NB>
 __device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
-    static_assert(kSpillBuckets == 512, "bucket = 9 bits");
-    return (h >> 11) & 511u;
+    static_assert(NB == 512 || NB == 2048, "bucket = 9 or 11 bits");
+    return (h >> 11) & (uint32_t)(NB - 1);
 }
 
 // ------------------------------------------------------------ wc map kernel
@@ -152,7 +158,7 @@ __device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uin
 // sc1, 0x8000 = sc0 sc1)
 constexpr int dma_policy(uint32_t mode) { return (mode & 0x100) ? 0 : (mode & 0x4000) ? 2 : (mode & 0x8000) ? 3 : 1; }
 
-template <uint32_t mode, int NW = kWavesPerWG>
+template <uint32_t mode, int NW = kWavesPerWG, int NB = kSpillBuckets>
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t cbeg,
                                                           uint32_t cend, uint32_t ctail, int resume, Tables t,
                                                           LetterTables lt) {
@@ -164,7 +170,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // sc1 / sc0 sc1 instead of nt.  (Measured and removed, DESIGN.md §6: the 4
     // hottest keys counted by ballots into SGPRs; key bytes by three aligned
     // 8-byte reads; a single-choice dictionary lookup.)
-    __shared__ MapLds L;
+    __shared__ MapLdsT<NW, NB> L;
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the DMA operands
@@ -172,7 +178,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     lds_u32* dcnt = (lds_u32*)L.dcnt;
     lds_u32* curs = (lds_u32*)L.curs;
     const lds_uint4* kmask4 = (const lds_uint4*)L.kmask;
-    if (t.dbg && tid == 0) t.dbg[2 * (kSpillBuckets + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
+    if (t.dbg && tid == 0) t.dbg[2 * (NB + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
 
     const bool use_dict = t.dict != nullptr;
     // NW (waves per workgroup) < kWavesPerWG only for the occupancy benchmark (map_mode 0x1000 / 0x2000)
@@ -183,10 +189,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // cursors and dictionary counts continue from what it wrote
     for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kT)
         dcnt[i] = resume && use_dict && i < (uint32_t)kDictSlots ? t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i] : 0u;
-    for (uint32_t b = tid; b < 2u * kSpillBuckets + kWave; b += kT) {
+    for (uint32_t b = tid; b < 2u * NB + kWave; b += kT) {
         uint32_t v = 0;
-        if (resume && b < (uint32_t)kSpillBuckets) v = t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
-        else if (resume && b < 2u * kSpillBuckets) v = t.sp.counts[(uint64_t)(b - kSpillBuckets) * t.sp.nwg + blockIdx.x];
+        if (resume && b < (uint32_t)NB) v = t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
+        else if (resume && b < 2u * NB) v = t.sp.counts[(uint64_t)(b - NB) * t.sp.nwg + blockIdx.x];
         curs[b] = v;
     }
     if (tid < 17 * 4) {  // byte masks: dword d of kmask[len] keeps clamp(len - 4d, 0, 4) bytes
@@ -202,10 +208,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // this workgroup's spill streams: [g][bucket][sub] (a workgroup's stores stay
     // within a few MiB, so they hit few TLB pages; mrgpu_internal.h Spill)
     const __amdgpu_buffer_rsrc_t rs8 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(t.sp.pool8 + (uint64_t)blockIdx.x * kSpillBuckets * sub8), (short)0, (int)(kSpillBuckets * sub8 * 8u),
+        (void*)(t.sp.pool8 + (uint64_t)blockIdx.x * NB * sub8), (short)0, (int)(NB * sub8 * 8u),
         0x00020000);
     const __amdgpu_buffer_rsrc_t rs16 = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(t.sp.pool + (uint64_t)blockIdx.x * kSpillBuckets * sub), (short)0, (int)(kSpillBuckets * sub * 16u),
+        (void*)(t.sp.pool + (uint64_t)blockIdx.x * NB * sub), (short)0, (int)(NB * sub * 16u),
         0x00020000);
     uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
     const uint32_t ring0 = lds_addr(L.ring[wv][0]);
@@ -416,9 +422,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                     (u32x4){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32)};
                         const u32x4 r = stage[lane];  // this wave's own writes, in order
                         const bool valid = lane < nm;
-                        const uint32_t b = spill_bucket(fold32(r.x, r.y, r.z, r.w));
+                        const uint32_t b = spill_bucket<NB>(fold32(r.x, r.y, r.z, r.w));
                         const bool big = (r.z | r.w) != 0;
-                        const uint32_t ci = valid ? b + (big ? (uint32_t)kSpillBuckets : 0u) : 2u * kSpillBuckets + lane;
+                        const uint32_t ci = valid ? b + (big ? (uint32_t)NB : 0u) : 2u * NB + lane;
                         const uint32_t pos = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         if constexpr ((mode & 32) != 0) {
                             acc += pos;
@@ -447,10 +453,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     uint32_t pos[kBatch];
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        const uint32_t b = spill_bucket(hh[u]);
+                        const uint32_t b = spill_bucket<NB>(hh[u]);
                         const uint32_t ci = __builtin_amdgcn_inverse_ballot_w64(mMiss[u])
-                                                ? b + (__builtin_amdgcn_inverse_ballot_w64(mBig[u]) ? (uint32_t)kSpillBuckets : 0u)
-                                                : 2u * kSpillBuckets + lane;  // per-lane dummy cursor
+                                                ? b + (__builtin_amdgcn_inverse_ballot_w64(mBig[u]) ? (uint32_t)NB : 0u)
+                                                : 2u * NB + lane;  // per-lane dummy cursor
                         pos[u] = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                     if constexpr ((mode & 32) != 0) {
@@ -460,7 +466,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     }
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        const uint32_t b = spill_bucket(hh[u]);
+                        const uint32_t b = spill_bucket<NB>(hh[u]);
                         const uint64_t mFit8 = __ballot(pos[u] < sub8), mFit16 = __ballot(pos[u] < sub);
                         const uint64_t mPut8 = mMiss[u] & ~mBig[u] & mFit8, mPut16 = mMiss[u] & mBig[u] & mFit16;
                         const uint32_t o8 = __builtin_amdgcn_inverse_ballot_w64(mPut8) ? (__umul24(b, sub8) + pos[u]) * 8u : kOutOfRange;
@@ -488,8 +494,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 
     __syncthreads();
     unsigned long long spilled = 0, hits = 0;
-    for (uint32_t b = tid; b < (uint32_t)kSpillBuckets; b += kT) {  // (this launch's share: minus the resumed values)
-        const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[kSpillBuckets + b], sub);
+    for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {  // (this launch's share: minus the resumed values)
+        const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[NB + b], sub);
         uint32_t* p16 = &t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x];
         uint32_t* p8 = &t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
         spilled += k + k8 - (resume ? *p16 + *p8 : 0u);
@@ -506,7 +512,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
     block_add4<NW>(&t.ctr->spilled, &t.ctr->dict_hits, &t.ctr->spill_ovf, &t.ctr->chunks_utf8, spilled, hits,
                             ovf, lane == 0 ? utf8_chunks : 0, L.red);
-    if (t.dbg && tid == 0) t.dbg[2 * (kSpillBuckets + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
+    if (t.dbg && tid == 0) t.dbg[2 * (NB + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------ bucket aggregator tables
@@ -838,7 +844,7 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
     constexpr uint32_t kAggShortSets = AL::kShortSets, kAggMidSets = AL::kMidSets;
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uint64_t b = blockIdx.x;
-    constexpr uint32_t E = (uint32_t)kSpillBuckets * kAggSegs;
+    const uint32_t E = t.sp.nb * kAggSegs;
     const bool later = t.sp.round != 0;
     if (later) {  // a later round: buckets with nothing carried over have nothing to do
         uint32_t tot = 0;
@@ -862,11 +868,11 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
     const bool keep_miss = emit != 2;
     uint64_t miss = 0, carried = 0;
     if (!later) {
-        // round 0: bucket b's stream of map workgroup g is pool[(g * kSpillBuckets + b) * sub]
+        // round 0: bucket b's stream of map workgroup g is pool[(g * nb + b) * sub]
         agg_pool<amode, false, 8>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg,
-                                  (uint64_t)kSpillBuckets * t.sp.sub8, t.sp.nwg, nullptr, keep_miss, miss);
+                                  (uint64_t)t.sp.nb * t.sp.sub8, t.sp.nwg, nullptr, keep_miss, miss);
         agg_pool<amode, true, 4>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
-                                 (uint64_t)kSpillBuckets * t.sp.sub_keys, t.sp.nwg, nullptr, keep_miss, miss);
+                                 (uint64_t)t.sp.nb * t.sp.sub_keys, t.sp.nwg, nullptr, keep_miss, miss);
     } else {
         // later rounds: wave w re-reads its own segment of the previous round's misses
         agg_pool<amode, false, 8>(A, t, t.sp.seg8_in, t.sp.seg_n_in + b * kAggSegs, 0, kAggWaves,
@@ -982,17 +988,17 @@ __global__ void __launch_bounds__(kMaxMapWGs) seg_count_kernel(Spill sp, uint32_
         atomicAdd(&sum[kAggSegs + g % kAggSegs], sp.counts[(uint64_t)b * sp.nwg + g]);
     }
     __syncthreads();
-    constexpr uint32_t E = (uint32_t)kSpillBuckets * kAggSegs;
+    const uint32_t E = sp.nb * kAggSegs;
     if (g < kAggSegs) {
         tmp[b * kAggSegs + g] = sum[g];
         tmp[E + b * kAggSegs + g] = sum[kAggSegs + g];
     }
 }
 
-// Step 2: exclusive scans (one workgroup; 4 entries per thread), totals at [E].
-__global__ void __launch_bounds__(1024) seg_scan_kernel(const uint32_t* tmp, uint64_t* off8, uint64_t* off16) {
-    constexpr uint32_t E = (uint32_t)kSpillBuckets * kAggSegs, PER = E / 1024;
-    static_assert(E % 1024 == 0, "scan layout");
+// Step 2: exclusive scans (one workgroup; E / 1024 entries per thread), totals at [E].
+__global__ void __launch_bounds__(1024) seg_scan_kernel(const uint32_t* tmp, uint64_t* off8, uint64_t* off16,
+                                                        uint32_t E) {
+    const uint32_t PER = E / 1024;  // E = nb * kAggSegs, a multiple of 1024
     __shared__ unsigned long long part[2][1024];
     const uint32_t tid = threadIdx.x;
     uint64_t a = 0, c = 0;
@@ -1156,6 +1162,10 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     const uint64_t n4 = n & ~3ull, reach = kSlotBytes - kBack;
     const uint32_t ctail = (n & 3) == 0 ? 0xFFFFFFFFu : n4 < reach ? 0u : (uint32_t)((n4 - reach) / kOwn + 1);
     const uint64_t g = wc_map_grid(n, grid);
+    if (t.sp.nb == kSpillBucketsHi) {  // high-cardinality layout (ablation modes apply to the default one only)
+        wc_map_kernel<0, 12, kSpillBucketsHi><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
+        return true;
+    }
     switch (mode) {
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;
@@ -1173,19 +1183,21 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
 void launch_wc_agg(const Tables& t, int mode, int emit, bool big, hipStream_t s) {
     // mode 512 (diagnostic only, wrong results): a read-only pass first, so the
     // timed pass runs with warm caches and address translations
-    if (mode & 512) wc_agg_kernel<128, AggLds><<<kSpillBuckets, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+    const uint32_t nb = t.sp.nb;
+    if (mode & 512) wc_agg_kernel<128, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
     if (big) {
-        if (mode & 128) wc_agg_kernel<128, AggLdsBig><<<kSpillBuckets, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
-        else wc_agg_kernel<0, AggLdsBig><<<kSpillBuckets, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
+        if (mode & 128) wc_agg_kernel<128, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
+        else wc_agg_kernel<0, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
     } else {
-        if (mode & 128) wc_agg_kernel<128, AggLds><<<kSpillBuckets, AggLds::kWaves * kWave, 0, s>>>(t, emit);
-        else wc_agg_kernel<0, AggLds><<<kSpillBuckets, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+        if (mode & 128) wc_agg_kernel<128, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+        else wc_agg_kernel<0, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
     }
 }
 
 void launch_seg_layout(const Tables& t, uint32_t* tmp, uint64_t* off8, uint64_t* off16, hipStream_t s) {
-    seg_count_kernel<<<kSpillBuckets, kMaxMapWGs, 0, s>>>(t.sp, tmp);
-    seg_scan_kernel<<<1, 1024, 0, s>>>(tmp, off8, off16);
+    static_assert(kSpillBuckets * kAggSegs % 1024 == 0 && kSpillBucketsHi * kAggSegs % 1024 == 0, "scan layout");
+    seg_count_kernel<<<t.sp.nb, kMaxMapWGs, 0, s>>>(t.sp, tmp);
+    seg_scan_kernel<<<1, 1024, 0, s>>>(tmp, off8, off16, t.sp.nb * kAggSegs);
 }
 
 void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s) {

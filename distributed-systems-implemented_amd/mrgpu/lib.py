@@ -73,6 +73,7 @@ class Stats(ctypes.Structure):
         ("shuffle_send_bytes", c_uint64),
         ("shuffle_recv_bytes", c_uint64),
         ("staged_bytes", c_uint64),
+        ("spill_buckets", c_uint64),
     ]
 
     def as_dict(self):

@@ -91,6 +91,7 @@ typedef struct {
     uint64_t shuffle_recv_bytes; /* exchange: wire bytes this rank received from other ranks */
     uint64_t staged_bytes;    /* map: bytes copied into the context's staging buffer first (host input,
                                  or a device pointer not 16-byte aligned) */
+    uint64_t spill_buckets;   /* wc: hash buckets of the map's spill (512; 2048 for high-cardinality splits) */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);

@@ -143,6 +143,34 @@ def test_wc_bucket_aggregator_overflow(ctx, rounds, big):
         ctx.set_option("agg_big_later", 0)
 
 
+@pytest.mark.parametrize("rounds", [0, 1])
+def test_wc_high_cardinality_buckets(ctx, rounds):
+    """2048 spill buckets (high-cardinality layout: 12-wave map workgroups, 4x
+    the aggregator workgroups), forced and chosen by the feedback rule: exact
+    on a 3M-word vocabulary, in rounds or with every miss counted in HBM."""
+    voc = C.Vocab(C.KIND_ASCII, 1.07, 3_000_000, 16)
+    files = [bytes(voc.fill_files([26_000_000], [16], C.wc_params(vocab_lo=0, vocab_hi=3_000_000))[0])]
+    ctx.set_option("agg_rounds", rounds)
+    ctx.set_option("spill_buckets", 2048)
+    try:
+        check(ctx, "wc", files, nreduces=(10,))
+        assert ctx.stats()["spill_buckets"] == 2048
+        ctx.set_option("spill_buckets", 0)
+        ctx.set_option("spill_hi_keys", 1_000_000)  # the feedback rule: this split has ~2.4M spilled keys
+        gpu_partitioned(ctx, "wc", files, 10)  # decides the next split's bucket count
+        got = gpu_partitioned(ctx, "wc", files, 10)
+        assert got == O.c_partitioned("wc", files, 10)
+        assert ctx.stats()["spill_buckets"] == 2048  # chosen from the previous split
+        ctx.set_option("spill_hi_keys", 1 << 40)
+        gpu_partitioned(ctx, "wc", files, 10)
+        gpu_partitioned(ctx, "wc", files, 10)
+        assert ctx.stats()["spill_buckets"] == 512
+    finally:
+        ctx.set_option("agg_rounds", 0)
+        ctx.set_option("spill_buckets", 0)
+        ctx.set_option("spill_hi_keys", 0)
+
+
 def test_wc_large_vs_oracle(wctx):
     """64 MB C2-style corpus: full bytes vs the C oracle."""
     voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
@@ -528,12 +556,14 @@ def test_exchange_group_c5_shape():
             assert outs[i][r] == (want[r] if r % P == i else b""), f"rank {i} partition {r}"
 
 
-@pytest.mark.parametrize("app", ["wc", "grep:distributed"])
+@pytest.mark.parametrize("app", ["wc", "grep:distributed", "wc-2048"])
 def test_host_input_streamed_in_pieces(ctx, app):
     """Host input copied piece by piece on a second stream while the map runs
     over the resident pieces: 1 MiB-ish pieces over a
     ~24 MB split (dictionary on, words / lines across every piece seam) equal the
     oracle, as does the same split as device input."""
+    nb = 2048 if app == "wc-2048" else 0
+    app = app.split("-")[0]
     if app == "wc":
         files = cases.synthetic(C.KIND_UTF8, 50000, [9_000_001, 8_000_000, 7_000_003], 71, 0.001)
     else:
@@ -545,10 +575,12 @@ def test_host_input_streamed_in_pieces(ctx, app):
     ctx.set_option("ingest_piece", 1 << 20)
     ctx.set_option("ingest_min", 1 << 20)
     ctx.set_option("dict_min_bytes", 1)
+    ctx.set_option("spill_buckets", nb)
     try:
         assert ctx.run_job(a, joined, pattern=pat, nreduce=10) == want
         assert ctx.stats()["staged_bytes"] == len(joined)
     finally:
+        ctx.set_option("spill_buckets", 0)
         ctx.set_option("ingest_piece", 0)
         ctx.set_option("ingest_min", 0)
         ctx.set_option("dict_min_bytes", 0)
