@@ -288,7 +288,7 @@ static Tables make_tables(mrg_ctx* c) {
     t.bflag = (uint32_t*)c->bflag.p;
     t.dict = nullptr;
     t.dict_cnt = (uint32_t*)c->dict_cnt.p;
-    t.dbg = c->debug_times && c->dbg.ensure(2 * kMaxMapWGs * 8 * 4) == hipSuccess ? (unsigned long long*)c->dbg.p : nullptr;
+    t.dbg = c->debug_times && c->dbg.ensure(2 * (kSpillBucketsHi + kMaxMapWGs) * 8) == hipSuccess ? (unsigned long long*)c->dbg.p : nullptr;
     return t;
 }
 

@@ -537,7 +537,7 @@ struct alignas(16) AggLdsT {
     unsigned long long sk[NS * 4];
     unsigned long long mk[NM * 4 * 2];  // way w of set s: mk[2(4s+w)] = k0, mk[2(4s+w)+1] = k1
     uint32_t sc[NS * 4 + kWave];        // counts (+ per-lane dummies for branch-free adds)
-    uint32_t mc[NM * 4];
+    uint32_t mc[NM * 4 + kWave];
     unsigned long long red[4 * NW + 4];  // block_add4 / block_alloc scratch
     uint32_t ncur8[kAggSegs], ncur16[kAggSegs];  // misses appended to each segment
 };
@@ -795,7 +795,8 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
         if constexpr ((amode & 128) != 0) {
 #pragma unroll
             for (uint32_t u = 0; u < kAggUnroll; u++) miss += h[u];
-        } else if constexpr (!kMid) {
+        } else if constexpr (!kMid && (amode & 64) != 0) {
+            // first-set lookups only, each miss its own slow path (sparse tables)
             uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
 #pragma unroll
             for (uint32_t u = 0; u < kAggUnroll; u++) {
@@ -818,13 +819,108 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
                 }
             }
-        } else {
+        } else if constexpr (!kMid) {
+            // Both sets of a key are looked up before anything diverges: a key
+            // sits in its second set only if its first was full when it was
+            // claimed (ways are never freed), so a first set with a free way and
+            // without the key settles it as new.  Only new keys (and lost claims)
+            // take the slow path, all of a lane's in one loop, so a wave runs it
+            // about once per block instead of once per record slot.
+            // mz[u]: first-set hit ways (bits 0-3), free ways (4-7), second-set hit ways (8-11)
+            uint32_t mz[kAggUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                uint32_t m, z;
+                short_set_masks(A, set_base<AL::kShortSets>(h[u]), ((uint64_t)cur[u].y << 32) | cur[u].x, m, z);
+                mz[u] = m | z << 4;
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                if ((cur[u].x | cur[u].y) != 0 && mz[u] == 0) {
+                    uint32_t m2, z2;
+                    short_set_masks(A, set_base<AL::kShortSets>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
+                                    m2, z2);
+                    mz[u] = m2 << 8;
+                }
+            }
+            uint32_t slow = 0;
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
+                const uint32_t m = mz[u] & 15u, m2 = (mz[u] >> 8) & 15u;
+                const uint32_t ci = !valid   ? (uint32_t)AL::kShortSets * 4 + lane
+                                    : m != 0  ? set_base<AL::kShortSets>(h[u]) + __builtin_ctz(m)
+                                    : m2 != 0 ? set_base<AL::kShortSets>(second_hash(h[u])) + __builtin_ctz(m2)
+                                              : (uint32_t)AL::kShortSets * 4 + lane;
+                if (valid && (m | m2) == 0) slow |= 1u << u;
+                __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            while (slow) {  // this lane's new keys, one per trip (register arrays read by selects, not indexing)
+                const uint32_t us = __builtin_ctz(slow);
+                slow &= slow - 1;
+                uint64_t k = 0;
+                uint32_t hk = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++)
+                    if (us == u) {
+                        k = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                        hk = h[u];
+                    }
+                if (!short_insert_slow(A, k, hk, 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
+            }
+        } else if constexpr ((amode & 64) != 0) {
 #pragma unroll
             for (uint32_t u = 0; u < kAggUnroll; u++) {
                 if ((cur[u].x | cur[u].y) != 0) {
                     const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
                     if (!mid_insert(A, k0, k1, h[u], 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
                 }
+            }
+        } else {
+            // mid keys: the same two-set lookup first (a way pending publication
+            // sends the record to the slow path, which retries or defers it)
+            uint32_t mm[kAggUnroll], slow = 0;  // mm[u]: first-set hit ways (bits 0-3), second-set (4-7)
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                uint32_t m, z, pend;
+                const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                mid_set_masks(A, set_base<AL::kMidSets>(h[u]), k0, k1, m, z, pend);
+                mm[u] = m;
+                if ((cur[u].x | cur[u].y) != 0 && m == 0 && (z | pend) != 0) slow |= 1u << u;  // new key / pending
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                if ((cur[u].x | cur[u].y) != 0 && mm[u] == 0 && !((slow >> u) & 1u)) {
+                    uint32_t m2, z2, p2;
+                    const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                    mid_set_masks(A, set_base<AL::kMidSets>(second_hash(h[u])), k0, k1, m2, z2, p2);
+                    mm[u] = m2 << 4;
+                    if (m2 == 0) slow |= 1u << u;
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                const bool valid = (cur[u].x | cur[u].y) != 0;
+                const uint32_t m = mm[u] & 15u, m2 = mm[u] >> 4;
+                const uint32_t ci = !valid   ? (uint32_t)AL::kMidSets * 4 + lane
+                                    : m != 0  ? set_base<AL::kMidSets>(h[u]) + __builtin_ctz(m)
+                                    : m2 != 0 ? set_base<AL::kMidSets>(second_hash(h[u])) + __builtin_ctz(m2)
+                                              : (uint32_t)AL::kMidSets * 4 + lane;
+                __hip_atomic_fetch_add(&A.mc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            while (slow) {
+                const uint32_t us = __builtin_ctz(slow);
+                slow &= slow - 1;
+                uint64_t k0 = 0, k1 = 0;
+                uint32_t hk = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++)
+                    if (us == u) {
+                        k0 = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                        k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                        hk = h[u];
+                    }
+                if (!mid_insert(A, k0, k1, hk, 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
             }
         }
 #pragma unroll
@@ -835,8 +931,9 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
     }
 }
 
-// amode (benchmark ablation only, compile-time; results are wrong unless 0):
-// 128 = read + hash the records only.  emit: see launch_wc_agg.
+// amode (compile-time): 0 = two-set lookups, 64 = first-set lookups (both
+// exact; launch_wc_agg picks by layout); 128 = benchmark ablation, read + hash
+// the records only (wrong results).  emit: see launch_wc_agg.
 template <uint32_t amode, class AL>
 __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int emit) {
     __shared__ AL A;
@@ -970,8 +1067,8 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
             if (k0 != 0) put_short(t, o++, k0, A.mk[2 * i + 1], A.mc[i], emit == 1);
         }
     }
-    if (amode != 0 && miss == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // no DCE in ablation builds
-    block_add4<kAggWaves>(&t.ctr->agg_miss, &t.ctr->carried, nullptr, nullptr, amode == 0 ? miss : 0, carried, 0, 0,
+    if ((amode & 128) != 0 && miss == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // no DCE in ablation builds
+    block_add4<kAggWaves>(&t.ctr->agg_miss, &t.ctr->carried, nullptr, nullptr, (amode & 128) == 0 ? miss : 0, carried, 0, 0,
                           A.red);
     if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
 }
@@ -1185,12 +1282,19 @@ void launch_wc_agg(const Tables& t, int mode, int emit, bool big, hipStream_t s)
     // timed pass runs with warm caches and address translations
     const uint32_t nb = t.sp.nb;
     if (mode & 512) wc_agg_kernel<128, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+    // Lookup strategy by layout (both exact; mode 64 swaps them for measurement):
+    // the two-set lookup pays off where buckets are full and keys often sit in
+    // their second set (C5 round 0: 16.7 -> 13.4 ms), the first-set one where
+    // tables are sparse (C2: 1.29 vs 1.50 ms).
+    const bool two_set = (nb == kSpillBucketsHi) != ((mode & 64) != 0);
     if (big) {
         if (mode & 128) wc_agg_kernel<128, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
-        else wc_agg_kernel<0, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
+        else if (two_set) wc_agg_kernel<0, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
+        else wc_agg_kernel<64, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
     } else {
         if (mode & 128) wc_agg_kernel<128, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
-        else wc_agg_kernel<0, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+        else if (two_set) wc_agg_kernel<0, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+        else wc_agg_kernel<64, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
     }
 }
 

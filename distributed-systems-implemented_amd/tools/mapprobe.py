@@ -1,8 +1,9 @@
 """Ablation probe for wc_map_kernel (benchmark-only; map_mode != 0 gives wrong results).
 
-Times the map kernel over the C2 corpus with phases switched off:
-  mode 1 = read input only, 2 = tokenize only, 4 = + key extraction (no table), 0 = full.
-usage: python tools/mapprobe.py [--gb 10] [--modes 1,2,4,0] [--grids 256,512]
+Times the map kernel over the C2 (or C5: --workload c5) corpus with phases switched off:
+  mode 1 = read input only, 2 = tokenize only, 4 = + key extraction (no table), 0 = full;
+  mode 128 = aggregator reads + hashes its records only (agg_ms).
+usage: python tools/mapprobe.py [--gb 10] [--modes 1,2,4,0] [--grids 256,512] [--workload c2|c5]
 """
 import argparse
 import json
@@ -11,6 +12,7 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))  # the repo root (bench.py's corpus generator)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402,F401
 
@@ -25,12 +27,17 @@ def main():
     ap.add_argument("--grids", default="0")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--opt", action="append", default=[], help="context option name=value (repeatable)")
+    ap.add_argument("--workload", default="c2", choices=["c2", "c5"])
     a = ap.parse_args()
     nfiles = max(1, int(a.gb * 4))
-    voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
-    sizes = [250_000_000] * nfiles
-    buf = np.empty(sum(sizes), dtype=np.uint8)
-    voc.fill_files(sizes, [2 + i for i in range(nfiles)], C.wc_params(), out=buf)
+    if a.workload == "c5":
+        import bench
+        buf = bench.gen_corpus(bench.WORKLOADS["c5"], 0, 250, nfiles)
+    else:
+        voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
+        sizes = [250_000_000] * nfiles
+        buf = np.empty(sum(sizes), dtype=np.uint8)
+        voc.fill_files(sizes, [2 + i for i in range(nfiles)], C.wc_params(), out=buf)
     ctx = Context(0)
     for o in a.opt:
         k, v = o.split("=")
