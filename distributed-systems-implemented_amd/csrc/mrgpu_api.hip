@@ -1055,6 +1055,12 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "spill_buckets")) {  // 0: chosen per split (feedback), else 512 or 2048
         if (v != 0 && v != kSpillBuckets && v != kSpillBucketsHi) return fail(c, MRG_EINVAL, "spill_buckets: 0, 512 or 2048");
         c->spill_buckets_opt = (int)v;
+    } else if (!strcmp(name, "sort_digit_bits")) {  // 64-bit radix passes: 8 or 10 bits per digit (0: by app)
+        reduce_ws_set(c->rws, (int)v, -1, -1);
+    } else if (!strcmp(name, "sort_fold_part")) {  // partition folded into the k0 sort key (-1: off)
+        reduce_ws_set(c->rws, 0, v >= 0 ? 1 : 0, -1);
+    } else if (!strcmp(name, "grep_sort_k1")) {  // grep radix over 16 key bytes (default) or 8 (-1)
+        reduce_ws_set(c->rws, 0, -1, v >= 0 ? 1 : 0);
     } else if (!strcmp(name, "spill_hi_keys")) c->spill_hi_keys = v > 0 ? (uint64_t)v : 6000ull * kSpillBuckets;
     else if (!strcmp(name, "dict_min_bytes")) c->dict_min_bytes = v > 0 ? (uint64_t)v : (32ull << 20);
     else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);

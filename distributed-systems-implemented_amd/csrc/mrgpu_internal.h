@@ -211,6 +211,10 @@ int map_grid_size(int device);
 struct ReduceWs;  // opaque workspace
 ReduceWs* reduce_ws_new();
 void reduce_ws_free(ReduceWs*);
+// Sort tuning: radix digit bits of the 64-bit passes (8 or 10; others ignored),
+// fold the partition into the first key pass (1 / 0; -1 keeps it), grep radix
+// passes over 16 key bytes (1) or 8 (0; -1 keeps it).
+void reduce_ws_set(ReduceWs*, int digit_bits, int fold_part, int grep_k1);
 // Sort recs (optionally only partition `only_part`), format "key value\n" lines.
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
 int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,

@@ -47,7 +47,16 @@ struct DBuf {
 struct ReduceWs {
     DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext;
     uint64_t* h_pinned = nullptr;  // small pinned staging
+    int digit_bits = 0;            // radix digit of the 64-bit key passes: 8, 10, 0 = by app (grep 10, wc 8)
+    bool fold_part = true;         // wc: partition folded into the top bits of the k0 sort key
+    bool grep_k1 = true;           // grep: radix passes over the first 16 key bytes (else 8, more ties)
 };
+
+void reduce_ws_set(ReduceWs* w, int digit_bits, int fold_part, int grep_k1) {
+    if (digit_bits == 0 || digit_bits == 8 || digit_bits == 10) w->digit_bits = digit_bits;
+    if (fold_part >= 0) w->fold_part = fold_part != 0;
+    if (grep_k1 >= 0) w->grep_k1 = grep_k1 != 0;
+}
 
 ReduceWs* reduce_ws_new() {
     ReduceWs* w = new ReduceWs();
@@ -63,20 +72,7 @@ void reduce_ws_free(ReduceWs* w) {
     delete w;
 }
 
-// flags[0]: any long record, flags[1]: any k1 != 0, flags[2]: tied runs found.
-// One atomic per block at most (same-address atomics serialize).
-__global__ void rec_flags_kernel(Recs r, unsigned long long* flags) {
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    bool lng = false, k1 = false;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += stride) {
-        lng |= r.len[i] > 16;
-        k1 |= r.k1[i] != 0;
-    }
-    lng = __syncthreads_or(lng);
-    k1 = __syncthreads_or(k1);
-    if (threadIdx.x == 0 && lng) atomicOr(&flags[0], 1ull);
-    if (threadIdx.x == 1 && k1) atomicOr(&flags[1], 1ull);
-}
+// flags[1]: any k1 != 0 (mark_ties), flags[2]: tied runs found, flags[3]: long runs.
 
 __global__ void iota_kernel(uint32_t* p, uint64_t n) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -88,26 +84,19 @@ __global__ void iota_kernel(uint32_t* p, uint64_t n) {
 // loads.
 constexpr int kExtWords = 6;
 
-// which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part
-__global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32) {
+// which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part, 4 = part in the top
+// `fold` bits over bswap(k0) >> fold (the first 64 - fold key bits)
+__global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32,
+                                  uint32_t fold = 0) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint32_t j = perm[i];
+        uint32_t j = perm ? perm[i] : (uint32_t)i;
         if (which == 0) k32[i] = r.len[j];
         else if (which == 1) k64[i] = __builtin_bswap64(r.k1[j]);
         else if (which == 2) k64[i] = __builtin_bswap64(r.k0[j]);
+        else if (which == 4) k64[i] = ((uint64_t)r.part[j] << (64 - fold)) | (__builtin_bswap64(r.k0[j]) >> fold);
         else k32[i] = r.part[j];
     }
-}
-
-__device__ __forceinline__ const uint8_t* rec_bytes(const Recs& r, uint32_t j, uint8_t* tmp16) {
-    if (r.koff[j] != ~0ull) return r.arena + r.koff[j];
-    uint64_t k0 = r.k0[j], k1 = r.k1[j];
-    for (int k = 0; k < 8; k++) {
-        tmp16[k] = (uint8_t)(k0 >> (8 * k));
-        tmp16[8 + k] = (uint8_t)(k1 >> (8 * k));
-    }
-    return tmp16;
 }
 
 // Big-endian 8-byte word of key bytes [pos, pos + 8), zero past the key's end.
@@ -204,8 +193,11 @@ __device__ int rec_cmp_ext(const Recs& r, const uint64_t* ext, uint32_t a, uint3
     return (la > lb) - (la < lb);
 }
 
-__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b, bool with_k1) {
-    return r.part[a] == r.part[b] && r.k0[a] == r.k0[b] && (!with_k1 || r.k1[a] == r.k1[b]);
+// fold > 0: the sort key held only the first 64 - fold bits of the key
+__device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t b, bool with_k1, uint32_t fold) {
+    if (r.part[a] != r.part[b]) return false;
+    if (fold) return (__builtin_bswap64(r.k0[a]) >> fold) == (__builtin_bswap64(r.k0[b]) >> fold);
+    return r.k0[a] == r.k0[b] && (!with_k1 || r.k1[a] == r.k1[b]);
 }
 
 // tie[i] = 1 when sorted position i has the same (part, prefix) as i-1, the
@@ -213,13 +205,15 @@ __device__ __forceinline__ bool same_prefix(const Recs& r, uint32_t a, uint32_t 
 // distinct keys with equal zero-padded prefixes are only ordered by a full
 // bytewise comparison.
 __global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8_t* tie, unsigned long long* flags,
-                                 bool with_k1) {
+                                 bool with_k1, uint32_t fold) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         uint8_t t = 0;
-        if (i > 0 && same_prefix(r, perm[i - 1], perm[i], with_k1)) t = 1;
+        if (i > 0 && same_prefix(r, perm[i - 1], perm[i], with_k1, fold)) t = 1;
         tie[i] = t;
+        const bool k1 = r.k1[perm[i]] != 0;  // flags[1]: some key has more than 8 bytes
         if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
+        if (__ballot(k1) && (threadIdx.x & 63) == 0 && flags[1] == 0) atomicOr(&flags[1], 1ull);
     }
 }
 
@@ -279,10 +273,30 @@ __global__ void scatter_perm_kernel(uint32_t* perm, const uint32_t* pos, const u
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) perm[pos[i]] = v[i];
 }
 
+// decimal digits of v: compares against the powers of ten, no divisions
 __device__ __forceinline__ uint32_t ndigits(uint64_t v) {
     uint32_t d = 1;
-    while (v >= 10) { v /= 10; d++; }
+    uint64_t p = 10;
+#pragma unroll
+    for (int k = 1; k < 20; k++, p *= 10) d += v >= p ? 1u : 0u;
     return d;
+}
+
+// The decimal digits of v (d of them) at o[0, d), most significant first.
+template <class OutPtr>
+__device__ __forceinline__ void put_digits(OutPtr o, uint64_t v, uint32_t d) {
+    if (v < (1ull << 32)) {  // 32-bit divisions for every count below 2^32
+        uint32_t w = (uint32_t)v;
+        for (uint32_t k = d; k > 0; k--) {
+            o[k - 1] = (uint8_t)('0' + w % 10u);
+            w /= 10u;
+        }
+    } else {
+        for (uint32_t k = d; k > 0; k--) {
+            o[k - 1] = (uint8_t)('0' + v % 10);
+            v /= 10;
+        }
+    }
 }
 
 __global__ void line_len_kernel(Recs r, const uint32_t* perm, uint64_t n, int app, uint64_t* ll) {
@@ -315,36 +329,66 @@ __global__ void write_lines_wave_kernel(Recs r, const uint32_t* perm, uint64_t n
     }
 }
 
-__global__ void write_lines_kernel(Recs r, const uint32_t* perm, uint64_t n, int app, const uint64_t* off, uint8_t* out) {
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint32_t j = perm[i];
-        uint8_t tmp[16];
-        const uint8_t* kb = rec_bytes(r, j, tmp);
-        uint32_t len = r.len[j];
-        uint8_t* o = out + off[i];
-        for (uint32_t k = 0; k < len; k++) o[k] = kb[k];
-        o += len;
-        *o++ = ' ';
-        if (app == 1) {
-            uint64_t v = r.cnt[j];
-            uint32_t d = ndigits(v);
-            for (uint32_t k = d; k > 0; k--) { o[k - 1] = (uint8_t)('0' + v % 10); v /= 10; }
-            o += d;
-        } else {
-            for (uint32_t k = 0; k < len; k++) o[k] = kb[k];
-            o += len;
+// wc lines ("key count\n"): a block's 256 consecutive lines are one contiguous
+// output range; each thread writes its line into LDS, then the block copies the
+// range out with 16-byte stores (byte stores only at the range's two ends, which
+// neighbouring blocks share).  A range longer than the LDS buffer (very long
+// keys) is written directly, byte by byte.
+constexpr uint32_t kWlLines = 256, kWlBytes = 16384;
+__global__ void __launch_bounds__(kWlLines) write_wc_lines_kernel(Recs r, const uint32_t* perm, uint64_t n,
+                                                                    const uint64_t* off, const uint64_t* ll, uint8_t* out) {
+    __shared__ __attribute__((aligned(16))) uint8_t buf[kWlBytes];
+    const uint32_t tid = threadIdx.x;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * kWlLines; i0 < n; i0 += (uint64_t)gridDim.x * kWlLines) {
+        const uint64_t iend = i0 + kWlLines < n ? i0 + kWlLines : n;
+        const uint64_t start = off[i0], end = iend < n ? off[iend] : off[n - 1] + ll[n - 1];
+        const uint64_t a0 = start & ~15ull;
+        const bool staged = end - a0 <= kWlBytes;  // block-uniform
+        const uint64_t i = i0 + tid;
+        if (i < iend) {
+            const uint32_t j = perm[i];
+            const uint32_t len = r.len[j];
+            const uint64_t k0 = r.k0[j], k1 = r.k1[j];
+            const uint8_t* kb = len > 16 ? r.arena + r.koff[j] : nullptr;
+            const uint64_t v = r.cnt[j];
+            const uint32_t d = ndigits(v);
+            auto emit = [&](auto o) {
+                for (uint32_t k = 0; k < len; k++)
+                    o[k] = kb ? kb[k] : (uint8_t)((k < 8 ? k0 : k1) >> (8 * (k & 7)));
+                o[len] = ' ';
+                put_digits(o + len + 1, v, d);
+                o[len + 1 + d] = '\n';
+            };
+            if (staged) emit(buf + (off[i] - a0));
+            else emit(out + off[i]);
         }
-        *o = '\n';
+        if (staged) {
+            __syncthreads();
+            const uint32_t nq = (uint32_t)((end - a0 + 15) / 16);
+            for (uint32_t q = tid; q < nq; q += kWlLines) {
+                const uint64_t ga = a0 + 16ull * q;
+                if (ga >= start && ga + 16 <= end) {
+                    *(uint4*)(out + ga) = *(const uint4*)(buf + 16 * q);
+                } else {
+                    for (uint32_t b = 0; b < 16; b++)
+                        if (ga + b >= start && ga + b < end) out[ga + b] = buf[16 * q + b];
+                }
+            }
+            __syncthreads();
+        }
     }
 }
 
 // offsets[p] = byte offset of the first line of partition p (lower bound on sorted part).
-__global__ void part_offsets_kernel(Recs r, const uint32_t* perm, uint64_t n, const uint64_t* off, uint64_t total,
-                                    uint32_t nparts, uint64_t* offsets) {
+// offsets[nparts] = the output's total bytes (last line's offset + length);
+// with one_part the output is one partition: offsets = {0, total}.
+__global__ void part_offsets_kernel(Recs r, const uint32_t* perm, uint64_t n, const uint64_t* off, const uint64_t* ll,
+                                    uint32_t nparts, bool one_part, uint64_t* offsets) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p > nparts) return;
+    const uint64_t total = off[n - 1] + ll[n - 1];
     if (p == nparts) { offsets[p] = total; return; }
+    if (one_part) { offsets[p] = 0; return; }
     uint64_t lo = 0, hi = n;
     while (lo < hi) {
         uint64_t mid = (lo + hi) >> 1;
@@ -390,11 +434,25 @@ static inline unsigned grid_for(uint64_t n) {
 // (~1e6 distinct keys); onesweep is several times faster there.
 using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config,
                                                (size_t)64 * 1024>;
+// 10-bit digits: a 64-bit key in 7 passes instead of 8 (each onesweep pass is a
+// ~25 us launch plus two look-back-state memsets at these sizes)
+using OnesweepCfg10 = rocprim::radix_sort_config<
+    rocprim::default_config, rocprim::default_config,
+    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<512, 12>, 10,
+                                        rocprim::block_radix_rank_algorithm::match>,
+    (size_t)64 * 1024>;
 
 template <class K>
 static int sort_pass(ReduceWs* ws, K* keys_in, K* keys_out, uint32_t* v_in, uint32_t* v_out, uint64_t n, unsigned bits,
                      hipStream_t s) {
     size_t tb = 0;
+    if (sizeof(K) == 8 && ws->digit_bits == 10 && bits > 32) {
+        RCHK(rocprim::radix_sort_pairs<OnesweepCfg10>(nullptr, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
+        RCHK(ws->tmp.ensure(tb));
+        RCHK(rocprim::radix_sort_pairs<OnesweepCfg10>(ws->tmp.p, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits,
+                                                      s));
+        return 0;
+    }
     RCHK(rocprim::radix_sort_pairs<OnesweepCfg>(nullptr, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
     RCHK(ws->tmp.ensure(tb));
     RCHK(rocprim::radix_sort_pairs<OnesweepCfg>(ws->tmp.p, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
@@ -424,6 +482,12 @@ int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64
 
 int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s) {
     size_t tb = 0;
+    if (ws->digit_bits != 8 && bits > 32) {  // (grep hit positions: 4 passes of 10 bits for a 34-bit split)
+        RCHK(rocprim::radix_sort_keys<OnesweepCfg10>(nullptr, tb, k_in, k_out, (size_t)n, 0u, bits, s));
+        RCHK(ws->tmp.ensure(tb));
+        RCHK(rocprim::radix_sort_keys<OnesweepCfg10>(ws->tmp.p, tb, k_in, k_out, (size_t)n, 0u, bits, s));
+        return 0;
+    }
     RCHK(rocprim::radix_sort_keys<OnesweepCfg>(nullptr, tb, k_in, k_out, (size_t)n, 0u, bits, s));
     RCHK(ws->tmp.ensure(tb));
     RCHK(rocprim::radix_sort_keys<OnesweepCfg>(ws->tmp.p, tb, k_in, k_out, (size_t)n, 0u, bits, s));
@@ -501,16 +565,18 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     }
     RCHK(ws->flags.ensure(64));
     unsigned long long* flags = ws->flags.as<unsigned long long>();
-    RCHK(hipMemsetAsync(flags, 0, 64, s));
-    rec_flags_kernel<<<grid_for(n) < 512 ? grid_for(n) : 512, 256, 0, s>>>(r, flags);
-    RCHK(hipMemcpyAsync(ws->h_pinned, flags, 24, hipMemcpyDeviceToHost, s));
     RCHK(ws->perm_a.ensure(n * 4));
     RCHK(ws->perm_b.ensure(n * 4));
     RCHK(ws->key_a.ensure(n * 8));
     RCHK(ws->key_b.ensure(n * 8));
     RCHK(ws->lineoff.ensure(n * 8 + 8));
-    RCHK(hipStreamSynchronize(s));
-    const bool has_long = ws->h_pinned[0] != 0, has_k1 = ws->h_pinned[1] != 0;
+    // Output bytes, bounded up front so nothing waits for the exact total: a wc
+    // line is key + ' ' + <= 20 digits + '\n', a grep line key + ' ' + key + '\n';
+    // key bytes past 16 live in the arena.
+    const uint64_t key_bound = 16 * n + r.arena_n;
+    RCHK(ws->out.ensure(app == 1 ? key_bound + 22 * n + 16 : 2 * key_bound + 2 * n + 16));
+    RCHK(ws->offs.ensure((size_t)(nparts + 1) * 8));
+    RCHK(hipMemsetAsync(flags, 0, 32, s));
 
     uint32_t* pa = ws->perm_a.as<uint32_t>();
     uint32_t* pb = ws->perm_b.as<uint32_t>();
@@ -518,9 +584,18 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     // sort with the k1 pass from the start; ties merge-sort on the ext words
     // (measured: two more 64-bit radix passes over bytes 16-31 cost more, ~16
     // launches, than the larger merge sort they save)
-    const bool k1_first = has_long && app != 1;
+    const bool grep = app != 1;
+    const bool k1_first = grep && ws->grep_k1;
+    // 10-bit digits: C3 reduce 1.50 -> 1.44 ms (15 passes instead of 17); C2 unchanged
+    const int saved_bits = ws->digit_bits;
+    if (saved_bits == 0) ws->digit_bits = grep ? 10 : 8;
+    struct Restore {
+        ReduceWs* w;
+        int b;
+        ~Restore() { w->digit_bits = b; }
+    } restore{ws, saved_bits};
     const uint64_t* ext = nullptr;
-    if (k1_first) {
+    if (grep) {
         RCHK(ws->ext.ensure(n * 8 * kExtWords));
         ext_words_kernel<<<grid_for(n), 256, 0, s>>>(r, ws->ext.as<uint64_t>());
         ext = ws->ext.as<uint64_t>();
@@ -531,26 +606,36 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         std::swap(pa, pb);
         return e;
     };
-    auto pass64 = [&](int which) -> int {
-        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, ws->key_a.as<uint64_t>(), nullptr);
+    auto pass64 = [&](int which, uint32_t fold = 0, bool first = false) -> int {
+        // first: the permutation is the identity (keys gathered in record order)
+        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, first ? nullptr : pa, n, which, ws->key_a.as<uint64_t>(),
+                                                      nullptr, fold);
+        if (first) iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
         int e = sort_pass<uint64_t>(ws, ws->key_a.as<uint64_t>(), ws->key_b.as<uint64_t>(), pa, pb, n, 64, s);
         std::swap(pa, pb);
         return e;
     };
+    // partition bits folded into the k0 key's top (wc without the k1 pass): one
+    // 64-bit pass orders (partition, first 64 - pbits key bits); keys equal there
+    // are tied runs for fix_ties
+    uint32_t pbits = 0;
+    if (all && nreduce > 1)
+        while ((1ull << pbits) < nreduce) pbits++;
+    const uint32_t fold = ws->fold_part && pbits > 0 && pbits <= 16 ? pbits : 0;
     // Stable LSD passes: (k1), k0, partition.  The k1 pass (bytes 8-15) is
     // skipped at first: keys that share their first 8 bytes form short tied runs
     // that fix_ties orders by full comparison; if a run is long (many keys with
     // one 8-byte prefix), everything is sorted again with the k1 pass.
     auto sort_all = [&](bool with_k1) -> int {
         int e;
-        iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
-        if (with_k1 && (e = pass64(1))) return e;
-        if ((e = pass64(2))) return e;
-        if (all && nreduce > 1) {
-            unsigned bits = 1;
-            while ((1ull << bits) < nreduce) bits++;
-            if ((e = pass32(3, bits))) return e;
+        if (!with_k1 && fold) return pass64(4, fold, true);
+        if (with_k1) {
+            if ((e = pass64(1, 0, true))) return e;
+            if ((e = pass64(2))) return e;
+        } else if ((e = pass64(2, 0, true))) {
+            return e;
         }
+        if (pbits && (e = pass32(3, pbits))) return e;
         return 0;
     };
     // Tied runs of up to kMaxRun are insertion-sorted in place (one thread per
@@ -561,8 +646,8 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         uint8_t* tie = ws->key_a.as<uint8_t>();
         uint8_t* lng = tie + n;
         RCHK(hipMemsetAsync(lng, 0, n, s));
-        RCHK(hipMemsetAsync(flags + 2, 0, 16, s));
-        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1);
+        RCHK(hipMemsetAsync(flags + 2, 0, 16, s));  // (flags[1] accumulates: any k1 seen by any pass)
+        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1, with_k1 ? 0u : fold);
         if (all_runs) {  // every tied run goes to the merge sort (no per-run insertion sort)
             mark_all_ties_kernel<<<grid_for(n), 256, 0, s>>>(tie, n, lng);
             RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 2, 8, hipMemcpyDeviceToHost, s));
@@ -571,7 +656,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
             return *any_long ? sort_long_runs(ws, r, pa, n, lng, ext, s) : 0;
         }
         fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, kMaxRun, flags, lng);
-        RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 3, 8, hipMemcpyDeviceToHost, s));
+        RCHK(hipMemcpyAsync(ws->h_pinned + 1, flags + 1, 24, hipMemcpyDeviceToHost, s));  // flags 1-3
         RCHK(hipStreamSynchronize(s));
         *any_long = ws->h_pinned[3] != 0;
         if (*any_long && merge) return sort_long_runs(ws, r, pa, n, lng, ext, s);
@@ -579,18 +664,22 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     };
     int e;
     if ((e = sort_all(k1_first))) return e;
-    if (k1_first) {
+    if (grep) {  // every tied run (equal first 16, or with !grep_k1 first 8 - pbits / 8, bytes) merge-sorted
         bool any_long = false;
-        if ((e = fix_ties(true, true, &any_long, true))) return e;
-    } else if (has_k1 || has_long || app != 1) {
+        if ((e = fix_ties(k1_first, true, &any_long, true))) return e;
+    } else {
         // keys of 9-16 bytes sharing an 8-byte prefix in a long run: sort again with
         // the k1 pass (cheaper than a comparison sort); any other long run (keys
-        // > 16 bytes, grep lines): comparison merge sort of the run members
+        // > 16 bytes; 8-byte keys differing in the folded-away bits): comparison
+        // merge sort of the run members
         bool any_long = false;
-        if ((e = fix_ties(false, !has_k1, &any_long))) return e;
-        if (has_k1 && any_long) {
+        if ((e = fix_ties(false, false, &any_long))) return e;
+        const bool has_k1 = ws->h_pinned[1] != 0;
+        if (any_long && has_k1) {
             if ((e = sort_all(true))) return e;
             if ((e = fix_ties(true, true, &any_long))) return e;
+        } else if (any_long) {
+            if ((e = sort_long_runs(ws, r, pa, n, ws->key_a.as<uint8_t>() + n, ext, s))) return e;
         }
     }
     uint64_t* ll = ws->key_b.as<uint64_t>();
@@ -600,27 +689,18 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     RCHK(rocprim::exclusive_scan(nullptr, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
     RCHK(ws->tmp.ensure(tb));
     RCHK(rocprim::exclusive_scan(ws->tmp.p, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
-    RCHK(hipMemcpyAsync(ws->h_pinned, off + (n - 1), 8, hipMemcpyDeviceToHost, s));
-    RCHK(hipMemcpyAsync(ws->h_pinned + 1, ll + (n - 1), 8, hipMemcpyDeviceToHost, s));
-    RCHK(hipStreamSynchronize(s));
-    const uint64_t total = ws->h_pinned[0] + ws->h_pinned[1];
-    RCHK(ws->out.ensure(total + 16));
     uint8_t* out = ws->out.as<uint8_t>();
     if (app != 1)
         write_lines_wave_kernel<<<2048, 256, 0, s>>>(r, pa, n, off, out);
     else
-        write_lines_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, app, off, out);
-    if (all) {
-        RCHK(ws->offs.ensure((size_t)(nparts + 1) * 8));
-        part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, total, nparts, ws->offs.as<uint64_t>());
-        RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
-        RCHK(hipStreamSynchronize(s));
-    } else {
-        h_offsets[0] = 0;
-        h_offsets[1] = total;
-    }
+        write_wc_lines_kernel<<<(unsigned)std::min<uint64_t>((n + kWlLines - 1) / kWlLines, 8192), kWlLines, 0, s>>>(
+            r, pa, n, off, ll, out);
+    part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, ll, nparts, !all,
+                                                                 ws->offs.as<uint64_t>());
+    RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
+    RCHK(hipStreamSynchronize(s));
     *d_out = out;
-    *out_n = total;
+    *out_n = h_offsets[nparts];
     return 0;
 }
 

@@ -171,6 +171,29 @@ def test_wc_high_cardinality_buckets(ctx, rounds):
         ctx.set_option("spill_hi_keys", 0)
 
 
+@pytest.mark.parametrize("digit_bits,fold,grep_k1", [(8, 0, 0), (8, -1, 0), (10, 0, 0), (10, -1, -1), (8, 0, -1)])
+def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1):
+    """The reduce's sort variants give the same bytes: 8- or 10-bit radix digits,
+    the partition folded into the first key pass (default) or sorted on its own,
+    grep lines radix-sorted on 16 key bytes (default) or 8 (more tied runs).
+    The corpus has 8-byte keys differing only in their last byte's low bits (ties
+    of the folded key), 9-16-byte keys sharing 8-byte prefixes, long keys and UTF-8."""
+    base = [b"abcdefg" + bytes([c]) for c in range(ord("a"), ord("z") + 1)]
+    base += [b"abcdefgh" + bytes([c]) * k for c in range(ord("a"), ord("p")) for k in (1, 3, 8, 20)]
+    words = b" ".join(base * 3) + b"\n"
+    files = [words] + cases.synthetic(C.KIND_UTF8, 30000, [2_000_000, 700_001], 41, 0.001)
+    ctx.set_option("sort_digit_bits", digit_bits)
+    ctx.set_option("sort_fold_part", fold)
+    ctx.set_option("grep_sort_k1", grep_k1)
+    try:
+        check(ctx, "wc", files, nreduces=(1, 10, 64))
+        check(ctx, "grep:distributed", cases.synthetic_grep(20000, [1_500_000], 42), nreduces=(1, 10))
+    finally:
+        ctx.set_option("sort_digit_bits", 0)
+        ctx.set_option("sort_fold_part", 0)
+        ctx.set_option("grep_sort_k1", 0)
+
+
 def test_wc_large_vs_oracle(wctx):
     """64 MB C2-style corpus: full bytes vs the C oracle."""
     voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
