@@ -297,11 +297,16 @@ __device__ int64_t first_nl_from(const uint8_t* in, int64_t n, int64_t q0) {
     return n;
 }
 
-// Append the (s, e) line pairs and deferred hit indices of a wave (one cursor
-// atomic each per wave).
+// Workgroup size of the grep line kernels: their shared cursors (lines, table
+// fill, records) take one device atomic per 1024 items.  Same-address atomics
+// serialize at ~25 ns each: one per wave cost C3 ~0.15 ms per kernel.
+constexpr int kLineWG = 1024, kLineWaves = kLineWG / 64;
+
+// Append the (s, e) line pairs (one cursor atomic per workgroup) and deferred
+// hit indices (rare: one per wave that has any) of a workgroup.
 __device__ __forceinline__ void put_line(const Tables& t, uint64_t cap, bool keep, uint64_t s, uint64_t e, bool defer,
-                                         uint64_t i) {
-    const unsigned long long o = wave_alloc(&t.ctr->nlines, keep);
+                                         uint64_t i, unsigned long long* scratch) {
+    const unsigned long long o = block_alloc<kLineWaves>(&t.ctr->nlines, keep ? 1u : 0u, scratch);
     if (keep) {
         if (o < cap) {
             t.lines[2 * o] = s;
@@ -318,8 +323,9 @@ __device__ __forceinline__ void put_line(const Tables& t, uint64_t cap, bool kee
 }
 
 // One lane per hit.  plen == 0: the hits are line starts (empty pattern).
-__global__ void __launch_bounds__(256) grep_resolve_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
-                                                           Tables t, uint64_t nhits) {
+__global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
+                                                               Tables t, uint64_t nhits) {
+    __shared__ unsigned long long scratch[kLineWaves + 1];
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool keep = false, defer = false;
     int64_t s = 0, e = 0;
@@ -341,7 +347,7 @@ __global__ void __launch_bounds__(256) grep_resolve_kernel(const uint8_t* __rest
             if (e == -2) { keep = false; defer = true; }
         }
     }
-    put_line(t, nhits, keep, (uint64_t)s, (uint64_t)e, defer, i);
+    put_line(t, nhits, keep, (uint64_t)s, (uint64_t)e, defer, i, scratch);
 }
 
 // Deferred hits: one 256-thread workgroup each, 16 bytes per lane per step
@@ -435,7 +441,8 @@ __device__ uint64_t hash_bytes(const uint8_t* in, int64_t s, int64_t e, uint64_t
     return h;
 }
 
-__global__ void __launch_bounds__(256) grep_insert_kernel(const uint8_t* __restrict__ in, Tables t, uint64_t nlines) {
+__global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __restrict__ in, Tables t, uint64_t nlines) {
+    __shared__ unsigned long long scratch[2 * kLineWaves];
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool claimed = false;
     uint64_t len = 0;
@@ -452,16 +459,25 @@ __global__ void __launch_bounds__(256) grep_insert_kernel(const uint8_t* __restr
         }
         claimed = long_try_insert_counted(t, h, in + s, len);
     }
-    // fill counters once per wave (same-address device atomics serialize)
-    const uint64_t mc = __ballot(claimed);
-    unsigned long long bytes = claimed ? len : 0;
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) bytes += __shfl_xor(bytes, off);
-    if (mc && lane_id() == (uint32_t)__builtin_ctzll(mc)) {
-        const unsigned long long k = (unsigned long long)__popcll(mc);
-        atomicAdd(&t.ctr->long_bytes, bytes);
-        const unsigned long long used = atomicAdd(&t.ctr->long_used, k) + k;
-        if (used * 10 > (t.lo_mask + 1) * 7) set_status(t.ctr, kStLongFull);
+    // fill counters once per workgroup (same-address device atomics serialize)
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint64_t k = wave_sum(claimed ? 1u : 0u), bytes = wave_sum(claimed ? len : 0);
+    if (lane == 0) {
+        scratch[wv] = k;
+        scratch[kLineWaves + wv] = bytes;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long kk = 0, bb = 0;
+        for (int w = 0; w < kLineWaves; w++) {
+            kk += scratch[w];
+            bb += scratch[kLineWaves + w];
+        }
+        if (kk) {
+            atomicAdd(&t.ctr->long_bytes, bb);
+            const unsigned long long used = atomicAdd(&t.ctr->long_used, kk) + kk;
+            if (used * 10 > (t.lo_mask + 1) * 7) set_status(t.ctr, kStLongFull);
+        }
     }
 }
 
@@ -490,8 +506,12 @@ __global__ void nrec_add_kernel(Counters* ctr, const uint32_t* d_count) { ctr->n
 // One LongTable record: key bytes copied to the arena at `off` by aligned
 // 16-byte blocks (the representative sits at a random input offset: one load
 // per block, not a chain of byte loads), prefix words and partition from them.
-__device__ __forceinline__ void emit_long_rec(const Tables& t, const LongSlot& s, uint64_t o, uint64_t off, uint64_t len) {
-    if (o >= t.out_cap || off + len > t.out.arena_n) { set_status(t.ctr, kStRecFull); return; }
+// Record o of a LongTable key (its bytes go to the arena at off, copied by the
+// caller): the first 16 bytes as k0/k1 and the partition from FNV-1a-32 of all
+// bytes (worker.go:76), read in aligned 16-byte blocks.  Returns false (and sets
+// kStRecFull) when the record or arena buffer is too small.
+__device__ __forceinline__ bool emit_long_rec(const Tables& t, const LongSlot& s, uint64_t o, uint64_t off, uint64_t len) {
+    if (o >= t.out_cap || off + len > t.out.arena_n) { set_status(t.ctr, kStRecFull); return false; }
     uint32_t h = 2166136261u;
     uint64_t k0 = 0, k1 = 0;
     for (int64_t q = 0; q < (int64_t)len;) {
@@ -503,7 +523,6 @@ __device__ __forceinline__ void emit_long_rec(const Tables& t, const LongSlot& s
             const int64_t k = bi + j;
             if (k < q || k >= (int64_t)len) continue;
             const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-            t.out.arena[off + k] = (uint8_t)b;
             h = fnv1a32_step(h, b);
             if (k < 8) k0 |= (uint64_t)b << (8 * k);
             else if (k < 16) k1 |= (uint64_t)b << (8 * (k - 8));
@@ -516,6 +535,7 @@ __device__ __forceinline__ void emit_long_rec(const Tables& t, const LongSlot& s
     t.out.cnt[o] = s.count;
     t.out.part[o] = (h & 0x7fffffffu) % t.nreduce;
     t.out.koff[o] = off;
+    return true;
 }
 
 // LongTable -> records.  Each wave takes kCollectSlots x 64 slots per step and
@@ -523,12 +543,17 @@ __device__ __forceinline__ void emit_long_rec(const Tables& t, const LongSlot& s
 // (same-address device atomics serialize at the memory side: one pair per 64
 // slots of a 1 M-slot table cost ~0.6 ms).
 constexpr int kCollectSlots = 8;
-__global__ void __launch_bounds__(256) collect_long_kernel(Tables t) {
-    const uint32_t lane = threadIdx.x & 63;
+__global__ void __launch_bounds__(kLineWG) collect_long_kernel(Tables t) {
+    __shared__ unsigned long long scratch[2 * kLineWaves + 2];
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t n = t.lo_mask + 1;
     constexpr uint64_t kStep = 64 * kCollectSlots;
     const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    for (uint64_t w0 = (((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6) * kStep; w0 < n; w0 += nw * kStep) {
+    // the loop bound is workgroup-uniform (whole workgroups step together): every
+    // thread reaches the barriers
+    const uint64_t wg0 = (uint64_t)blockIdx.x * kLineWaves * kStep;
+    for (uint64_t g0 = wg0; g0 < n; g0 += nw * kStep) {
+        const uint64_t w0 = g0 + wv * kStep;
         LongSlot sl[kCollectSlots];
         uint32_t c = 0;
         uint64_t bytes = 0;
@@ -548,22 +573,55 @@ __global__ void __launch_bounds__(256) collect_long_kernel(Tables t) {
             const uint64_t yc = __shfl_up(ic, off), yb = __shfl_up(ib, off);
             if (lane >= (uint32_t)off) { ic += yc; ib += yb; }
         }
-        unsigned long long rbase = 0, abase = 0;
-        if (lane == 63 && ic) {
-            rbase = atomicAdd(&t.ctr->nrec, (unsigned long long)ic);
-            abase = atomicAdd(&t.ctr->arena, (unsigned long long)ib);
-            atomicAdd(&t.ctr->nlong_rec, (unsigned long long)ic);
+        // one cursor pair per workgroup step: wave totals -> LDS -> exclusive
+        // prefix per wave and one atomic each
+        if (lane == 63) {
+            scratch[wv] = ic;
+            scratch[kLineWaves + wv] = ib;
         }
-        rbase = __shfl(rbase, 63);
-        abase = __shfl(abase, 63);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long rc = 0, rb = 0;
+            for (int w = 0; w < kLineWaves; w++) {
+                const unsigned long long xc = scratch[w], xb = scratch[kLineWaves + w];
+                scratch[w] = rc;
+                scratch[kLineWaves + w] = rb;
+                rc += xc;
+                rb += xb;
+            }
+            scratch[2 * kLineWaves] = rc ? atomicAdd(&t.ctr->nrec, rc) : 0ull;
+            scratch[2 * kLineWaves + 1] = rc ? atomicAdd(&t.ctr->arena, rb) : 0ull;
+            if (rc) atomicAdd(&t.ctr->nlong_rec, rc);
+        }
+        __syncthreads();
+        const uint64_t rbase = scratch[2 * kLineWaves] + scratch[wv], abase = scratch[2 * kLineWaves + 1] + scratch[kLineWaves + wv];
+        __syncthreads();
         uint64_t o = rbase + ic - c, off = abase + ib - bytes;
+        uint64_t offk[kCollectSlots];
+        uint32_t ok = 0;  // bit k: slot k's record was written (its bytes still to copy)
 #pragma unroll
         for (int k = 0; k < kCollectSlots; k++) {
+            offk[k] = off;
             if (sl[k].len == 0) continue;
             const uint64_t len = sl[k].len - 1;
-            emit_long_rec(t, sl[k], o, off, len);
+            if (emit_long_rec(t, sl[k], o, off, len)) ok |= 1u << k;
             o++;
             off += len;
+        }
+        // key bytes to the arena, one key at a time by the whole wave (consecutive
+        // lanes on consecutive bytes: a wave-instruction stores one contiguous run
+        // instead of 64 scattered bytes)
+#pragma unroll
+        for (int k = 0; k < kCollectSlots; k++) {
+            uint64_t m = __ballot((ok >> k) & 1u);
+            while (m) {
+                const int l = __builtin_ctzll(m);
+                m &= m - 1;
+                const uint8_t* src = (const uint8_t*)__shfl((unsigned long long)(uintptr_t)sl[k].rep, l);
+                const uint64_t len = __shfl((unsigned long long)sl[k].len, l) - 1;
+                uint8_t* dst = t.out.arena + __shfl((unsigned long long)offk[k], l);
+                for (uint64_t b = lane; b < len; b += 64) dst[b] = src[b];
+            }
         }
     }
 }
@@ -651,7 +709,7 @@ void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int g
 
 void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, hipStream_t s) {
     if (nhits == 0) return;
-    grep_resolve_kernel<<<(unsigned)((nhits + 255) / 256), 256, 0, s>>>(in, n, plen, t, nhits);
+    grep_resolve_kernel<<<(unsigned)((nhits + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, n, plen, t, nhits);
 }
 
 void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t ndefer,
@@ -663,7 +721,7 @@ void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, cons
 
 void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, hipStream_t s) {
     if (nlines == 0) return;
-    grep_insert_kernel<<<(unsigned)((nlines + 255) / 256), 256, 0, s>>>(in, t, nlines);
+    grep_insert_kernel<<<(unsigned)((nlines + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, t, nlines);
 }
 
 int launch_collect(const Tables& t, ReduceWs* ws, uint64_t base, uint64_t short_used, bool long_table, hipStream_t s) {
@@ -678,8 +736,8 @@ int launch_collect(const Tables& t, ReduceWs* ws, uint64_t base, uint64_t short_
     }
     if (long_table) {
         const uint64_t steps = (t.lo_mask + 1 + 64 * kCollectSlots - 1) / (64 * kCollectSlots);  // wave steps
-        const uint64_t g = (steps + 3) / 4 < 2048 ? (steps + 3) / 4 : 2048;
-        collect_long_kernel<<<(unsigned)g, 256, 0, s>>>(t);
+        const uint64_t g = (steps + kLineWaves - 1) / kLineWaves < 512 ? (steps + kLineWaves - 1) / kLineWaves : 512;
+        collect_long_kernel<<<(unsigned)g, kLineWG, 0, s>>>(t);
     }
     return (int)hipGetLastError();
 }

@@ -308,35 +308,17 @@ __global__ void line_len_kernel(Recs r, const uint32_t* perm, uint64_t n, int ap
     }
 }
 
-// grep lines ("L L\n"): one wave per line, lanes on consecutive output bytes
-// (coalesced loads and stores).  Key bytes from the arena, or from k0/k1 for a
-// record without arena bytes (<= 16 bytes).
-__global__ void write_lines_wave_kernel(Recs r, const uint32_t* perm, uint64_t n, const uint64_t* off, uint8_t* out) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t nw = (uint64_t)gridDim.x * (blockDim.x / 64);
-    for (uint64_t i = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); i < n; i += nw) {
-        const uint32_t j = perm[i];
-        const uint32_t len = r.len[j];
-        const uint64_t ko = r.koff[j], k0 = r.k0[j], k1 = r.k1[j];
-        const uint8_t* kb = r.arena + (ko == ~0ull ? 0 : ko);
-        uint8_t* o = out + off[i];
-        for (uint32_t k = lane; k < 2 * len + 2; k += 64) {
-            const uint32_t src = k < len ? k : k - len - 1;
-            const uint8_t b = k == len || k == 2 * len + 1 ? (uint8_t)0
-                              : ko != ~0ull ? kb[src] : (uint8_t)((src < 8 ? k0 : k1) >> (8 * (src & 7)));
-            o[k] = k == len ? (uint8_t)' ' : k == 2 * len + 1 ? (uint8_t)'\n' : b;
-        }
-    }
-}
-
-// wc lines ("key count\n"): a block's 256 consecutive lines are one contiguous
-// output range; each thread writes its line into LDS, then the block copies the
-// range out with 16-byte stores (byte stores only at the range's two ends, which
-// neighbouring blocks share).  A range longer than the LDS buffer (very long
-// keys) is written directly, byte by byte.
-constexpr uint32_t kWlLines = 256, kWlBytes = 16384;
-__global__ void __launch_bounds__(kWlLines) write_wc_lines_kernel(Recs r, const uint32_t* perm, uint64_t n,
-                                                                    const uint64_t* off, const uint64_t* ll, uint8_t* out) {
+// Output lines ("key count\n" for wc, "line line\n" for grep): a block's 256
+// consecutive lines are one contiguous output range; each thread writes its line
+// into LDS, then the block copies the range out with 16-byte stores (byte stores
+// only at the range's two ends, which neighbouring blocks share).  A range longer
+// than the LDS buffer (very long keys) is written directly, byte by byte.
+constexpr uint32_t kWlLines = 256;
+template <int kApp>
+__global__ void __launch_bounds__(kWlLines) write_lines_staged_kernel(Recs r, const uint32_t* perm, uint64_t n,
+                                                                        const uint64_t* off, const uint64_t* ll,
+                                                                        uint8_t* out) {
+    constexpr uint32_t kWlBytes = kApp == 1 ? 16384 : 49152;  // C2 lines ~14 B, C3 lines ~120 B
     __shared__ __attribute__((aligned(16))) uint8_t buf[kWlBytes];
     const uint32_t tid = threadIdx.x;
     for (uint64_t i0 = (uint64_t)blockIdx.x * kWlLines; i0 < n; i0 += (uint64_t)gridDim.x * kWlLines) {
@@ -351,13 +333,38 @@ __global__ void __launch_bounds__(kWlLines) write_wc_lines_kernel(Recs r, const 
             const uint64_t k0 = r.k0[j], k1 = r.k1[j];
             const uint8_t* kb = len > 16 ? r.arena + r.koff[j] : nullptr;
             const uint64_t v = r.cnt[j];
-            const uint32_t d = ndigits(v);
+            const uint32_t d = kApp == 1 ? ndigits(v) : 0u;
             auto emit = [&](auto o) {
+                if (kApp != 1 && kb) {  // grep: the line twice, its arena bytes read in aligned 16-byte blocks
+                    for (int64_t q = 0; q < (int64_t)len;) {
+                        const uintptr_t a = (uintptr_t)(kb + q), ab = a & ~(uintptr_t)15;
+                        const int64_t bi = q - (int64_t)(a - ab);
+                        const uint4 v4 = *(const uint4*)ab;
+                        const uint32_t w4[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+                        for (int b = 0; b < 16; b++) {
+                            const int64_t k = bi + b;
+                            if (k < q || k >= (int64_t)len) continue;
+                            const uint8_t c = (uint8_t)(w4[b >> 2] >> (8 * (b & 3)));
+                            o[k] = c;
+                            o[len + 1 + k] = c;
+                        }
+                        q = bi + 16;
+                    }
+                    o[len] = ' ';
+                    o[2 * len + 1] = '\n';
+                    return;
+                }
                 for (uint32_t k = 0; k < len; k++)
                     o[k] = kb ? kb[k] : (uint8_t)((k < 8 ? k0 : k1) >> (8 * (k & 7)));
                 o[len] = ' ';
-                put_digits(o + len + 1, v, d);
-                o[len + 1 + d] = '\n';
+                if (kApp == 1) {
+                    put_digits(o + len + 1, v, d);
+                    o[len + 1 + d] = '\n';
+                } else {
+                    for (uint32_t k = 0; k < len; k++) o[len + 1 + k] = o[k];
+                    o[2 * len + 1] = '\n';
+                }
             };
             if (staged) emit(buf + (off[i] - a0));
             else emit(out + off[i]);
@@ -690,11 +697,9 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     RCHK(ws->tmp.ensure(tb));
     RCHK(rocprim::exclusive_scan(ws->tmp.p, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
     uint8_t* out = ws->out.as<uint8_t>();
-    if (app != 1)
-        write_lines_wave_kernel<<<2048, 256, 0, s>>>(r, pa, n, off, out);
-    else
-        write_wc_lines_kernel<<<(unsigned)std::min<uint64_t>((n + kWlLines - 1) / kWlLines, 8192), kWlLines, 0, s>>>(
-            r, pa, n, off, ll, out);
+    const unsigned wl_grid = (unsigned)std::min<uint64_t>((n + kWlLines - 1) / kWlLines, 8192);
+    if (app != 1) write_lines_staged_kernel<2><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
+    else write_lines_staged_kernel<1><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
     part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, ll, nparts, !all,
                                                                  ws->offs.as<uint64_t>());
     RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
