@@ -216,6 +216,7 @@ struct mrg_parts {
     int app = 0;
     uint32_t nreduce = 1;
     int device = 0;
+    bool ascii = false;  // every key byte < 0x80 (the map saw no byte >= 0x80): the reduce packs its sort key
     Recs r{};
     void* block = nullptr;  // record arrays
     uint8_t* arena = nullptr;
@@ -821,6 +822,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         p->app = MRG_APP_WC;
         p->nreduce = nreduce;
         p->device = c->device;
+        p->ascii = h.chunks_utf8 == 0;
         p->r = t.out;
         p->r.n = h.nrec;
         p->r.arena_n = h.long_bytes;
@@ -1213,6 +1215,7 @@ int mrg_parts_merge(mrg_ctx* c, mrg_parts* into, const mrg_parts* from) {
     into->arena = m->arena;
     into->arena_bytes = m->arena_bytes;
     into->r = m->r;
+    into->ascii = into->ascii && from->ascii;
     m->block = nullptr;
     m->arena = nullptr;
     delete m;
@@ -1544,14 +1547,14 @@ static int reduce_common(mrg_ctx* c, const mrg_parts* p, uint32_t only, uint8_t*
     if ((rc = bind(c))) return rc;
     HCHK(c, hipEventRecord(c->ev[4], c->s));
     if (only == 0xFFFFFFFFu) {
-        rc = reduce_format(c->rws, p->r, p->app, p->nreduce, only, d_out, n_out, offsets, c->s);
+        rc = reduce_format(c->rws, p->r, p->app, p->nreduce, only, d_out, n_out, offsets, c->s, p->ascii);
         if (rc) return fail(c, MRG_EDEVICE, "reduce_format: %s", hipGetErrorString((hipError_t)rc));
     } else {
         mrg_parts* sel = nullptr;
         if ((rc = parts_alloc(c, p->r.n, 0, p->app, p->nreduce, &sel))) return rc;
         Recs d = sel->r;
         if (select_recs(c->rws, p->r, p->nreduce, only, &d, c->s)) { mrg_parts_free(sel); return fail(c, MRG_EDEVICE, "select"); }
-        rc = reduce_format(c->rws, d, p->app, p->nreduce, only, d_out, n_out, offsets, c->s);
+        rc = reduce_format(c->rws, d, p->app, p->nreduce, only, d_out, n_out, offsets, c->s, p->ascii);
         HCHK(c, hipStreamSynchronize(c->s));
         mrg_parts_free(sel);
         if (rc) return fail(c, MRG_EDEVICE, "reduce_format: %s", hipGetErrorString((hipError_t)rc));

@@ -217,8 +217,9 @@ void reduce_ws_free(ReduceWs*);
 void reduce_ws_set(ReduceWs*, int digit_bits, int fold_part, int grep_k1);
 // Sort recs (optionally only partition `only_part`), format "key value\n" lines.
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
+// ascii_keys: every key byte is < 0x80 (the sort key then packs 7 bits per byte).
 int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,
-                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s);
+                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s, bool ascii_keys);
 // Indices of occupied ShortTable slots; *d_count (device) = how many.
 int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64_t max_used, uint32_t** d_idx,
                       uint32_t** d_count, hipStream_t s);

@@ -72,7 +72,7 @@ void reduce_ws_free(ReduceWs* w) {
     delete w;
 }
 
-// flags[1]: any k1 != 0 (mark_ties), flags[2]: tied runs found, flags[3]: long runs.
+// flags[2]: tied runs found, flags[3]: long runs (flags[0], flags[1]: unused).
 
 __global__ void iota_kernel(uint32_t* p, uint64_t n) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -84,8 +84,18 @@ __global__ void iota_kernel(uint32_t* p, uint64_t n) {
 // loads.
 constexpr int kExtWords = 6;
 
+// The first 8 key bytes of an ASCII key (every byte < 0x80) in 56 bits: the
+// low 7 bits of each byte, first byte highest (order-preserving, lossless).
+__device__ __forceinline__ uint64_t pack7(uint64_t k0) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int b = 0; b < 8; b++) v = (v << 7) | ((k0 >> (8 * b)) & 0x7Full);
+    return v;
+}
+
 // which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part, 4 = part in the top
-// `fold` bits over bswap(k0) >> fold (the first 64 - fold key bits)
+// `fold` bits over bswap(k0) >> fold (the first 64 - fold key bits), 5 = part
+// over pack7(k0) (ASCII keys: 56 + fold bits, nothing dropped).
 __global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32,
                                   uint32_t fold = 0) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -95,7 +105,19 @@ __global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int 
         else if (which == 1) k64[i] = __builtin_bswap64(r.k1[j]);
         else if (which == 2) k64[i] = __builtin_bswap64(r.k0[j]);
         else if (which == 4) k64[i] = ((uint64_t)r.part[j] << (64 - fold)) | (__builtin_bswap64(r.k0[j]) >> fold);
+        else if (which == 5) k64[i] = ((uint64_t)r.part[j] << 56) | pack7(r.k0[j]);
         else k32[i] = r.part[j];
+    }
+}
+
+// tie[i] = 1 when sorted position i has the same sort key as i - 1 (the single
+// folded / packed key pass: equal keys are equal (partition, prefix)).
+__global__ void mark_ties_sorted_kernel(const uint64_t* keys, uint64_t n, uint8_t* tie, unsigned long long* flags) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint8_t t = i > 0 && keys[i] == keys[i - 1] ? 1 : 0;  // (coalesced: no record gathers)
+        tie[i] = t;
+        if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
     }
 }
 
@@ -211,9 +233,7 @@ __global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8
         uint8_t t = 0;
         if (i > 0 && same_prefix(r, perm[i - 1], perm[i], with_k1, fold)) t = 1;
         tie[i] = t;
-        const bool k1 = r.k1[perm[i]] != 0;  // flags[1]: some key has more than 8 bytes
         if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
-        if (__ballot(k1) && (threadIdx.x & 63) == 0 && flags[1] == 0) atomicOr(&flags[1], 1ull);
     }
 }
 
@@ -559,7 +579,7 @@ int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs
 }
 
 int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,
-                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s) {
+                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s, bool ascii_keys) {
     const uint64_t n = r.n;
     const bool all = only_part == 0xFFFFFFFFu;
     const uint32_t nparts = all ? nreduce : 1;
@@ -593,9 +613,10 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     // launches, than the larger merge sort they save)
     const bool grep = app != 1;
     const bool k1_first = grep && ws->grep_k1;
-    // 10-bit digits: C3 reduce 1.50 -> 1.44 ms (15 passes instead of 17); C2 unchanged
+    // 10-bit digits: C3 reduce 1.50 -> 1.44 ms (15 passes instead of 17); C2's
+    // packed 60-bit key: 6 passes instead of 8
     const int saved_bits = ws->digit_bits;
-    if (saved_bits == 0) ws->digit_bits = grep ? 10 : 8;
+    if (saved_bits == 0) ws->digit_bits = 10;
     struct Restore {
         ReduceWs* w;
         int b;
@@ -613,12 +634,12 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         std::swap(pa, pb);
         return e;
     };
-    auto pass64 = [&](int which, uint32_t fold = 0, bool first = false) -> int {
+    auto pass64 = [&](int which, uint32_t fold = 0, bool first = false, unsigned bits = 64) -> int {
         // first: the permutation is the identity (keys gathered in record order)
         gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, first ? nullptr : pa, n, which, ws->key_a.as<uint64_t>(),
                                                       nullptr, fold);
         if (first) iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
-        int e = sort_pass<uint64_t>(ws, ws->key_a.as<uint64_t>(), ws->key_b.as<uint64_t>(), pa, pb, n, 64, s);
+        int e = sort_pass<uint64_t>(ws, ws->key_a.as<uint64_t>(), ws->key_b.as<uint64_t>(), pa, pb, n, bits, s);
         std::swap(pa, pb);
         return e;
     };
@@ -629,12 +650,18 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     if (all && nreduce > 1)
         while ((1ull << pbits) < nreduce) pbits++;
     const uint32_t fold = ws->fold_part && pbits > 0 && pbits <= 16 ? pbits : 0;
+    // ASCII keys (the map saw no byte >= 0x80): (partition, 7 bits per byte of the
+    // first 8 bytes) loses nothing and sorts 56 + pbits bits
+    const bool packed = ws->fold_part && ascii_keys && pbits <= 8 && !grep;
+    bool keys_sorted = false;  // key_b holds the sort keys of the single (partition, prefix) pass
     // Stable LSD passes: (k1), k0, partition.  The k1 pass (bytes 8-15) is
     // skipped at first: keys that share their first 8 bytes form short tied runs
     // that fix_ties orders by full comparison; if a run is long (many keys with
     // one 8-byte prefix), everything is sorted again with the k1 pass.
     auto sort_all = [&](bool with_k1) -> int {
         int e;
+        keys_sorted = !with_k1 && (packed || fold);
+        if (!with_k1 && packed) return pass64(5, 0, true, 56 + pbits);
         if (!with_k1 && fold) return pass64(4, fold, true);
         if (with_k1) {
             if ((e = pass64(1, 0, true))) return e;
@@ -653,8 +680,9 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         uint8_t* tie = ws->key_a.as<uint8_t>();
         uint8_t* lng = tie + n;
         RCHK(hipMemsetAsync(lng, 0, n, s));
-        RCHK(hipMemsetAsync(flags + 2, 0, 16, s));  // (flags[1] accumulates: any k1 seen by any pass)
-        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1, with_k1 ? 0u : fold);
+        RCHK(hipMemsetAsync(flags + 2, 0, 16, s));
+        if (!with_k1 && keys_sorted) mark_ties_sorted_kernel<<<grid_for(n), 256, 0, s>>>(ws->key_b.as<uint64_t>(), n, tie, flags);
+        else mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1, with_k1 ? 0u : fold);
         if (all_runs) {  // every tied run goes to the merge sort (no per-run insertion sort)
             mark_all_ties_kernel<<<grid_for(n), 256, 0, s>>>(tie, n, lng);
             RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 2, 8, hipMemcpyDeviceToHost, s));
@@ -679,14 +707,13 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         // the k1 pass (cheaper than a comparison sort); any other long run (keys
         // > 16 bytes; 8-byte keys differing in the folded-away bits): comparison
         // merge sort of the run members
+        // (a run over 64 needs 65 distinct keys sharing the sort key's prefix:
+        // 9-16-byte keys, or longer ones; <= 8-byte keys differ within 2^fold)
         bool any_long = false;
         if ((e = fix_ties(false, false, &any_long))) return e;
-        const bool has_k1 = ws->h_pinned[1] != 0;
-        if (any_long && has_k1) {
+        if (any_long) {
             if ((e = sort_all(true))) return e;
             if ((e = fix_ties(true, true, &any_long))) return e;
-        } else if (any_long) {
-            if ((e = sort_long_runs(ws, r, pa, n, ws->key_a.as<uint8_t>() + n, ext, s))) return e;
         }
     }
     uint64_t* ll = ws->key_b.as<uint64_t>();

@@ -706,7 +706,7 @@ __device__ __forceinline__ void defer_miss(AL& A, const Tables& t, uint64_t k0, 
     miss++;
 }
 
-template <uint32_t amode, bool kMid, uint32_t kAggUnroll, class AL>
+template <uint32_t amode, bool kMid, uint32_t kAggUnroll, bool kRound0, class AL>
 __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* pool_b, const uint32_t* gcounts,
                                          uint64_t gstride, uint32_t nwg, const uint64_t* gbase, bool keep_miss,
                                          uint64_t& miss) {
@@ -724,34 +724,267 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
     };
     const uint32_t lane = threadIdx.x & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    // The wave's streams are wv + kAggWaves * j, j < js; lane j holds stream j's
-    // record count, so moving to the next stream is a readlane, not a load.
-    const uint32_t js = nwg > wv ? (nwg - wv + kAggWaves - 1) / kAggWaves : 0u;
-    uint32_t vcnt = 0;
-    if (lane < js) {
-        uint32_t b0;
-        vcnt = gbase ? part_range(wv + kAggWaves * lane, b0) : gcounts[wv + kAggWaves * lane];
-    }
-    // wave-uniform cursor: stream j, record offset off within it (cnt records)
-    uint32_t j = 0, off = 0, cnt = __builtin_amdgcn_readlane(vcnt, 0);
-    while (j < js && off >= cnt) {
-        j++;
-        cnt = j < js ? __builtin_amdgcn_readlane(vcnt, j) : 0u;
-    }
     uint4 cur[kAggUnroll], nxt[kAggUnroll];
-    auto load = [&](uint32_t jj, uint32_t o, uint32_t c, uint4* r) {
-        const uint32_t sid = wv + kAggWaves * jj;
-        uint64_t row = (uint64_t)sid * gstride;
-        if (gbase) {
-            uint32_t b0 = 0;
-            if (jj < js) part_range(sid, b0);
-            row = jj < js ? gbase[sid % kAggSegs] + b0 : 0ull;
+    // (the block body appears in both loaders: as a lambda it changed the register
+    // allocation, 102 -> 128 VGPRs + scratch)
+    // first-set variant: the streams as one virtual sequence (see below)
+    // (measured: for C2's main aggregation, ~2.7 K-record 8-byte streams, the
+    // per-record search cost more than the idle lanes it saves, 1.28 -> 1.71 ms;
+    // for the dictionary sample's few-record streams the whole dictionary step
+    // went 0.30 -> 0.21 ms)
+    constexpr bool kVirtual = (amode & 256) != 0;
+    static_assert(kMid || kAggUnroll % 2 == 0, "8-byte records load in pairs");
+    if constexpr (kVirtual) {
+        // The wave's streams are wv + kAggWaves * j, j < js, read as ONE virtual
+        // sequence of records, so a block spans stream ends instead of idling lanes
+        // past them (a C2 bucket's 16-byte map streams hold ~340 records, the
+        // dictionary sample's a few).  Lane j holds stream j's record count, start
+        // and exclusive prefix; record g of the sequence lies in the last stream j
+        // with prefix <= g (binary search over the lanes).  Round 0's 8-byte streams
+        // count as even lengths, so records 2i and 2i+1 share one aligned 16-byte
+        // load (a map stream starts 16-byte aligned; the padding record reads as
+        // zero; 8-byte loads run at ~0.6x the 16-byte rate, MI355X_MICROARCH.md).
+        const uint32_t js = nwg > wv ? (nwg - wv + kAggWaves - 1) / kAggWaves : 0u;
+        uint32_t vcnt = 0;
+        uint64_t vrow = 0;
+        if (lane < js) {
+            const uint32_t sid = wv + kAggWaves * lane;
+            if constexpr (!kRound0) {
+                uint32_t b0;
+                vcnt = part_range(sid, b0);
+                vrow = gbase[sid % kAggSegs] + b0;
+            } else {
+                vcnt = gcounts[sid];
+                vrow = (uint64_t)sid * gstride;
+            }
         }
-        if constexpr (!kMid && (kAggUnroll % 2) == 0) {
-            if (!gbase) {
+        constexpr bool pairs = !kMid && kRound0;
+        const uint32_t vlen = pairs ? (vcnt + 1u) & ~1u : vcnt;
+        uint32_t incl = vlen;
+    #pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(incl, o);
+            if (lane >= (uint32_t)o) incl += y;
+        }
+        const uint32_t ex = incl - vlen;
+        const uint32_t T = __builtin_amdgcn_readlane(incl, 63);
+        // record g: its element index in pool_b and the records of its stream from g on
+        auto locate = [&](uint32_t g, uint64_t& at, uint32_t& left) {
+            uint32_t jl = 0;
+    #pragma unroll
+            for (uint32_t st = 32; st >= 1; st >>= 1) {
+                // every lane takes part in the shuffle (a bpermute from a lane that
+                // is not active returns nothing), then the condition applies
+                const uint32_t c = jl + st;  // <= 63
+                const uint32_t e = (uint32_t)__shfl((int)ex, (int)c);
+                if (c < js && e <= g) jl = c;
+            }
+            const uint32_t o = g - (uint32_t)__shfl((int)ex, (int)jl);
+            at = (uint64_t)__shfl((unsigned long long)vrow, (int)jl) + o;
+            left = (uint32_t)__shfl((int)vcnt, (int)jl) - o;
+        };
+        auto load = [&](uint32_t g0, uint4* r) {
+            if constexpr (pairs) {
+    #pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll / 2; u++) {
+                    const uint32_t g = g0 + 2 * (u * kWave + lane);
+                    uint64_t at;
+                    uint32_t left;
+                    locate(g, at, left);
+                    uint4 v = make_uint4(0, 0, 0, 0);
+                    if (g < T) v = *(const uint4*)((const uint64_t*)pool_b + at);
+                    if (g >= T || left < 2) v.z = v.w = 0;  // the padding record of an odd stream
+                    r[2 * u] = make_uint4(v.x, v.y, 0, 0);
+                    r[2 * u + 1] = make_uint4(v.z, v.w, 0, 0);
+                }
+                return;
+            }
+    #pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                const uint32_t g = g0 + u * kWave + lane;
+                uint64_t at;
+                uint32_t left;
+                locate(g, at, left);
+                if (g >= T) {
+                    r[u] = make_uint4(0, 0, 0, 0);
+                } else if constexpr (kMid) {
+                    r[u] = ((const uint4*)pool_b)[at];
+                } else {
+                    const uint64_t k = ((const uint64_t*)pool_b)[at];
+                    r[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), 0, 0);
+                }
+            }
+        };
+        if (T == 0) return;
+        load(0, cur);
+        for (uint32_t g0 = 0; g0 < T; g0 += kAggBlock) {
+            load(g0 + kAggBlock, nxt);  // the next block in flight while this one is counted
+            uint32_t h[kAggUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) h[u] = fold32(cur[u].x, cur[u].y, cur[u].z, cur[u].w);
+            if constexpr ((amode & 128) != 0) {
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) miss += h[u];
+            } else if constexpr (!kMid && (amode & 64) != 0) {
+                // first-set lookups only, each miss its own slow path (sparse tables)
+                uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    base[u] = set_base<AL::kShortSets>(h[u]);
+                    short_set_masks(A, base[u], ((uint64_t)cur[u].y << 32) | cur[u].x, m[u], z[u]);
+                }
+                bool slow[kAggUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
+                    const bool hit = valid && m[u] != 0;
+                    slow[u] = valid && m[u] == 0;
+                    const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)AL::kShortSets * 4 + lane;
+                    __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    if (slow[u]) {
+                        const uint64_t k = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                        if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
+                    }
+                }
+            } else if constexpr (!kMid) {
+                // Both sets of a key are looked up before anything diverges: a key
+                // sits in its second set only if its first was full when it was
+                // claimed (ways are never freed), so a first set with a free way and
+                // without the key settles it as new.  Only new keys (and lost claims)
+                // take the slow path, all of a lane's in one loop, so a wave runs it
+                // about once per block instead of once per record slot.
+                // mz[u]: first-set hit ways (bits 0-3), free ways (4-7), second-set hit ways (8-11)
+                uint32_t mz[kAggUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    uint32_t m, z;
+                    short_set_masks(A, set_base<AL::kShortSets>(h[u]), ((uint64_t)cur[u].y << 32) | cur[u].x, m, z);
+                    mz[u] = m | z << 4;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    if ((cur[u].x | cur[u].y) != 0 && mz[u] == 0) {
+                        uint32_t m2, z2;
+                        short_set_masks(A, set_base<AL::kShortSets>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
+                                        m2, z2);
+                        mz[u] = m2 << 8;
+                    }
+                }
+                uint32_t slow = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
+                    const uint32_t m = mz[u] & 15u, m2 = (mz[u] >> 8) & 15u;
+                    const uint32_t ci = !valid   ? (uint32_t)AL::kShortSets * 4 + lane
+                                        : m != 0  ? set_base<AL::kShortSets>(h[u]) + __builtin_ctz(m)
+                                        : m2 != 0 ? set_base<AL::kShortSets>(second_hash(h[u])) + __builtin_ctz(m2)
+                                                  : (uint32_t)AL::kShortSets * 4 + lane;
+                    if (valid && (m | m2) == 0) slow |= 1u << u;
+                    __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                while (slow) {  // this lane's new keys, one per trip (register arrays read by selects, not indexing)
+                    const uint32_t us = __builtin_ctz(slow);
+                    slow &= slow - 1;
+                    uint64_t k = 0;
+                    uint32_t hk = 0;
+#pragma unroll
+                    for (uint32_t u = 0; u < kAggUnroll; u++)
+                        if (us == u) {
+                            k = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                            hk = h[u];
+                        }
+                    if (!short_insert_slow(A, k, hk, 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
+                }
+            } else if constexpr ((amode & 64) != 0) {
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    if ((cur[u].x | cur[u].y) != 0) {
+                        const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                        if (!mid_insert(A, k0, k1, h[u], 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
+                    }
+                }
+            } else {
+                // mid keys: the same two-set lookup first (a way pending publication
+                // sends the record to the slow path, which retries or defers it)
+                uint32_t mm[kAggUnroll], slow = 0;  // mm[u]: first-set hit ways (bits 0-3), second-set (4-7)
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    uint32_t m, z, pend;
+                    const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                    mid_set_masks(A, set_base<AL::kMidSets>(h[u]), k0, k1, m, z, pend);
+                    mm[u] = m;
+                    if ((cur[u].x | cur[u].y) != 0 && m == 0 && (z | pend) != 0) slow |= 1u << u;  // new key / pending
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    if ((cur[u].x | cur[u].y) != 0 && mm[u] == 0 && !((slow >> u) & 1u)) {
+                        uint32_t m2, z2, p2;
+                        const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                        mid_set_masks(A, set_base<AL::kMidSets>(second_hash(h[u])), k0, k1, m2, z2, p2);
+                        mm[u] = m2 << 4;
+                        if (m2 == 0) slow |= 1u << u;
+                    }
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    const bool valid = (cur[u].x | cur[u].y) != 0;
+                    const uint32_t m = mm[u] & 15u, m2 = mm[u] >> 4;
+                    const uint32_t ci = !valid   ? (uint32_t)AL::kMidSets * 4 + lane
+                                        : m != 0  ? set_base<AL::kMidSets>(h[u]) + __builtin_ctz(m)
+                                        : m2 != 0 ? set_base<AL::kMidSets>(second_hash(h[u])) + __builtin_ctz(m2)
+                                                  : (uint32_t)AL::kMidSets * 4 + lane;
+                    __hip_atomic_fetch_add(&A.mc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                while (slow) {
+                    const uint32_t us = __builtin_ctz(slow);
+                    slow &= slow - 1;
+                    uint64_t k0 = 0, k1 = 0;
+                    uint32_t hk = 0;
+#pragma unroll
+                    for (uint32_t u = 0; u < kAggUnroll; u++)
+                        if (us == u) {
+                            k0 = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                            k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                            hk = h[u];
+                        }
+                    if (!mid_insert(A, k0, k1, hk, 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
+                }
+            }
+    #pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) cur[u] = nxt[u];
+        }
+
+    } else {
+        // The wave's streams are wv + kAggWaves * j, j < js, walked one after the
+        // other; lane j holds stream j's record count, so moving to the next stream
+        // is a readlane, not a load.  (The two-set variant keeps this loader: the
+        // virtual one's per-record search raises its registers past 128.)
+        const uint32_t js = nwg > wv ? (nwg - wv + kAggWaves - 1) / kAggWaves : 0u;
+        uint32_t vcnt = 0;
+        if (lane < js) {
+            uint32_t b0;
+            vcnt = !kRound0 ? part_range(wv + kAggWaves * lane, b0) : gcounts[wv + kAggWaves * lane];
+        }
+        // wave-uniform cursor: stream j, record offset off within it (cnt records)
+        uint32_t j = 0, off = 0, cnt = __builtin_amdgcn_readlane(vcnt, 0);
+        while (j < js && off >= cnt) {
+            j++;
+            cnt = j < js ? __builtin_amdgcn_readlane(vcnt, j) : 0u;
+        }
+        auto load = [&](uint32_t jj, uint32_t o, uint32_t c, uint4* r) {
+            const uint32_t sid = wv + kAggWaves * jj;
+            uint64_t row = (uint64_t)sid * gstride;
+            if constexpr (!kRound0) {
+                uint32_t b0 = 0;
+                if (jj < js) part_range(sid, b0);
+                row = jj < js ? gbase[sid % kAggSegs] + b0 : 0ull;
+            }
+            if constexpr (!kMid && kRound0) {
                 // round 0's 8-byte records: two per 16-byte load (a map stream starts
-                // 16-byte aligned and a block at a multiple of kAggBlock records);
-                // 8-byte loads run at ~0.6x the 16-byte rate (MI355X_MICROARCH.md)
+                // 16-byte aligned and a block at a multiple of kAggBlock records)
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll / 2; u++) {
                     const uint32_t i = o + 2 * (u * kWave + lane);
@@ -763,177 +996,178 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                 }
                 return;
             }
-        }
 #pragma unroll
-        for (uint32_t u = 0; u < kAggUnroll; u++) {
-            const uint32_t i = o + u * kWave + lane;
-            if (jj < js && i < c) {
-                if constexpr (kMid) {
-                    r[u] = ((const uint4*)pool_b)[row + i];
+            for (uint32_t u = 0; u < kAggUnroll; u++) {
+                const uint32_t i = o + u * kWave + lane;
+                if (jj < js && i < c) {
+                    if constexpr (kMid) {
+                        r[u] = ((const uint4*)pool_b)[row + i];
+                    } else {
+                        const uint64_t k = ((const uint64_t*)pool_b)[row + i];
+                        r[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), 0, 0);
+                    }
                 } else {
-                    const uint64_t k = ((const uint64_t*)pool_b)[row + i];
-                    r[u] = make_uint4((uint32_t)k, (uint32_t)(k >> 32), 0, 0);
+                    r[u] = make_uint4(0, 0, 0, 0);
+                }
+            }
+        };
+        load(j, off, cnt, cur);
+        while (j < js) {
+            // next block's position and loads
+            uint32_t j2 = j, off2 = off + kAggBlock, cnt2 = cnt;
+            while (j2 < js && off2 >= cnt2) {
+                j2++;
+                off2 = 0;
+                cnt2 = j2 < js ? __builtin_amdgcn_readlane(vcnt, j2) : 0u;
+            }
+            load(j2, off2, cnt2, nxt);
+            uint32_t h[kAggUnroll];
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) h[u] = fold32(cur[u].x, cur[u].y, cur[u].z, cur[u].w);
+            if constexpr ((amode & 128) != 0) {
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) miss += h[u];
+            } else if constexpr (!kMid && (amode & 64) != 0) {
+                // first-set lookups only, each miss its own slow path (sparse tables)
+                uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    base[u] = set_base<AL::kShortSets>(h[u]);
+                    short_set_masks(A, base[u], ((uint64_t)cur[u].y << 32) | cur[u].x, m[u], z[u]);
+                }
+                bool slow[kAggUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
+                    const bool hit = valid && m[u] != 0;
+                    slow[u] = valid && m[u] == 0;
+                    const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)AL::kShortSets * 4 + lane;
+                    __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    if (slow[u]) {
+                        const uint64_t k = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                        if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
+                    }
+                }
+            } else if constexpr (!kMid) {
+                // Both sets of a key are looked up before anything diverges: a key
+                // sits in its second set only if its first was full when it was
+                // claimed (ways are never freed), so a first set with a free way and
+                // without the key settles it as new.  Only new keys (and lost claims)
+                // take the slow path, all of a lane's in one loop, so a wave runs it
+                // about once per block instead of once per record slot.
+                // mz[u]: first-set hit ways (bits 0-3), free ways (4-7), second-set hit ways (8-11)
+                uint32_t mz[kAggUnroll];
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    uint32_t m, z;
+                    short_set_masks(A, set_base<AL::kShortSets>(h[u]), ((uint64_t)cur[u].y << 32) | cur[u].x, m, z);
+                    mz[u] = m | z << 4;
+                }
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    if ((cur[u].x | cur[u].y) != 0 && mz[u] == 0) {
+                        uint32_t m2, z2;
+                        short_set_masks(A, set_base<AL::kShortSets>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
+                                        m2, z2);
+                        mz[u] = m2 << 8;
+                    }
+                }
+                uint32_t slow = 0;
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
+                    const uint32_t m = mz[u] & 15u, m2 = (mz[u] >> 8) & 15u;
+                    const uint32_t ci = !valid   ? (uint32_t)AL::kShortSets * 4 + lane
+                                        : m != 0  ? set_base<AL::kShortSets>(h[u]) + __builtin_ctz(m)
+                                        : m2 != 0 ? set_base<AL::kShortSets>(second_hash(h[u])) + __builtin_ctz(m2)
+                                                  : (uint32_t)AL::kShortSets * 4 + lane;
+                    if (valid && (m | m2) == 0) slow |= 1u << u;
+                    __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                while (slow) {  // this lane's new keys, one per trip (register arrays read by selects, not indexing)
+                    const uint32_t us = __builtin_ctz(slow);
+                    slow &= slow - 1;
+                    uint64_t k = 0;
+                    uint32_t hk = 0;
+#pragma unroll
+                    for (uint32_t u = 0; u < kAggUnroll; u++)
+                        if (us == u) {
+                            k = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                            hk = h[u];
+                        }
+                    if (!short_insert_slow(A, k, hk, 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
+                }
+            } else if constexpr ((amode & 64) != 0) {
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    if ((cur[u].x | cur[u].y) != 0) {
+                        const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                        if (!mid_insert(A, k0, k1, h[u], 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
+                    }
                 }
             } else {
-                r[u] = make_uint4(0, 0, 0, 0);
-            }
-        }
-    };
-    load(j, off, cnt, cur);
-    while (j < js) {
-        // next block's position and loads
-        uint32_t j2 = j, off2 = off + kAggBlock, cnt2 = cnt;
-        while (j2 < js && off2 >= cnt2) {
-            j2++;
-            off2 = 0;
-            cnt2 = j2 < js ? __builtin_amdgcn_readlane(vcnt, j2) : 0u;
-        }
-        load(j2, off2, cnt2, nxt);
-        uint32_t h[kAggUnroll];
+                // mid keys: the same two-set lookup first (a way pending publication
+                // sends the record to the slow path, which retries or defers it)
+                uint32_t mm[kAggUnroll], slow = 0;  // mm[u]: first-set hit ways (bits 0-3), second-set (4-7)
 #pragma unroll
-        for (uint32_t u = 0; u < kAggUnroll; u++) h[u] = fold32(cur[u].x, cur[u].y, cur[u].z, cur[u].w);
-        if constexpr ((amode & 128) != 0) {
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) miss += h[u];
-        } else if constexpr (!kMid && (amode & 64) != 0) {
-            // first-set lookups only, each miss its own slow path (sparse tables)
-            uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                base[u] = set_base<AL::kShortSets>(h[u]);
-                short_set_masks(A, base[u], ((uint64_t)cur[u].y << 32) | cur[u].x, m[u], z[u]);
-            }
-            bool slow[kAggUnroll];
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
-                const bool hit = valid && m[u] != 0;
-                slow[u] = valid && m[u] == 0;
-                const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)AL::kShortSets * 4 + lane;
-                __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                if (slow[u]) {
-                    const uint64_t k = ((uint64_t)cur[u].y << 32) | cur[u].x;
-                    if (!short_insert_slow(A, k, h[u], 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
-                }
-            }
-        } else if constexpr (!kMid) {
-            // Both sets of a key are looked up before anything diverges: a key
-            // sits in its second set only if its first was full when it was
-            // claimed (ways are never freed), so a first set with a free way and
-            // without the key settles it as new.  Only new keys (and lost claims)
-            // take the slow path, all of a lane's in one loop, so a wave runs it
-            // about once per block instead of once per record slot.
-            // mz[u]: first-set hit ways (bits 0-3), free ways (4-7), second-set hit ways (8-11)
-            uint32_t mz[kAggUnroll];
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                uint32_t m, z;
-                short_set_masks(A, set_base<AL::kShortSets>(h[u]), ((uint64_t)cur[u].y << 32) | cur[u].x, m, z);
-                mz[u] = m | z << 4;
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                if ((cur[u].x | cur[u].y) != 0 && mz[u] == 0) {
-                    uint32_t m2, z2;
-                    short_set_masks(A, set_base<AL::kShortSets>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
-                                    m2, z2);
-                    mz[u] = m2 << 8;
-                }
-            }
-            uint32_t slow = 0;
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
-                const uint32_t m = mz[u] & 15u, m2 = (mz[u] >> 8) & 15u;
-                const uint32_t ci = !valid   ? (uint32_t)AL::kShortSets * 4 + lane
-                                    : m != 0  ? set_base<AL::kShortSets>(h[u]) + __builtin_ctz(m)
-                                    : m2 != 0 ? set_base<AL::kShortSets>(second_hash(h[u])) + __builtin_ctz(m2)
-                                              : (uint32_t)AL::kShortSets * 4 + lane;
-                if (valid && (m | m2) == 0) slow |= 1u << u;
-                __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            while (slow) {  // this lane's new keys, one per trip (register arrays read by selects, not indexing)
-                const uint32_t us = __builtin_ctz(slow);
-                slow &= slow - 1;
-                uint64_t k = 0;
-                uint32_t hk = 0;
-#pragma unroll
-                for (uint32_t u = 0; u < kAggUnroll; u++)
-                    if (us == u) {
-                        k = ((uint64_t)cur[u].y << 32) | cur[u].x;
-                        hk = h[u];
-                    }
-                if (!short_insert_slow(A, k, hk, 1)) defer_miss(A, t, k, 0, keep_miss, wv, miss);
-            }
-        } else if constexpr ((amode & 64) != 0) {
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                if ((cur[u].x | cur[u].y) != 0) {
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    uint32_t m, z, pend;
                     const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
-                    if (!mid_insert(A, k0, k1, h[u], 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
+                    mid_set_masks(A, set_base<AL::kMidSets>(h[u]), k0, k1, m, z, pend);
+                    mm[u] = m;
+                    if ((cur[u].x | cur[u].y) != 0 && m == 0 && (z | pend) != 0) slow |= 1u << u;  // new key / pending
                 }
-            }
-        } else {
-            // mid keys: the same two-set lookup first (a way pending publication
-            // sends the record to the slow path, which retries or defers it)
-            uint32_t mm[kAggUnroll], slow = 0;  // mm[u]: first-set hit ways (bits 0-3), second-set (4-7)
 #pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                uint32_t m, z, pend;
-                const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
-                mid_set_masks(A, set_base<AL::kMidSets>(h[u]), k0, k1, m, z, pend);
-                mm[u] = m;
-                if ((cur[u].x | cur[u].y) != 0 && m == 0 && (z | pend) != 0) slow |= 1u << u;  // new key / pending
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                if ((cur[u].x | cur[u].y) != 0 && mm[u] == 0 && !((slow >> u) & 1u)) {
-                    uint32_t m2, z2, p2;
-                    const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
-                    mid_set_masks(A, set_base<AL::kMidSets>(second_hash(h[u])), k0, k1, m2, z2, p2);
-                    mm[u] = m2 << 4;
-                    if (m2 == 0) slow |= 1u << u;
-                }
-            }
-#pragma unroll
-            for (uint32_t u = 0; u < kAggUnroll; u++) {
-                const bool valid = (cur[u].x | cur[u].y) != 0;
-                const uint32_t m = mm[u] & 15u, m2 = mm[u] >> 4;
-                const uint32_t ci = !valid   ? (uint32_t)AL::kMidSets * 4 + lane
-                                    : m != 0  ? set_base<AL::kMidSets>(h[u]) + __builtin_ctz(m)
-                                    : m2 != 0 ? set_base<AL::kMidSets>(second_hash(h[u])) + __builtin_ctz(m2)
-                                              : (uint32_t)AL::kMidSets * 4 + lane;
-                __hip_atomic_fetch_add(&A.mc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
-            while (slow) {
-                const uint32_t us = __builtin_ctz(slow);
-                slow &= slow - 1;
-                uint64_t k0 = 0, k1 = 0;
-                uint32_t hk = 0;
-#pragma unroll
-                for (uint32_t u = 0; u < kAggUnroll; u++)
-                    if (us == u) {
-                        k0 = ((uint64_t)cur[u].y << 32) | cur[u].x;
-                        k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
-                        hk = h[u];
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    if ((cur[u].x | cur[u].y) != 0 && mm[u] == 0 && !((slow >> u) & 1u)) {
+                        uint32_t m2, z2, p2;
+                        const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                        mid_set_masks(A, set_base<AL::kMidSets>(second_hash(h[u])), k0, k1, m2, z2, p2);
+                        mm[u] = m2 << 4;
+                        if (m2 == 0) slow |= 1u << u;
                     }
-                if (!mid_insert(A, k0, k1, hk, 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
-            }
-        }
+                }
 #pragma unroll
-        for (uint32_t u = 0; u < kAggUnroll; u++) cur[u] = nxt[u];
-        j = j2;
-        off = off2;
-        cnt = cnt2;
+                for (uint32_t u = 0; u < kAggUnroll; u++) {
+                    const bool valid = (cur[u].x | cur[u].y) != 0;
+                    const uint32_t m = mm[u] & 15u, m2 = mm[u] >> 4;
+                    const uint32_t ci = !valid   ? (uint32_t)AL::kMidSets * 4 + lane
+                                        : m != 0  ? set_base<AL::kMidSets>(h[u]) + __builtin_ctz(m)
+                                        : m2 != 0 ? set_base<AL::kMidSets>(second_hash(h[u])) + __builtin_ctz(m2)
+                                                  : (uint32_t)AL::kMidSets * 4 + lane;
+                    __hip_atomic_fetch_add(&A.mc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+                while (slow) {
+                    const uint32_t us = __builtin_ctz(slow);
+                    slow &= slow - 1;
+                    uint64_t k0 = 0, k1 = 0;
+                    uint32_t hk = 0;
+#pragma unroll
+                    for (uint32_t u = 0; u < kAggUnroll; u++)
+                        if (us == u) {
+                            k0 = ((uint64_t)cur[u].y << 32) | cur[u].x;
+                            k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
+                            hk = h[u];
+                        }
+                    if (!mid_insert(A, k0, k1, hk, 1)) defer_miss(A, t, k0, k1, keep_miss, wv, miss);
+                }
+            }
+#pragma unroll
+            for (uint32_t u = 0; u < kAggUnroll; u++) cur[u] = nxt[u];
+            j = j2;
+            off = off2;
+            cnt = cnt2;
+        }
     }
 }
 
 // amode (compile-time): 0 = two-set lookups, 64 = first-set lookups (both
-// exact; launch_wc_agg picks by layout); 128 = benchmark ablation, read + hash
-// the records only (wrong results).  emit: see launch_wc_agg.
+// exact; launch_wc_agg picks by layout); 256 = the wave's streams read as one
+// virtual sequence (the dictionary sample); 128 = benchmark ablation, read +
+// hash the records only (wrong results).  emit: see launch_wc_agg.
 template <uint32_t amode, class AL>
 __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int emit) {
     __shared__ AL A;
@@ -966,15 +1200,15 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
     uint64_t miss = 0, carried = 0;
     if (!later) {
         // round 0: bucket b's stream of map workgroup g is pool[(g * nb + b) * sub]
-        agg_pool<amode, false, 8>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg,
+        agg_pool<amode, false, 8, true>(A, t, t.sp.pool8 + b * t.sp.sub8, t.sp.counts8 + b * t.sp.nwg,
                                   (uint64_t)t.sp.nb * t.sp.sub8, t.sp.nwg, nullptr, keep_miss, miss);
-        agg_pool<amode, true, 4>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
+        agg_pool<amode, true, 4, true>(A, t, t.sp.pool + b * t.sp.sub_keys, t.sp.counts + b * t.sp.nwg,
                                  (uint64_t)t.sp.nb * t.sp.sub_keys, t.sp.nwg, nullptr, keep_miss, miss);
     } else {
         // later rounds: wave w re-reads its own segment of the previous round's misses
-        agg_pool<amode, false, 8>(A, t, t.sp.seg8_in, t.sp.seg_n_in + b * kAggSegs, 0, kAggWaves,
+        agg_pool<amode, false, 8, false>(A, t, t.sp.seg8_in, t.sp.seg_n_in + b * kAggSegs, 0, kAggWaves,
                                   t.sp.seg_off8 + b * kAggSegs, keep_miss, miss);
-        agg_pool<amode, true, 4>(A, t, t.sp.seg16_in, t.sp.seg_n_in + E + b * kAggSegs, 0, kAggWaves,
+        agg_pool<amode, true, 4, false>(A, t, t.sp.seg16_in, t.sp.seg_n_in + E + b * kAggSegs, 0, kAggWaves,
                                  t.sp.seg_off16 + b * kAggSegs, keep_miss, miss);
     }
     __syncthreads();
@@ -1293,6 +1527,7 @@ void launch_wc_agg(const Tables& t, int mode, int emit, bool big, hipStream_t s)
         else wc_agg_kernel<64, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
     } else {
         if (mode & 128) wc_agg_kernel<128, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
+        else if (emit == 2) wc_agg_kernel<64 | 256, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
         else if (two_set) wc_agg_kernel<0, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
         else wc_agg_kernel<64, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
     }

@@ -187,6 +187,7 @@ def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1):
     ctx.set_option("grep_sort_k1", grep_k1)
     try:
         check(ctx, "wc", files, nreduces=(1, 10, 64))
+        check(ctx, "wc", [words, words[::-1]], nreduces=(1, 10, 300))  # ASCII only: the packed sort key
         check(ctx, "grep:distributed", cases.synthetic_grep(20000, [1_500_000], 42), nreduces=(1, 10))
     finally:
         ctx.set_option("sort_digit_bits", 0)
