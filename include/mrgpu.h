@@ -163,7 +163,20 @@ int mrg_memcpy_d2h(mrg_ctx* ctx, void* dst, const void* src, size_t n);
 int mrg_sync(mrg_ctx* ctx);
 int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
 
-/* Tuning knobs (0 = default); for benchmarks and tests of the overflow paths. */
+/* Tuning knobs (0 = default); for benchmarks and tests of the overflow paths.
+ * Results never depend on them (every path is exact); unknown names -> MRG_EINVAL.
+ *   short_table_log2, long_table_log2, list_cap, rec_cap   HBM table / buffer sizes
+ *   map_grid, map_mode                   map workgroups; ablation modes (benchmarks)
+ *   spill_stream_keys                    force tiny spill streams (overflow tests)
+ *   spill_buckets (0, 512, 2048)         spill buckets; 0 = chosen per split from the
+ *                                        previous split's aggregated keys
+ *   spill_hi_keys                        aggregated keys above which 2048 are chosen
+ *   agg_rounds, agg_carry_min, agg_big0, agg_big_later   bucket aggregation rounds
+ *   dict (-1: off), dict_warm (-1: off), dict_min_bytes, dict_sample_bytes
+ *   ingest_piece, ingest_min             host input streamed in pieces of this size
+ *   skip_exchange                        mrg_run_job: no shuffle (per-rank timing)
+ *   sort_digit_bits (8, 10), sort_fold_part (-1: off), grep_sort_k1 (-1: 8-byte
+ *                                        prefix passes only)   reduce sort variants */
 int mrg_set_option(mrg_ctx* ctx, const char* name, int64_t value);
 
 uint32_t mrg_ihash(const uint8_t* key, size_t n);
