@@ -242,6 +242,11 @@ def main():
         log(f"--gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if world > 1:
         dist.init_process_group("gloo")  # control plane only; the shuffle is RCCL inside libmrgpu
+    # one GPU per rank; ranks beyond the visible devices share them (a rehearsal of
+    # the N > 1 path on a smaller box — the driver's N-GPU runs have one each)
+    ndev = max(1, torch.cuda.device_count())
+    shared = world > ndev  # rehearsal: RCCL refuses two ranks on one device, so no exchange
+    local = local % ndev
     torch.cuda.set_device(local)
     # torch initializes its CUDA runtime lazily on first use; do it now, so it can
     # never overlap a timed step (seen: one 57 ms map kernel in the first step)
@@ -257,10 +262,13 @@ def main():
     for o in args.opt:
         k, v = o.split("=")
         ctx.set_option(k, int(v))
-    if world > 1:
+    if world > 1 and not shared:
         obj = [Context.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         ctx.comm_init(obj[0], world, rank)
+    if shared:
+        log(f"{world} ranks on {ndev} device(s): rehearsal without the RCCL exchange")
+        ctx.set_option("skip_exchange", 1)
     # the split, resident in HBM before the timed region (a torch tensor: the
     # independent word count below reads it with plain torch ops)
     dev = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{local}")
@@ -347,7 +355,7 @@ def main():
         ctx.sync()
         t1 = time.perf_counter() - t1
         dist.barrier()
-        ctx.set_option("skip_exchange", 0)
+        ctx.set_option("skip_exchange", 1 if shared else 0)
         v = torch.tensor([ex_ms, snd, t1], dtype=torch.float64)
         vmax = v.clone()
         dist.all_reduce(vmax, op=dist.ReduceOp.MAX)
@@ -361,6 +369,8 @@ def main():
                  "note": "shuffle bytes = wire bytes a rank sends to the other ranks (max over ranks of the mean over timed "
                          "steps); xgmi_frac = those bytes / exchange time / (min(P-1,7) x 153 GB/s); "
                          "E(P) = T(1) / T(P), T(1) = the same per-GPU splits run with no shuffle in this process"}
+        if shared:
+            multi["rehearsal"] = f"{world} ranks shared {ndev} device(s): no RCCL exchange ran (not a measurement)"
 
     total_bytes = nbytes * world * args.steps
     value = total_bytes / t_max / 1e9
