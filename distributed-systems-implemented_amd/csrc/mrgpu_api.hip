@@ -169,6 +169,12 @@ struct mrg_ctx {
     int dict_mode = 0;                 // <0: never build the hot-key dictionary
     bool dict_warm = true;             // level-1 dictionary = the previous map task's (see build_dict)
     bool dict_valid = false;           // c->dict holds a dictionary built by an earlier call
+    // Dictionary reuse: the previous split's dictionary is kept (no rebuild) when
+    // it hits this split's sample at >= dict_keep x the fraction it hit on the
+    // split it was built for (dict_frac_built, measured on that split's map).
+    double dict_keep = 0.97;
+    double dict_frac_built = 0;
+    bool dict_fresh = false;           // the current split built its own dictionary
     uint64_t dict_min_bytes = 32ull << 20;
     uint64_t dict_sample_bytes = 16ull << 20;  // C2: 16 vs 64 MB loses 0.13% of dictionary hits, halves the build
     uint64_t spill_sub_keys = 0, spill_sub8 = 0;
@@ -493,7 +499,8 @@ static void print_stamps(mrg_ctx* c, const char* what, uint32_t nblocks, uint32_
 // become the records the final dictionary is built from.  Only speed depends
 // on the dictionary: every key it misses is counted exactly through the spill.
 static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win, uint32_t nwin, LetterTables lt,
-                       bool with_dict, uint64_t* nrec_out, double* spill_rate = nullptr, const uint8_t* host = nullptr) {
+                       bool with_dict, uint64_t* nrec_out, double* spill_rate = nullptr, const uint8_t* host = nullptr,
+                       double* hit_frac = nullptr) {
     const uint64_t stride = ((len - win) / nwin) & ~15ull;
     const uint64_t sn = (uint64_t)nwin * (win + 16);
     HCHK(c, c->sample.ensure(sn + 64));
@@ -530,6 +537,10 @@ static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win
     if ((rc = read_counters(c))) return rc;
     *nrec_out = std::min<uint64_t>(c->h_ctr->nrec, c->rec_cap);
     if (spill_rate) *spill_rate = (double)(c->h_ctr->spilled + c->h_ctr->spill_ovf) / (double)sn;
+    if (hit_frac) {
+        const double words = (double)(c->h_ctr->dict_hits + c->h_ctr->spilled + c->h_ctr->spill_ovf);
+        *hit_frac = words > 0 ? (double)c->h_ctr->dict_hits / words : 0.0;
+    }
     return MRG_OK;
 }
 
@@ -575,12 +586,17 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
         if (nrec == 0) return MRG_OK;
         if ((rc = dict_from_recs(c, nrec))) return rc;
     }
+    c->dict_fresh = true;
     if (target > small) {
-        double rate = 0;
+        double rate = 0, frac = 0;
         if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, target / win), lt, true, &nrec, &rate,
-                              host)))
+                              host, &frac)))
             return rc;
-        if (nrec && (rc = dict_from_recs(c, nrec))) return rc;
+        // a warm dictionary that still hits this split's sample about as well as it
+        // hit its own split is kept: the candidate sort and placement are skipped
+        const bool keep = warm && c->dict_keep > 0 && c->dict_frac_built > 0 && frac >= c->dict_keep * c->dict_frac_built;
+        c->dict_fresh = !keep;
+        if (!keep && nrec && (rc = dict_from_recs(c, nrec))) return rc;
         // Spill streams hold 0.094 8-byte records per input byte at scale 1 (C2
         // spills 0.04).  A split whose sample misses its (first-level) dictionary
         // more often gets proportionally longer streams, 30 % over the estimate
@@ -842,6 +858,10 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         c->stats.agg_rounds = (uint64_t)__builtin_popcountll(h.round_mask);
         c->stats.spill_buckets = c->spill_nb;
         c->stats.dict_hits = h.dict_hits;
+        if (have_dict && c->dict_fresh) {  // what this split's own dictionary hit (dictionary reuse, build_dict)
+            const double words = (double)(h.dict_hits + h.spilled + h.spill_ovf);
+            c->dict_frac_built = words > 0 ? (double)h.dict_hits / words : 0.0;
+        }
         c->stats.distinct_keys = h.nrec;
         c->stats.long_keys = h.nlong_rec;
         *out = p;
@@ -1054,6 +1074,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "agg_carry_min")) c->agg_carry_min = v > 0 ? (uint32_t)v : v < 0 ? 0u : 64u;  // -1: always carry
     else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
     else if (!strcmp(name, "dict_warm")) c->dict_warm = v >= 0;  // -1: always build the level-1 dictionary
+    else if (!strcmp(name, "dict_keep")) c->dict_keep = v > 0 ? (double)v / 1000.0 : v < 0 ? 0.0 : 0.97;  // permille; -1: never
     else if (!strcmp(name, "spill_buckets")) {  // 0: chosen per split (feedback), else 512 or 2048
         if (v != 0 && v != kSpillBuckets && v != kSpillBucketsHi) return fail(c, MRG_EINVAL, "spill_buckets: 0, 512 or 2048");
         c->spill_buckets_opt = (int)v;

@@ -172,7 +172,8 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        previous split's aggregated keys
  *   spill_hi_keys                        aggregated keys above which 2048 are chosen
  *   agg_rounds, agg_carry_min, agg_big0, agg_big_later   bucket aggregation rounds
- *   dict (-1: off), dict_warm (-1: off), dict_min_bytes, dict_sample_bytes
+ *   dict (-1: off), dict_warm (-1: off), dict_keep (permille; -1: always rebuild),
+ *                                        dict_min_bytes, dict_sample_bytes
  *   ingest_piece, ingest_min             host input streamed in pieces of this size
  *   skip_exchange                        mrg_run_job: no shuffle (per-rank timing)
  *   sort_digit_bits (8, 10), sort_fold_part (-1: off), grep_sort_k1 (-1: 8-byte
