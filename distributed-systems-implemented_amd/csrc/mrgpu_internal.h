@@ -215,6 +215,8 @@ void reduce_ws_free(ReduceWs*);
 // fold the partition into the first key pass (1 / 0; -1 keeps it), grep radix
 // passes over 16 key bytes (1) or 8 (0; -1 keeps it).
 void reduce_ws_set(ReduceWs*, int digit_bits, int fold_part, int grep_k1);
+// Tied runs merge-sorted on compact key copies (default) or on the records.
+void reduce_ws_set_compact_ties(ReduceWs*, bool on);
 // Sort recs (optionally only partition `only_part`), format "key value\n" lines.
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
 // ascii_keys: every key byte is < 0x80 (the sort key then packs 7 bits per byte).

@@ -45,17 +45,21 @@ struct DBuf {
 };
 
 struct ReduceWs {
-    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext;
+    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext, tiek;
     uint64_t* h_pinned = nullptr;  // small pinned staging
     int digit_bits = 0;            // radix digit of the 64-bit key passes: 8, 10, 0 = by app (grep 10, wc 8)
     bool fold_part = true;         // wc: partition folded into the top bits of the k0 sort key
     bool grep_k1 = true;           // grep: radix passes over the first 16 key bytes (else 8, more ties)
+    bool compact_ties = true;      // tied runs merge-sorted on compact key copies (TieKey)
 };
 
 void reduce_ws_set(ReduceWs* w, int digit_bits, int fold_part, int grep_k1) {
     if (digit_bits == 0 || digit_bits == 8 || digit_bits == 10) w->digit_bits = digit_bits;
     if (fold_part >= 0) w->fold_part = fold_part != 0;
     if (grep_k1 >= 0) w->grep_k1 = grep_k1 != 0;
+}
+
+void reduce_ws_set_compact_ties(ReduceWs* w, bool on) { w->compact_ties = on;
 }
 
 ReduceWs* reduce_ws_new() {
@@ -66,7 +70,7 @@ ReduceWs* reduce_ws_new() {
 
 void reduce_ws_free(ReduceWs* w) {
     if (!w) return;
-    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext};
+    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek};
     for (DBuf* b : bs) b->release();
     if (w->h_pinned) hipHostFree(w->h_pinned);
     delete w;
@@ -283,6 +287,63 @@ struct FullLess {
         return (ext ? rec_cmp_ext(r, ext, a, b) : rec_cmp(r, a, b)) < 0;
     }
 };
+
+// The merge sort of tied records compares copies of their keys laid out
+// contiguously in sort-input order (80 bytes each: the first 64 key bytes as
+// big-endian words, partition, length, record index), not the records' scattered
+// fields: a comparison touches one or two cache lines per key instead of four.
+struct alignas(16) TieKey {
+    uint64_t w[2 + kExtWords];
+    uint32_t part, len, rec, pad;
+};
+
+__global__ void tie_keys_kernel(Recs r, const uint64_t* ext, const uint32_t* va, const uint32_t* d_m, TieKey* K,
+                                uint32_t* ia) {
+    const uint32_t m = *d_m;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) {
+        const uint32_t j = va[i];
+        TieKey k;
+        k.w[0] = __builtin_bswap64(r.k0[j]);
+        k.w[1] = __builtin_bswap64(r.k1[j]);
+#pragma unroll
+        for (int w = 0; w < kExtWords; w++) k.w[2 + w] = ext[(uint64_t)kExtWords * j + w];
+        k.part = r.part[j];
+        k.len = r.len[j];
+        k.rec = j;
+        k.pad = 0;
+        K[i] = k;
+        ia[i] = i;
+    }
+}
+
+struct CompactLess {
+    const TieKey* K;
+    Recs r;
+    __device__ bool operator()(const uint32_t& a, const uint32_t& b) const {
+        const TieKey& A = K[a];
+        const TieKey& B = K[b];
+        if (A.part != B.part) return A.part < B.part;
+#pragma unroll
+        for (int w = 0; w < 2 + kExtWords; w++)
+            if (A.w[w] != B.w[w]) return A.w[w] < B.w[w];
+        constexpr uint32_t kCovered = 16 + 8 * kExtWords;
+        if (A.len > kCovered && B.len > kCovered) {  // equal first 64 bytes: the rest from the arena
+            const uint8_t* pa = r.arena + r.koff[A.rec];
+            const uint8_t* pb = r.arena + r.koff[B.rec];
+            const uint32_t mx = A.len > B.len ? A.len : B.len;
+            for (uint32_t pos = kCovered; pos < mx; pos += 8) {
+                const uint64_t wa = key_word_be(pa, pos, A.len), wb = key_word_be(pb, pos, B.len);
+                if (wa != wb) return wa < wb;
+            }
+        }
+        return A.len < B.len;
+    }
+};
+
+__global__ void untie_perm_kernel(const uint32_t* va, const uint32_t* ib, const uint32_t* d_m, uint32_t* vb) {
+    const uint32_t m = *d_m;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < m; i += gridDim.x * blockDim.x) vb[i] = va[ib[i]];
+}
 
 __global__ void gather_perm_kernel(const uint32_t* perm, const uint32_t* pos, const uint32_t* d_m, uint32_t* v) {
     const uint32_t m = *d_m;
@@ -556,9 +617,21 @@ static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
     const unsigned g = (unsigned)((m + 255) / 256 < 4096 ? (m + 255) / 256 : 4096);
     gather_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, va);
     tb = 0;
-    RCHK(rocprim::merge_sort(nullptr, tb, va, vb, (size_t)m, FullLess{r, ext}, s));
-    RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::merge_sort(ws->tmp.p, tb, va, vb, (size_t)m, FullLess{r, ext}, s));
+    if (ext && ws->compact_ties) {
+        RCHK(ws->tiek.ensure((size_t)m * (sizeof(TieKey) + 8) + 64));
+        TieKey* K = ws->tiek.as<TieKey>();
+        uint32_t* ia = (uint32_t*)(K + m);
+        uint32_t* ib = ia + m;
+        tie_keys_kernel<<<g, 256, 0, s>>>(r, ext, va, d_m, K, ia);
+        RCHK(rocprim::merge_sort(nullptr, tb, ia, ib, (size_t)m, CompactLess{K, r}, s));
+        RCHK(ws->tmp.ensure(tb));
+        RCHK(rocprim::merge_sort(ws->tmp.p, tb, ia, ib, (size_t)m, CompactLess{K, r}, s));
+        untie_perm_kernel<<<g, 256, 0, s>>>(va, ib, d_m, vb);
+    } else {
+        RCHK(rocprim::merge_sort(nullptr, tb, va, vb, (size_t)m, FullLess{r, ext}, s));
+        RCHK(ws->tmp.ensure(tb));
+        RCHK(rocprim::merge_sort(ws->tmp.p, tb, va, vb, (size_t)m, FullLess{r, ext}, s));
+    }
     scatter_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, vb);
     return 0;
 }

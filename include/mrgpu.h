@@ -177,7 +177,8 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *   ingest_piece, ingest_min             host input streamed in pieces of this size
  *   skip_exchange                        mrg_run_job: no shuffle (per-rank timing)
  *   sort_digit_bits (8, 10), sort_fold_part (-1: off), grep_sort_k1 (-1: 8-byte
- *                                        prefix passes only)   reduce sort variants */
+ *                                        prefix passes only), sort_compact_ties (-1:
+ *                                        off)   reduce sort variants */
 int mrg_set_option(mrg_ctx* ctx, const char* name, int64_t value);
 
 uint32_t mrg_ihash(const uint8_t* key, size_t n);

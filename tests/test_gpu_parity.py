@@ -171,11 +171,13 @@ def test_wc_high_cardinality_buckets(ctx, rounds):
         ctx.set_option("spill_hi_keys", 0)
 
 
-@pytest.mark.parametrize("digit_bits,fold,grep_k1", [(8, 0, 0), (8, -1, 0), (10, 0, 0), (10, -1, -1), (8, 0, -1)])
-def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1):
+@pytest.mark.parametrize("digit_bits,fold,grep_k1,compact",
+                         [(8, 0, 0, 0), (8, -1, 0, -1), (10, 0, 0, 0), (10, -1, -1, -1), (8, 0, -1, 0)])
+def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact):
     """The reduce's sort variants give the same bytes: 8- or 10-bit radix digits,
     the partition folded into the first key pass (default) or sorted on its own,
-    grep lines radix-sorted on 16 key bytes (default) or 8 (more tied runs).
+    grep lines radix-sorted on 16 key bytes (default) or 8 (more tied runs), tied
+    runs merge-sorted on compact key copies (default) or on the records.
     The corpus has 8-byte keys differing only in their last byte's low bits (ties
     of the folded key), 9-16-byte keys sharing 8-byte prefixes, long keys and UTF-8."""
     base = [b"abcdefg" + bytes([c]) for c in range(ord("a"), ord("z") + 1)]
@@ -185,6 +187,7 @@ def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1):
     ctx.set_option("sort_digit_bits", digit_bits)
     ctx.set_option("sort_fold_part", fold)
     ctx.set_option("grep_sort_k1", grep_k1)
+    ctx.set_option("sort_compact_ties", compact)
     try:
         check(ctx, "wc", files, nreduces=(1, 10, 64))
         check(ctx, "wc", [words, words[::-1]], nreduces=(1, 10, 300))  # ASCII only: the packed sort key
@@ -193,6 +196,7 @@ def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1):
         ctx.set_option("sort_digit_bits", 0)
         ctx.set_option("sort_fold_part", 0)
         ctx.set_option("grep_sort_k1", 0)
+        ctx.set_option("sort_compact_ties", 0)
 
 
 def test_wc_large_vs_oracle(wctx):
