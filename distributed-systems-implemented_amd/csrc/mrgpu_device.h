@@ -279,20 +279,35 @@ __device__ __forceinline__ void load16u(const uint8_t* p, uint64_t avail, uint64
     }
 }
 
-// len bytes at a == len bytes at b, 16 bytes per step (long keys, grep lines:
-// a chain of byte loads would cost a memory round trip per byte).
+// len bytes at a == len bytes at b, 64 bytes per step: four independent
+// 16-byte pieces per side in flight at once (long keys, grep lines: a chain of
+// byte loads, or of one 16-byte load per step, costs a memory round trip each).
 __device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint64_t len) {
-    for (uint64_t k = 0; k < len; k += 16) {
-        const uint64_t left = len - k;
-        uint64_t a0, a1, b0, b1;
-        load16u(a + k, left, a0, a1);
-        load16u(b + k, left, b0, b1);
-        if (left < 16) {
-            const uint64_t m0 = left >= 8 ? ~0ull : (1ull << (8 * left)) - 1;
-            const uint64_t m1 = left <= 8 ? 0ull : (1ull << (8 * (left - 8))) - 1;
-            a0 &= m0; b0 &= m0; a1 &= m1; b1 &= m1;
+    for (uint64_t k0 = 0; k0 < len; k0 += 64) {
+        uint64_t a0[4], a1[4], b0[4], b1[4];
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint64_t k = k0 + 16 * i;
+            a0[i] = a1[i] = b0[i] = b1[i] = 0;
+            if (k < len) {
+                load16u(a + k, len - k, a0[i], a1[i]);
+                load16u(b + k, len - k, b0[i], b1[i]);
+            }
         }
-        if (a0 != b0 || a1 != b1) return false;
+        bool eq = true;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const uint64_t k = k0 + 16 * i;
+            if (k >= len) break;
+            const uint64_t left = len - k;
+            uint64_t m0 = ~0ull, m1 = ~0ull;
+            if (left < 16) {
+                m0 = left >= 8 ? ~0ull : (1ull << (8 * left)) - 1;
+                m1 = left <= 8 ? 0ull : (1ull << (8 * (left - 8))) - 1;
+            }
+            eq &= ((a0[i] ^ b0[i]) & m0) == 0 && ((a1[i] ^ b1[i]) & m1) == 0;
+        }
+        if (!eq) return false;
     }
     return true;
 }

@@ -233,6 +233,11 @@ __device__ __forceinline__ uint4 block16(const uint8_t* in, int64_t q, int64_t& 
     bi = q - (int64_t)(a - ab);
     return *(const uint4*)ab;
 }
+// Offset (relative to in) of the 16-byte-aligned block holding byte q.
+__device__ __forceinline__ int64_t block_start(const uint8_t* in, int64_t q) {
+    const uintptr_t a = (uintptr_t)(in + q);
+    return q - (int64_t)(a - (a & ~(uintptr_t)15));
+}
 
 // long_insert (mrgpu_device.h) without its fill counters: returns whether this
 // lane claimed a new slot, and the caller counts claims once per wave.
@@ -429,14 +434,25 @@ __global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* _
 // (equal lines hash equally, and slot matches are confirmed bytewise anyway).
 constexpr uint64_t kHashAll = 8192, kHashEdge = 2048;
 __device__ uint64_t hash_bytes(const uint8_t* in, int64_t s, int64_t e, uint64_t h) {
+    // 64 bytes per step: the four aligned 16-byte loads are issued together (one
+    // memory round trip per step, not per 16 bytes: long lines dominated the
+    // kernel); only blocks holding bytes before e are read
     for (int64_t q = s; q < e;) {
-        int64_t bi;
-        const uint4 v = block16(in, q, bi);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+        const int64_t bi = block_start(in, q);
+        const uint8_t* ab = in + bi;
+        uint4 v[4];
 #pragma unroll
-        for (int j = 0; j < 16; j++)
-            if (bi + j >= q && bi + j < e) h = fnv1a64_step(h, (w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
-        q = bi + 16;
+        for (int k = 0; k < 4; k++) v[k] = bi + 16 * k < e ? *(const uint4*)(ab + 16 * k) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const int64_t p = bi + 16 * k + j;
+                if (p >= q && p < e) h = fnv1a64_step(h, (w[j >> 2] >> (8 * (j & 3))) & 0xFFu);
+            }
+        }
+        q = bi + 64;
     }
     return h;
 }
@@ -514,20 +530,27 @@ __device__ __forceinline__ bool emit_long_rec(const Tables& t, const LongSlot& s
     if (o >= t.out_cap || off + len > t.out.arena_n) { set_status(t.ctr, kStRecFull); return false; }
     uint32_t h = 2166136261u;
     uint64_t k0 = 0, k1 = 0;
-    for (int64_t q = 0; q < (int64_t)len;) {
-        int64_t bi;
-        const uint4 v = block16(s.rep, q, bi);
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+    for (int64_t q = 0; q < (int64_t)len;) {  // 64 bytes (four loads in flight) per step, as hash_bytes
+        const int64_t bi = block_start(s.rep, q);
+        const uint8_t* ab = s.rep + bi;
+        uint4 v[4];
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            const int64_t k = bi + j;
-            if (k < q || k >= (int64_t)len) continue;
-            const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-            h = fnv1a32_step(h, b);
-            if (k < 8) k0 |= (uint64_t)b << (8 * k);
-            else if (k < 16) k1 |= (uint64_t)b << (8 * (k - 8));
+        for (int k = 0; k < 4; k++)
+            v[k] = bi + 16 * k < (int64_t)len ? *(const uint4*)(ab + 16 * k) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const int64_t p = bi + 16 * k + j;
+                if (p < q || p >= (int64_t)len) continue;
+                const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                h = fnv1a32_step(h, b);
+                if (p < 8) k0 |= (uint64_t)b << (8 * p);
+                else if (p < 16) k1 |= (uint64_t)b << (8 * (p - 8));
+            }
         }
-        q = bi + 16;
+        q = bi + 64;
     }
     t.out.k0[o] = k0;
     t.out.k1[o] = k1;
