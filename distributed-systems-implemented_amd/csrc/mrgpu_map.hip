@@ -522,9 +522,9 @@ __global__ void nrec_add_kernel(Counters* ctr, const uint32_t* d_count) { ctr->n
 // One LongTable record: key bytes copied to the arena at `off` by aligned
 // 16-byte blocks (the representative sits at a random input offset: one load
 // per block, not a chain of byte loads), prefix words and partition from them.
-// Record o of a LongTable key (its bytes go to the arena at off, copied by the
-// caller): the first 16 bytes as k0/k1 and the partition from FNV-1a-32 of all
-// bytes (worker.go:76), read in aligned 16-byte blocks.  Returns false (and sets
+// Record o of a LongTable key, its bytes copied to the arena at off: the first
+// 16 bytes as k0/k1 and the partition from FNV-1a-32 of all bytes
+// (worker.go:76), read in aligned 16-byte blocks.  Returns false (and sets
 // kStRecFull) when the record or arena buffer is too small.
 __device__ __forceinline__ bool emit_long_rec(const Tables& t, const LongSlot& s, uint64_t o, uint64_t off, uint64_t len) {
     if (o >= t.out_cap || off + len > t.out.arena_n) { set_status(t.ctr, kStRecFull); return false; }
@@ -545,6 +545,7 @@ __device__ __forceinline__ bool emit_long_rec(const Tables& t, const LongSlot& s
                 const int64_t p = bi + 16 * k + j;
                 if (p < q || p >= (int64_t)len) continue;
                 const uint32_t b = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                t.out.arena[off + p] = (uint8_t)b;  // (stores do not wait)
                 h = fnv1a32_step(h, b);
                 if (p < 8) k0 |= (uint64_t)b << (8 * p);
                 else if (p < 16) k1 |= (uint64_t)b << (8 * (p - 8));
@@ -565,7 +566,9 @@ __device__ __forceinline__ bool emit_long_rec(const Tables& t, const LongSlot& s
 // reserves their records and arena bytes with ONE pair of cursor atomics
 // (same-address device atomics serialize at the memory side: one pair per 64
 // slots of a 1 M-slot table cost ~0.6 ms).
-constexpr int kCollectSlots = 8;
+// Latency-bound (each key's bytes sit at a random input offset): many waves with
+// few slots each beat few waves with many (8 slots per lane: C3 collect 0.4 ms).
+constexpr int kCollectSlots = 2;
 __global__ void __launch_bounds__(kLineWG) collect_long_kernel(Tables t) {
     __shared__ unsigned long long scratch[2 * kLineWaves + 2];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -620,31 +623,13 @@ __global__ void __launch_bounds__(kLineWG) collect_long_kernel(Tables t) {
         const uint64_t rbase = scratch[2 * kLineWaves] + scratch[wv], abase = scratch[2 * kLineWaves + 1] + scratch[kLineWaves + wv];
         __syncthreads();
         uint64_t o = rbase + ic - c, off = abase + ib - bytes;
-        uint64_t offk[kCollectSlots];
-        uint32_t ok = 0;  // bit k: slot k's record was written (its bytes still to copy)
 #pragma unroll
         for (int k = 0; k < kCollectSlots; k++) {
-            offk[k] = off;
             if (sl[k].len == 0) continue;
             const uint64_t len = sl[k].len - 1;
-            if (emit_long_rec(t, sl[k], o, off, len)) ok |= 1u << k;
+            emit_long_rec(t, sl[k], o, off, len);
             o++;
             off += len;
-        }
-        // key bytes to the arena, one key at a time by the whole wave (consecutive
-        // lanes on consecutive bytes: a wave-instruction stores one contiguous run
-        // instead of 64 scattered bytes)
-#pragma unroll
-        for (int k = 0; k < kCollectSlots; k++) {
-            uint64_t m = __ballot((ok >> k) & 1u);
-            while (m) {
-                const int l = __builtin_ctzll(m);
-                m &= m - 1;
-                const uint8_t* src = (const uint8_t*)__shfl((unsigned long long)(uintptr_t)sl[k].rep, l);
-                const uint64_t len = __shfl((unsigned long long)sl[k].len, l) - 1;
-                uint8_t* dst = t.out.arena + __shfl((unsigned long long)offk[k], l);
-                for (uint64_t b = lane; b < len; b += 64) dst[b] = src[b];
-            }
         }
     }
 }
