@@ -328,7 +328,8 @@ static int ensure_spill(mrg_ctx* c, uint64_t n) {
     uint64_t sub = (uint64_t)((double)((n - n / 4) / 16 / (nb * nwg)) * c->spill_scale) + 64;
     sub = (sub + 63) & ~63ull;
     uint64_t sub8 = 2 * sub;
-    if (c->spill_force_sub > 0) sub = sub8 = (uint64_t)c->spill_force_sub;  // test knob: tiny streams
+    // test knob: tiny streams (even: the aggregator reads 8-byte records in pairs)
+    if (c->spill_force_sub > 0) sub = sub8 = ((uint64_t)c->spill_force_sub + 1) & ~1ull;
     // a workgroup's streams are addressed by 32-bit byte offsets in the map kernel
     // ((b * sub + pos) * 16 < 2^32): 2^32 bytes of 16-byte and as many of 8-byte
     // streams per workgroup is a ~1 TB split at scale 1 with 512 workgroups

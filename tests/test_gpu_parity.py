@@ -92,16 +92,21 @@ def test_wc_lds_overflow_and_table_growth(ctx):
         ctx.set_option("short_table_log2", 0)
 
 
-def test_wc_spill_region_full(wctx):
+@pytest.mark.parametrize("nb", [0, 2048])
+def test_wc_spill_region_full(wctx, nb):
     """Tiny spill streams: they overflow and the rest of their keys take the HBM-table path
-    (those buckets then merge through the HBM table instead of emitting directly)."""
+    (those buckets then merge through the HBM table instead of emitting directly), in
+    the default and the high-cardinality (2048-bucket, 12-wave) layouts."""
     files = cases.synthetic(C.KIND_ASCII, 1_000_000, [6_000_000], 15)
-    wctx.set_option("spill_stream_keys", 8)
+    wctx.set_option("spill_stream_keys", 8 if nb == 0 else 2)  # (2048 buckets: ~0.5 records per stream)
+    wctx.set_option("spill_buckets", nb)
     try:
         check(wctx, "wc", files, nreduces=(10,))
         assert wctx.stats()["spill_ovf"] > 0
+        assert wctx.stats()["spill_buckets"] == (nb or 512)
     finally:
         wctx.set_option("spill_stream_keys", 0)
+        wctx.set_option("spill_buckets", 0)
 
 
 def test_wc_record_buffer_growth(wctx):
