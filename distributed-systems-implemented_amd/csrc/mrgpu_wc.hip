@@ -76,12 +76,16 @@ __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, ui
     s2 = off + (a ^ (((h >> 4) & m) | 1u));
 }
 
-// Spill bucket of a key: bits 11..19 of its hash (the bucket aggregator's table
-// indexes by the top bits, so a bucket's keys still spread over all its sets).
+// Spill bucket of a key: bits 11..19 (512 buckets) or 10..20 (2048) of its hash.
+// The bucket aggregator's tables index their first set by the top 11 bits
+// (21..31), so the bucket bits must stay below bit 21: a shared bit fixes one
+// set-index bit within a bucket and halves the first-choice sets (measured with
+// 2048 buckets taken from bits 11..21: 2.3 % of C5's records found both their
+// sets full and went to the next round).
 template <int NB>
 __device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
     static_assert(NB == 512 || NB == 2048, "bucket = 9 or 11 bits");
-    return (h >> 11) & (uint32_t)(NB - 1);
+    return NB == 512 ? (h >> 11) & 511u : (h >> 10) & 2047u;
 }
 
 // ------------------------------------------------------------ wc map kernel
@@ -547,6 +551,9 @@ static_assert(AggLds::kWaves == kAggSegs && AggLdsBig::kWaves == 2 * kAggSegs, "
 static_assert(2 * sizeof(AggLds) <= 160 * 1024, "two aggregator workgroups per CU");
 static_assert(sizeof(AggLdsBig) <= 160 * 1024, "one big aggregator workgroup per CU");
 
+// Claim attempts before a key is deferred to the next round (a lost race re-reads
+// and retries: the winner, often the same key, published its way with its CAS).
+constexpr int kClaimAttempts = 4;
 __device__ __forceinline__ uint32_t second_hash(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 16) * 0xC2B2AE3Du; }
 template <int NSETS>
 __device__ __forceinline__ uint32_t set_base(uint32_t h) { return __umulhi(h, NSETS) * 4; }
@@ -569,7 +576,7 @@ __device__ __forceinline__ void short_set_masks(const AL& A, uint32_t base, uint
 // made C5's aggregation 51 -> 79 ms, a code-generation effect; not done.)
 template <class AL>
 __device__ bool short_insert_slow(AL& A, uint64_t k, uint32_t h, uint32_t add) {
-    for (int attempt = 0; attempt < 2; attempt++) {
+    for (int attempt = 0; attempt < kClaimAttempts; attempt++) {
         bool raced = false;
         for (int c = 0; c < 2 && !raced; c++) {
             const uint32_t base = set_base<AL::kShortSets>(c == 0 ? h : second_hash(h));
@@ -611,7 +618,7 @@ __device__ __forceinline__ void mid_set_masks(const AL& A, uint32_t base, uint64
 
 template <class AL>
 __device__ bool mid_insert(AL& A, uint64_t k0, uint64_t k1, uint32_t h, uint32_t add) {
-    for (int attempt = 0; attempt < 2; attempt++) {
+    for (int attempt = 0; attempt < kClaimAttempts; attempt++) {
         bool raced = false;
         for (int c = 0; c < 2 && !raced; c++) {
             const uint32_t base = set_base<AL::kMidSets>(c == 0 ? h : second_hash(h));
@@ -840,7 +847,8 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     const bool hit = valid && m[u] != 0;
                     slow[u] = valid && m[u] == 0;
                     const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)AL::kShortSets * 4 + lane;
-                    __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
+                    else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
@@ -870,22 +878,30 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                         uint32_t m2, z2;
                         short_set_masks(A, set_base<AL::kShortSets>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
                                         m2, z2);
-                        mz[u] = m2 << 8;
+                        mz[u] = m2 << 8 | z2 << 12 | 1u << 16;  // bit 16: second set read
                     }
                 }
-                uint32_t slow = 0;
+                uint32_t slow = 0, full = 0;
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
                     const uint32_t m = mz[u] & 15u, m2 = (mz[u] >> 8) & 15u;
+                    // both sets read, full, without the key: final for this round (ways are
+                    // never freed), so the key is deferred without the claim path
+                    if (valid && (mz[u] >> 8) == (1u << 8)) full |= 1u << u;
                     const uint32_t ci = !valid   ? (uint32_t)AL::kShortSets * 4 + lane
                                         : m != 0  ? set_base<AL::kShortSets>(h[u]) + __builtin_ctz(m)
                                         : m2 != 0 ? set_base<AL::kShortSets>(second_hash(h[u])) + __builtin_ctz(m2)
                                                   : (uint32_t)AL::kShortSets * 4 + lane;
-                    if (valid && (m | m2) == 0) slow |= 1u << u;
-                    __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (valid && (m | m2) == 0 && !((full >> u) & 1u)) slow |= 1u << u;
+                    if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
+                    else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                while (slow) {  // this lane's new keys, one per trip (register arrays read by selects, not indexing)
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++)
+                    if ((full >> u) & 1u) defer_miss(A, t, ((uint64_t)cur[u].y << 32) | cur[u].x, 0, keep_miss, wv, miss);
+                if constexpr ((amode & 2048) != 0) slow = 0;  // ablation: no claims
+            while (slow) {  // this lane's new keys, one per trip (register arrays read by selects, not indexing)
                     const uint32_t us = __builtin_ctz(slow);
                     slow &= slow - 1;
                     uint64_t k = 0;
@@ -909,7 +925,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
             } else {
                 // mid keys: the same two-set lookup first (a way pending publication
                 // sends the record to the slow path, which retries or defers it)
-                uint32_t mm[kAggUnroll], slow = 0;  // mm[u]: first-set hit ways (bits 0-3), second-set (4-7)
+                uint32_t mm[kAggUnroll], slow = 0, full = 0;  // mm[u]: first-set hit ways (bits 0-3), second-set (4-7)
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     uint32_t m, z, pend;
@@ -925,7 +941,9 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                         const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
                         mid_set_masks(A, set_base<AL::kMidSets>(second_hash(h[u])), k0, k1, m2, z2, p2);
                         mm[u] = m2 << 4;
-                        if (m2 == 0) slow |= 1u << u;
+                        // both sets full without the key (none pending): deferred directly
+                        if (m2 == 0 && (z2 | p2) == 0) full |= 1u << u;
+                        else if (m2 == 0) slow |= 1u << u;
                     }
                 }
 #pragma unroll
@@ -938,6 +956,11 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                                                   : (uint32_t)AL::kMidSets * 4 + lane;
                     __hip_atomic_fetch_add(&A.mc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++)
+                    if ((full >> u) & 1u)
+                        defer_miss(A, t, ((uint64_t)cur[u].y << 32) | cur[u].x, ((uint64_t)cur[u].w << 32) | cur[u].z,
+                                   keep_miss, wv, miss);
                 while (slow) {
                     const uint32_t us = __builtin_ctz(slow);
                     slow &= slow - 1;
@@ -1042,7 +1065,8 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     const bool hit = valid && m[u] != 0;
                     slow[u] = valid && m[u] == 0;
                     const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)AL::kShortSets * 4 + lane;
-                    __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
+                    else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
@@ -1072,22 +1096,30 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                         uint32_t m2, z2;
                         short_set_masks(A, set_base<AL::kShortSets>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
                                         m2, z2);
-                        mz[u] = m2 << 8;
+                        mz[u] = m2 << 8 | z2 << 12 | 1u << 16;  // bit 16: second set read
                     }
                 }
-                uint32_t slow = 0;
+                uint32_t slow = 0, full = 0;
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
                     const uint32_t m = mz[u] & 15u, m2 = (mz[u] >> 8) & 15u;
+                    // both sets read, full, without the key: final for this round (ways are
+                    // never freed), so the key is deferred without the claim path
+                    if (valid && (mz[u] >> 8) == (1u << 8)) full |= 1u << u;
                     const uint32_t ci = !valid   ? (uint32_t)AL::kShortSets * 4 + lane
                                         : m != 0  ? set_base<AL::kShortSets>(h[u]) + __builtin_ctz(m)
                                         : m2 != 0 ? set_base<AL::kShortSets>(second_hash(h[u])) + __builtin_ctz(m2)
                                                   : (uint32_t)AL::kShortSets * 4 + lane;
-                    if (valid && (m | m2) == 0) slow |= 1u << u;
-                    __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (valid && (m | m2) == 0 && !((full >> u) & 1u)) slow |= 1u << u;
+                    if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
+                    else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
-                while (slow) {  // this lane's new keys, one per trip (register arrays read by selects, not indexing)
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++)
+                    if ((full >> u) & 1u) defer_miss(A, t, ((uint64_t)cur[u].y << 32) | cur[u].x, 0, keep_miss, wv, miss);
+                if constexpr ((amode & 2048) != 0) slow = 0;  // ablation: no claims
+            while (slow) {  // this lane's new keys, one per trip (register arrays read by selects, not indexing)
                     const uint32_t us = __builtin_ctz(slow);
                     slow &= slow - 1;
                     uint64_t k = 0;
@@ -1111,7 +1143,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
             } else {
                 // mid keys: the same two-set lookup first (a way pending publication
                 // sends the record to the slow path, which retries or defers it)
-                uint32_t mm[kAggUnroll], slow = 0;  // mm[u]: first-set hit ways (bits 0-3), second-set (4-7)
+                uint32_t mm[kAggUnroll], slow = 0, full = 0;  // mm[u]: first-set hit ways (bits 0-3), second-set (4-7)
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     uint32_t m, z, pend;
@@ -1127,7 +1159,9 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                         const uint64_t k0 = ((uint64_t)cur[u].y << 32) | cur[u].x, k1 = ((uint64_t)cur[u].w << 32) | cur[u].z;
                         mid_set_masks(A, set_base<AL::kMidSets>(second_hash(h[u])), k0, k1, m2, z2, p2);
                         mm[u] = m2 << 4;
-                        if (m2 == 0) slow |= 1u << u;
+                        // both sets full without the key (none pending): deferred directly
+                        if (m2 == 0 && (z2 | p2) == 0) full |= 1u << u;
+                        else if (m2 == 0) slow |= 1u << u;
                     }
                 }
 #pragma unroll
@@ -1140,6 +1174,11 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                                                   : (uint32_t)AL::kMidSets * 4 + lane;
                     __hip_atomic_fetch_add(&A.mc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+#pragma unroll
+                for (uint32_t u = 0; u < kAggUnroll; u++)
+                    if ((full >> u) & 1u)
+                        defer_miss(A, t, ((uint64_t)cur[u].y << 32) | cur[u].x, ((uint64_t)cur[u].w << 32) | cur[u].z,
+                                   keep_miss, wv, miss);
                 while (slow) {
                     const uint32_t us = __builtin_ctz(slow);
                     slow &= slow - 1;
@@ -1301,7 +1340,7 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
             if (k0 != 0) put_short(t, o++, k0, A.mk[2 * i + 1], A.mc[i], emit == 1);
         }
     }
-    if ((amode & 128) != 0 && miss == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // no DCE in ablation builds
+    if ((amode & (128 | 1024)) != 0 && miss == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // no DCE in ablation builds
     block_add4<kAggWaves>(&t.ctr->agg_miss, &t.ctr->carried, nullptr, nullptr, (amode & 128) == 0 ? miss : 0, carried, 0, 0,
                           A.red);
     if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
@@ -1516,13 +1555,16 @@ void launch_wc_agg(const Tables& t, int mode, int emit, bool big, hipStream_t s)
     // timed pass runs with warm caches and address translations
     const uint32_t nb = t.sp.nb;
     if (mode & 512) wc_agg_kernel<128, AggLds><<<nb, AggLds::kWaves * kWave, 0, s>>>(t, emit);
-    // Lookup strategy by layout (both exact; mode 64 swaps them for measurement):
-    // the two-set lookup pays off where buckets are full and keys often sit in
-    // their second set (C5 round 0: 16.7 -> 13.4 ms), the first-set one where
-    // tables are sparse (C2: 1.29 vs 1.50 ms).
-    const bool two_set = (nb == kSpillBucketsHi) != ((mode & 64) != 0);
+    // Lookup strategy (both exact): first-set lookups, or with mode 64 (A/B) the
+    // two-set variant.  The two-set lookup paid off for C5 only while its 2048
+    // buckets shared a hash bit with the table's set index (13.4 vs 16.7 ms);
+    // with disjoint bits the first-set path is faster there too (11.6 vs 12.5
+    // ms) and on C2 (1.29 vs 1.50 ms).
+    const bool two_set = (mode & 64) != 0;
     if (big) {
         if (mode & 128) wc_agg_kernel<128, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
+        else if (mode & 1024) wc_agg_kernel<1024, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
+        else if (mode & 2048) wc_agg_kernel<2048, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
         else if (two_set) wc_agg_kernel<0, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
         else wc_agg_kernel<64, AggLdsBig><<<nb, AggLdsBig::kWaves * kWave, 0, s>>>(t, emit);
     } else {
