@@ -160,8 +160,13 @@ struct mrg_ctx {
     uint32_t agg_carry_min = 64;
     // 1024-thread aggregator workgroups with twice the LDS table (one per CU)
     // instead of 512-thread ones (two per CU), in round 0 / later rounds.
-    // Measured: C2 aggregation 1.63 -> 1.56 ms, C5 50 -> 30 ms (4 rounds, not 6).
-    bool agg_big0 = true, agg_big_later = true;
+    // Round 0: 0 = by layout (agg_big0), 1 = big, -1 = small.  Measured: the
+    // 2048-bucket layout's ~4.9 K keys per bucket need the big table; at 512
+    // buckets (C2, ~2 K keys) two small workgroups per CU are faster, their
+    // few overflowing keys settling in round 1 (1.20 -> 1.13 ms).  Later
+    // rounds: big (C5 at 512 buckets, 4 rounds instead of 6).
+    int agg_big0 = 0;
+    bool agg_big_later = true;
     double spill_scale = 1.0;           // spill stream capacity factor (from the dictionary sample's miss rate)
     bool debug_times = getenv("MRG_DEBUG_TIMES") != nullptr;
     uint64_t rec_cap = 1u << 21;       // record output buffer capacity (grows on overflow)
@@ -650,7 +655,8 @@ static int aggregate_rounds(mrg_ctx* c, Tables& t) {
         t.sp.seg16_out = (uint4*)c->seg16[o].p;
         HCHK(c, hipMemsetAsync(&t.ctr->carried, 0, 8, c->s));
         if (c->debug_times) HCHK(c, hipEventRecord(c->ev[11], c->s));
-        launch_wc_agg(t, c->map_mode, 1, r > 0 ? c->agg_big_later : c->agg_big0, c->s);
+        const bool big0 = c->agg_big0 > 0 || (c->agg_big0 == 0 && c->spill_nb == kSpillBucketsHi);
+        launch_wc_agg(t, c->map_mode, 1, r > 0 ? c->agg_big_later : big0, c->s);
         HCHK(c, hipGetLastError());
         if (c->debug_times) {  // diagnostics: per-round time and carried misses
             HCHK(c, hipEventRecord(c->ev[5], c->s));
@@ -1071,7 +1077,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "spill_stream_keys")) c->spill_force_sub = v > 0 ? v : 0;
     else if (!strcmp(name, "agg_rounds")) c->agg_rounds = v > 0 ? (int)v : 8;
     else if (!strcmp(name, "agg_big_later")) c->agg_big_later = v >= 0;  // -1: off
-    else if (!strcmp(name, "agg_big0")) c->agg_big0 = v >= 0;  // -1: off
+    else if (!strcmp(name, "agg_big0")) c->agg_big0 = v > 0 ? 1 : v < 0 ? -1 : 0;  // 0: by layout
     else if (!strcmp(name, "agg_carry_min")) c->agg_carry_min = v > 0 ? (uint32_t)v : v < 0 ? 0u : 64u;  // -1: always carry
     else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
     else if (!strcmp(name, "dict_warm")) c->dict_warm = v >= 0;  // -1: always build the level-1 dictionary

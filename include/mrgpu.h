@@ -171,7 +171,8 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *   spill_buckets (0, 512, 2048)         spill buckets; 0 = chosen per split from the
  *                                        previous split's aggregated keys
  *   spill_hi_keys                        aggregated keys above which 2048 are chosen
- *   agg_rounds, agg_carry_min, agg_big0, agg_big_later   bucket aggregation rounds
+ *   agg_rounds, agg_carry_min, agg_big0 (0: by layout, 1 big, -1 small tables),
+ *                                        agg_big_later   bucket aggregation rounds
  *   dict (-1: off), dict_warm (-1: off), dict_keep (permille; -1: always rebuild),
  *                                        dict_min_bytes, dict_sample_bytes
  *   ingest_piece, ingest_min             host input streamed in pieces of this size

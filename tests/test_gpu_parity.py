@@ -128,9 +128,9 @@ def test_wc_bucket_aggregator_overflow(ctx, rounds, big):
     files = [bytes(voc.fill_files([26_000_000], [16], C.wc_params(vocab_lo=0, vocab_hi=3_000_000))[0])]
     ctx.set_option("agg_rounds", rounds)
     ctx.set_option("agg_carry_min", -1)  # carry every miss (default: < 64 per bucket settle in HBM)
-    # big = 0: 1024-thread tables in every round (default); -1: 512-thread tables
-    # in every round; 2: 512-thread round 0, 1024-thread later rounds
-    ctx.set_option("agg_big0", -1 if big != 0 else 0)
+    # big = 0: 1024-thread tables in every round; -1: 512-thread tables in every
+    # round; 2: 512-thread round 0, 1024-thread later rounds (the 512-bucket default)
+    ctx.set_option("agg_big0", -1 if big != 0 else 1)
     ctx.set_option("agg_big_later", -1 if big < 0 else 0)
     try:
         check(ctx, "wc", files, nreduces=(10,))
