@@ -61,6 +61,7 @@ WORKLOADS = {
 }
 PATTERN = b"distributed"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
+HBM_COPY_GBS = 6290.0  # measured copy bandwidth (secondary reference)
 XGMI_LINK_GBS = 153.0  # per xGMI link (7 links x ~153 GB/s per GPU)
 
 
@@ -438,8 +439,11 @@ def main():
                          "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": traffic,
+                         "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
+                         "map_kernel_ms_median": round(sorted(kern_ms)[len(kern_ms) // 2], 3),
                          "note": "achieved = input bytes per launch / mean HIP-event duration of the map kernel "
-                                 "on the library stream over the timed steps"},
+                                 "on the library stream over the timed steps; frac_of_measured_copy = achieved / "
+                                 "6.29 TB/s (SURVEY.md 8(d))"},
             "phases_ms": {"map_kernel": round(avg_kern, 3), "map_total": round(last["map_total_ms"], 3),
                           "dict": round(last["dict_ms"], 3), "agg": round(last["agg_ms"], 3),
                           "exchange": round(last["exchange_ms"], 3), "reduce": round(last["reduce_ms"], 3),
