@@ -185,10 +185,11 @@ struct mrg_ctx {
     uint64_t spill_sub_keys = 0, spill_sub8 = 0;
     uint32_t spill_nwg = 1;
     // Spill buckets of the current layout and of the next wc split.  2048 when
-    // the previous split's aggregated keys would not fit 512 buckets' LDS tables
-    // in one round (C5-like splits: 1e7 keys), else 512; option spill_buckets
-    // fixes it (0 = this feedback rule).
-    uint32_t spill_nb = kSpillBuckets, next_nb = kSpillBuckets;
+    // the previous split's aggregated keys would not fit 256 buckets' LDS tables
+    // (the 1024-thread ones) in one round (C5-like splits: 1e7 keys), else 256;
+    // option spill_buckets fixes it (0 = this feedback rule; 512 = the previous
+    // default, small round-0 tables).
+    uint32_t spill_nb = kSpillBucketsLo, next_nb = kSpillBucketsLo;
     int spill_buckets_opt = 0;
     uint64_t spill_hi_keys = 6000ull * kSpillBuckets;  // aggregated keys above which the next split uses 2048
     int64_t spill_force_sub = 0;
@@ -655,7 +656,7 @@ static int aggregate_rounds(mrg_ctx* c, Tables& t) {
         t.sp.seg16_out = (uint4*)c->seg16[o].p;
         HCHK(c, hipMemsetAsync(&t.ctr->carried, 0, 8, c->s));
         if (c->debug_times) HCHK(c, hipEventRecord(c->ev[11], c->s));
-        const bool big0 = c->agg_big0 > 0 || (c->agg_big0 == 0 && c->spill_nb == kSpillBucketsHi);
+        const bool big0 = c->agg_big0 > 0 || (c->agg_big0 == 0 && c->spill_nb != kSpillBuckets);
         launch_wc_agg(t, c->map_mode, 1, r > 0 ? c->agg_big_later : big0, c->s);
         HCHK(c, hipGetLastError());
         if (c->debug_times) {  // diagnostics: per-round time and carried misses
@@ -827,7 +828,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             // keys each), with hysteresis.
             const uint64_t agg_keys = h.nrec > (uint64_t)kDictSlots ? h.nrec - kDictSlots : 0;
             if (agg_keys > c->spill_hi_keys) c->next_nb = kSpillBucketsHi;
-            else if (agg_keys < c->spill_hi_keys / 3 * 2) c->next_nb = kSpillBuckets;
+            else if (agg_keys < c->spill_hi_keys / 3 * 2) c->next_nb = kSpillBucketsLo;
         }
         if (grow_on_overflow(c, h.status & (kStShortFull | kStLongFull | kStRecFull))) continue;
         if (h.long_bytes + 16 > c->recarena.cap) {  // the arena is written by collect below
@@ -1082,8 +1083,9 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "dict")) c->dict_mode = (int)v;
     else if (!strcmp(name, "dict_warm")) c->dict_warm = v >= 0;  // -1: always build the level-1 dictionary
     else if (!strcmp(name, "dict_keep")) c->dict_keep = v > 0 ? (double)v / 1000.0 : v < 0 ? 0.0 : 0.97;  // permille; -1: never
-    else if (!strcmp(name, "spill_buckets")) {  // 0: chosen per split (feedback), else 512 or 2048
-        if (v != 0 && v != kSpillBuckets && v != kSpillBucketsHi) return fail(c, MRG_EINVAL, "spill_buckets: 0, 512 or 2048");
+    else if (!strcmp(name, "spill_buckets")) {  // 0: chosen per split (feedback), else 256, 512 or 2048
+        if (v != 0 && v != kSpillBuckets && v != kSpillBucketsHi && v != kSpillBucketsLo)
+            return fail(c, MRG_EINVAL, "spill_buckets: 0, 256, 512 or 2048");
         c->spill_buckets_opt = (int)v;
     } else if (!strcmp(name, "sort_digit_bits")) {  // 64-bit radix passes: 8 or 10 bits per digit (0: by app)
         reduce_ws_set(c->rws, (int)v, -1, -1);

@@ -74,6 +74,7 @@ struct Counters {
 // the HBM table instead.
 constexpr int kSpillBuckets = 512;
 constexpr int kSpillBucketsHi = 2048;
+constexpr int kSpillBucketsLo = 256;  // the default layout: fewer, longer streams; 1024-thread aggregator tables
 constexpr int kMaxMapWGs = 512;   // map workgroups (spill streams per bucket) at most
 constexpr int kAggSegs = 8;       // aggregator waves per bucket = miss segments per bucket
 // Keys of at most 8 bytes (k1 == 0) are spilled as 8-byte records into pool8,

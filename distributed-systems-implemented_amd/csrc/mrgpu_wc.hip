@@ -45,9 +45,11 @@ constexpr uint64_t kOwn = 16 * kOwnLanes;  // 944
 constexpr int kRing = 3;                    // LDS slots per wave: current, in flight, free (the word list)
 static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot");
 
-// NW waves per workgroup, NB spill buckets.  16 waves x 512 buckets is the
-// default; high-cardinality splits use 2048 buckets, whose cursors take the
-// LDS of 4 waves' rings (12 waves per workgroup).
+// NW waves per workgroup, NB spill buckets.  16 waves x 256 buckets is the
+// default (512 streams per workgroup: fewer partially written lines competing
+// for an XCD's 4 MB L2 than 512 buckets' 1024: C2 map 8.64 -> 8.29 ms);
+// high-cardinality splits use 2048 buckets, whose cursors take the LDS of 4
+// waves' rings (12 waves per workgroup).
 template <int NW, int NB>
 struct alignas(16) MapLdsT {
     uint4 dset[kDictSets];                      // dictionary image
@@ -59,6 +61,7 @@ struct alignas(16) MapLdsT {
     uint4 kmask[17];                            // kmask[len]: the first len of 16 key bytes
 };
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBuckets>) <= 160 * 1024, "map LDS budget");
+static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBucketsLo>) <= 160 * 1024, "map LDS budget (256 buckets)");
 static_assert(sizeof(MapLdsT<12, kSpillBucketsHi>) <= 160 * 1024, "map LDS budget (high-cardinality)");
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -76,7 +79,7 @@ __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, ui
     s2 = off + (a ^ (((h >> 4) & m) | 1u));
 }
 
-// Spill bucket of a key: bits 11..19 (512 buckets) or 10..20 (2048) of its hash.
+// Spill bucket of a key: bits 11..18 (256 buckets), 11..19 (512) or 10..20 (2048) of its hash.
 // The bucket aggregator's tables index their first set by the top 11 bits
 // (21..31), so the bucket bits must stay below bit 21: a shared bit fixes one
 // set-index bit within a bucket and halves the first-choice sets (measured with
@@ -84,8 +87,8 @@ __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, ui
 // sets full and went to the next round).
 template <int NB>
 __device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
-    static_assert(NB == 512 || NB == 2048, "bucket = 9 or 11 bits");
-    return NB == 512 ? (h >> 11) & 511u : (h >> 10) & 2047u;
+    static_assert(NB == 256 || NB == 512 || NB == 2048, "bucket = 8, 9 or 11 bits");
+    return NB == 256 ? (h >> 11) & 255u : NB == 512 ? (h >> 11) & 511u : (h >> 10) & 2047u;
 }
 
 // ------------------------------------------------------------ wc map kernel
@@ -1534,6 +1537,16 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     const uint64_t g = wc_map_grid(n, grid);
     if (t.sp.nb == kSpillBucketsHi) {  // high-cardinality layout (ablation modes apply to the default one only)
         wc_map_kernel<0, 12, kSpillBucketsHi><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
+        return true;
+    }
+    if (t.sp.nb == kSpillBucketsLo) {  // the default layout (ablation modes: mapprobe.py)
+        switch (mode) {
+#define MRG_MAP_MODE(M) \
+    case M: wc_map_kernel<M, kWavesPerWG, kSpillBucketsLo><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;
+            MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(8) MRG_MAP_MODE(16) MRG_MAP_MODE(32)
+#undef MRG_MAP_MODE
+            default: wc_map_kernel<0, kWavesPerWG, kSpillBucketsLo><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
+        }
         return true;
     }
     switch (mode) {

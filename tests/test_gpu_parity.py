@@ -92,18 +92,22 @@ def test_wc_lds_overflow_and_table_growth(ctx):
         ctx.set_option("short_table_log2", 0)
 
 
-@pytest.mark.parametrize("nb", [0, 2048])
+DEFAULT_SPILL_BUCKETS = 256  # mrgpu_internal.h kSpillBucketsLo
+
+
+@pytest.mark.parametrize("nb", [0, 512, 2048])
 def test_wc_spill_region_full(wctx, nb):
     """Tiny spill streams: they overflow and the rest of their keys take the HBM-table path
     (those buckets then merge through the HBM table instead of emitting directly), in
-    the default and the high-cardinality (2048-bucket, 12-wave) layouts."""
+    the default (256 buckets), the 512-bucket and the high-cardinality (2048-bucket,
+    12-wave) layouts."""
     files = cases.synthetic(C.KIND_ASCII, 1_000_000, [6_000_000], 15)
     wctx.set_option("spill_stream_keys", 8 if nb == 0 else 2)  # (2048 buckets: ~0.5 records per stream)
     wctx.set_option("spill_buckets", nb)
     try:
         check(wctx, "wc", files, nreduces=(10,))
         assert wctx.stats()["spill_ovf"] > 0
-        assert wctx.stats()["spill_buckets"] == (nb or 512)
+        assert wctx.stats()["spill_buckets"] == (nb or DEFAULT_SPILL_BUCKETS)
     finally:
         wctx.set_option("spill_stream_keys", 0)
         wctx.set_option("spill_buckets", 0)
@@ -169,7 +173,7 @@ def test_wc_high_cardinality_buckets(ctx, rounds):
         ctx.set_option("spill_hi_keys", 1 << 40)
         gpu_partitioned(ctx, "wc", files, 10)
         gpu_partitioned(ctx, "wc", files, 10)
-        assert ctx.stats()["spill_buckets"] == 512
+        assert ctx.stats()["spill_buckets"] == DEFAULT_SPILL_BUCKETS
     finally:
         ctx.set_option("agg_rounds", 0)
         ctx.set_option("spill_buckets", 0)
