@@ -272,7 +272,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             // distance to the next non-letter, capped at 31 by a forced bit (a word
             // without a terminator in the window has more than 16 bytes).
             const uint32_t nl = ~(mA | (x1 << 16));
-            const bool owned = lane >= 1 && lane <= (uint32_t)kOwnLanes;
+            // lanes 1..kOwnLanes as a constant lane mask (a compare result is
+            // loop-invariant: hoisted, it was spilled to VGPR lanes and reloaded)
+            static_assert(kOwnLanes == 59, "owned-lane mask");
+            const bool owned = __builtin_amdgcn_inverse_ballot_w64(0x0FFFFFFFFFFFFFFEull);
             uint32_t SA = owned ? (mA & ~((mA << 1) | ((pv >> 15) & 1u)) & 0xFFFFu) : 0u;
             uint32_t total;
             uint32_t j = wave_excl_scan<4>(__popc(SA), &total);
@@ -316,6 +319,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     uint64_t k0[kBatch], k1[kBatch];
                     uint32_t hh[kBatch];
                     bool ok[kBatch], lng[kBatch];
+                    // lane masks taken once, before the long-word branch: per-lane bools
+                    // live across a branch as 0/1 VGPRs and get re-compared after it
+                    uint64_t mOk[kBatch], mMid[kBatch];
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         const uint32_t w = base + lane + 64u * u;
@@ -334,6 +340,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         k0[u] = ((uint64_t)(w1 & km[u].y) << 32) | (w0 & km[u].x);
                         k1[u] = ((uint64_t)(w3 & km[u].w) << 32) | (w2 & km[u].z);
                         hh[u] = fold32((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
+                        mOk[u] = __ballot(ok[u]);
+                        mMid[u] = __ballot(k1[u] != 0);
                     }
                     // words of more than 16 bytes: resolved by wc_long_kernel from the input (rare)
                     if (__ballot(lng[0] || lng[1] || lng[2])) {  // rare: a global atomic, then drain
@@ -348,13 +356,13 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         continue;
                     }
                     bool hit[kBatch];
-                    uint64_t mHit[kBatch], mOk[kBatch];  // lane masks of hit[], ok[]
+                    uint64_t mHit[kBatch];  // lane mask of hit[]
                     if (use_dict) {
                         u32x4 A[kBatch], B[kBatch];
                         uint32_t s1[kBatch], s2[kBatch];
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
-                            dict_sets(hh[u], k1[u] != 0, s1[u], s2[u]);
+                            dict_sets(hh[u], __builtin_amdgcn_inverse_ballot_w64(mMid[u]), s1[u], s2[u]);
                             A[u] = dset[s1[u]];
                             B[u] = dset[s2[u]];
                         }
@@ -364,7 +372,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             // short key: any of the 4 ways of its two sets; mid key: the single
                             // 16-byte way of either set (kk = the word compared with each set's
                             // second 8 bytes)
-                            const bool mid = k1[u] != 0;
+                            const bool mid = __builtin_amdgcn_inverse_ballot_w64(mMid[u]);
                             const uint64_t kk = mid ? k1[u] : k0[u];
                             const uint64_t alo = ((uint64_t)A[u].y << 32) | A[u].x, ahi = ((uint64_t)A[u].w << 32) | A[u].z;
                             const uint64_t blo = ((uint64_t)B[u].y << 32) | B[u].x, bhi = ((uint64_t)B[u].w << 32) | B[u].z;
@@ -373,17 +381,17 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             // (&&, ||) or to 0/1 VALU arithmetic.  inverse_ballot reads this
                             // lane's bit back as a condition at no cost.  The batch runs with
                             // every lane active.
-                            const uint64_t mMid = __ballot(mid);
-                            mOk[u] = __ballot(ok[u]);
+                            const uint64_t mMidU = mMid[u];
                             const uint64_t mA0 = __ballot(alo == k0[u]), mA1 = __ballot(ahi == kk);
                             const uint64_t mB0 = __ballot(blo == k0[u]), mB1 = __ballot(bhi == kk);
-                            const uint64_t mHa = (mA0 & mA1) | (~mMid & (mA0 | mA1));
-                            const uint64_t mHb = (mB0 & mB1) | (~mMid & (mB0 | mB1));
+                            const uint64_t mHa = (mA0 & mA1) | (~mMidU & (mA0 | mA1));
+                            const uint64_t mHb = (mB0 & mB1) | (~mMidU & (mB0 | mB1));
                             mHit[u] = mOk[u] & (mHa | mHb);
                             hit[u] = __builtin_amdgcn_inverse_ballot_w64(mHit[u]);
-                            const uint32_t wa = __builtin_amdgcn_inverse_ballot_w64(~mMid & ~mA0) ? 1u : 0u;
-                            const uint32_t wb = __builtin_amdgcn_inverse_ballot_w64(~mMid & ~mB0) ? 1u : 0u;
-                            const uint32_t slot = __builtin_amdgcn_inverse_ballot_w64(mHa) ? 2 * s1[u] + wa : 2 * s2[u] + wb;
+                            // way within the hit set (scalar mask logic), then one select of the set
+                            const uint64_t mWay = ~mMidU & ((mHa & ~mA0) | (~mHa & ~mB0));
+                            const uint32_t hset = __builtin_amdgcn_inverse_ballot_w64(mHa) ? s1[u] : s2[u];
+                            const uint32_t slot = 2 * hset + (__builtin_amdgcn_inverse_ballot_w64(mWay) ? 1u : 0u);
                             bool cnt_lds = hit[u];
                             if constexpr ((mode & 8) != 0) cnt_lds = false;  // ablation: counters not updated
                             const uint32_t ci = cnt_lds ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
@@ -394,7 +402,6 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         for (int u = 0; u < kBatch; u++) {
                             hit[u] = false;
                             mHit[u] = 0;
-                            mOk[u] = __ballot(ok[u]);
                         }
                     }
                     if constexpr ((mode & 16) != 0) {
@@ -416,7 +423,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         mMiss[u] = mOk[u] & ~mHit[u];
-                        mBig[u] = __ballot(k1[u] != 0);  // key of 9-16 bytes: 16-byte record
+                        mBig[u] = mMid[u];  // key of 9-16 bytes: 16-byte record
                         nmu[u + 1] = nmu[u] + (uint32_t)__popcll(mMiss[u]);
                     }
                     const uint32_t nm = nmu[kBatch];
@@ -446,9 +453,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                                               put8 ? (__umul24(b, sub8) + pos) * 8u : kOutOfRange, 0, 0);
                         __builtin_amdgcn_raw_buffer_store_b128(r, rs16, put16 ? (__umul24(b, sub) + pos) * 16u : kOutOfRange,
                                                                0, 0);
-                        const bool over = valid & (big ? !fit16 : !fit8);
-                        if (__ballot(over)) {  // a stream is full: count in the HBM table; the bucket then merges through it
-                            if (over) {
+                        // (lane masks, not a per-lane bool: no 0/1 VGPR round trip)
+                        const uint64_t mBigS = __ballot(big), mF8 = __ballot(fit8), mF16 = __ballot(fit16);
+                        const uint64_t mOver = __ballot(valid) & ((mBigS & ~mF16) | (~mBigS & ~mF8));
+                        if (mOver) {  // a stream is full: count in the HBM table; the bucket then merges through it
+                            if (__builtin_amdgcn_inverse_ballot_w64(mOver)) {
                                 short_insert(t, ((uint64_t)r.y << 32) | r.x, ((uint64_t)r.w << 32) | r.z, 1);
                                 t.bflag[b] = 1u;
                                 ovf++;
