@@ -73,6 +73,20 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t c, uint32_t* total) 
     return base;
 }
 
+// Inclusive prefix sum over the wave by DPP (gfx9 row_shr 1/2/4/8 within 16-lane
+// rows, then row_bcast 15 / 31 across rows): 6 adds, against ballot bit-planes'
+// 2 VALU + 2 mbcnt per bit.  Lanes whose DPP source is outside the row read the
+// old value 0.
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // One wave-wide atomicAdd for the lanes with `want` set; returns each such
 // lane's slot (base + rank among the wanting lanes).  Replaces one same-address
 // atomic per lane (which serialises at the memory side) by one per wave.

@@ -277,8 +277,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             static_assert(kOwnLanes == 59, "owned-lane mask");
             const bool owned = __builtin_amdgcn_inverse_ballot_w64(0x0FFFFFFFFFFFFFFEull);
             uint32_t SA = owned ? (mA & ~((mA << 1) | ((pv >> 15) & 1u)) & 0xFFFFu) : 0u;
-            uint32_t total;
-            uint32_t j = wave_excl_scan<4>(__popc(SA), &total);
+            const uint32_t nsa = __popc(SA);
+            const uint32_t incl = wave_incl_scan_dpp(nsa);
+            const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+            uint32_t j = incl - nsa;
             const uint32_t pos0 = 16 * lane;
             while (SA) {
                 const uint32_t bit = __builtin_ctz(SA);
@@ -304,7 +306,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         const uint32_t w = base + lane + 64u * u;
-                        e[u] = list[w < total ? w : 0u];
+                        // slots past the list read stale LDS (w <= 575: inside the workgroup's
+                        // allocation); every use below is masked by valid = w < total
+                        e[u] = list[w];
                     }
                     // the 20 bytes [s & ~3, +20) of each key: five dword reads (the same LDS
                     // cycles as three aligned 8-byte reads, without their 8-byte-phase selects)
@@ -318,17 +322,17 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     }
                     uint64_t k0[kBatch], k1[kBatch];
                     uint32_t hh[kBatch];
-                    bool ok[kBatch], lng[kBatch];
-                    // lane masks taken once, before the long-word branch: per-lane bools
-                    // live across a branch as 0/1 VGPRs and get re-compared after it
-                    uint64_t mOk[kBatch], mMid[kBatch];
+                    // lane masks straight from the compares, taken once before the
+                    // long-word branch (a per-lane bool lives across a branch as a 0/1
+                    // VGPR and is re-compared after it)
+                    uint64_t mOk[kBatch], mLng[kBatch], mMid[kBatch];
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         const uint32_t w = base + lane + 64u * u;
-                        const bool valid = w < total;
                         const uint32_t s = e[u] & 0x3FFu, len = e[u] >> 10;
-                        ok[u] = valid & (len <= 16);
-                        lng[u] = valid & (len > 16);
+                        const uint64_t mValid = __ballot(w < total), mLe16 = __ballot(len <= 16);
+                        mOk[u] = mValid & mLe16;
+                        mLng[u] = mValid & ~mLe16;
                         // 16 key bytes at [s, s+16)
                         const uint32_t sh = s & 3u;
                         const uint32_t a0 = g0[u], a1 = g1[u], a2 = g2[u], a3 = g3[u], a4 = g4[u];
@@ -340,19 +344,18 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         k0[u] = ((uint64_t)(w1 & km[u].y) << 32) | (w0 & km[u].x);
                         k1[u] = ((uint64_t)(w3 & km[u].w) << 32) | (w2 & km[u].z);
                         hh[u] = fold32((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
-                        mOk[u] = __ballot(ok[u]);
                         mMid[u] = __ballot(k1[u] != 0);
                     }
                     // words of more than 16 bytes: resolved by wc_long_kernel from the input (rare)
-                    if (__ballot(lng[0] || lng[1] || lng[2])) {  // rare: a global atomic, then drain
+                    if (mLng[0] | mLng[1] | mLng[2]) {  // rare: a global atomic, then drain
         #pragma unroll
                         for (int u = 0; u < kBatch; u++)
-                            if (lng[u]) list_append(t, cs - kBack + (e[u] & 0x3FFu));
+                            if (__builtin_amdgcn_inverse_ballot_w64(mLng[u])) list_append(t, cs - kBack + (e[u] & 0x3FFu));
                         wait_vmem_all();
                     }
                     if constexpr ((mode & 4) != 0) {
         #pragma unroll
-                        for (int u = 0; u < kBatch; u++) acc += ok[u] ? hh[u] : 0u;
+                        for (int u = 0; u < kBatch; u++) acc += __builtin_amdgcn_inverse_ballot_w64(mOk[u]) ? hh[u] : 0u;
                         continue;
                     }
                     bool hit[kBatch];
