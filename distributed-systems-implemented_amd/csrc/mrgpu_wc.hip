@@ -50,16 +50,21 @@ static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot"
 // for an XCD's 4 MB L2 than 512 buckets' 1024: C2 map 8.64 -> 8.29 ms);
 // high-cardinality splits use 2048 buckets, whose cursors take the LDS of 4
 // waves' rings (12 waves per workgroup).
+// Field order keeps the ring slots 1 KiB-aligned and the mask table 512-byte
+// aligned (dset is 68 KiB), so addresses inside them are one v_and_or_b32.
+constexpr int kMaskLens = 18;  // kmask[len], len = 0..17 (17 = "more than 16 bytes", never used as a key)
 template <int NW, int NB>
 struct alignas(16) MapLdsT {
-    uint4 dset[kDictSets];                      // dictionary image
-    uint32_t dcnt[kDictSlots + kWave];          // dictionary counts of this workgroup (+ per-lane miss dummies)
+    uint4 dset[kDictSets];                      // dictionary image (LDS offset 0: set addresses are plain offsets)
     uint8_t ring[NW][kRing][kSlotBytes];
+    uint4 kmask[kMaskLens];                     // kmask[len]: the first min(len, 16) of 16 key bytes
+    uint32_t dcnt[kDictSlots + kWave];          // dictionary counts of this workgroup (+ per-lane miss dummies)
     // spill cursors: [0, NB) 8-byte streams, [NB, 2 NB) 16-byte streams, then per-lane dummies for hits
     uint32_t curs[2 * NB + kWave];
     unsigned long long red[4 * kWavesPerWG];    // block_add4 scratch
-    uint4 kmask[17];                            // kmask[len]: the first len of 16 key bytes
 };
+static_assert(sizeof(uint4) * kDictSets % 1024 == 0, "ring slots 1 KiB-aligned");
+static_assert(kSlotBytes == 1024 && kMaskLens * 16 <= 512, "kmask 512-byte aligned, index fits 0x1F0");
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBuckets>) <= 160 * 1024, "map LDS budget");
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBucketsLo>) <= 160 * 1024, "map LDS budget (256 buckets)");
 static_assert(sizeof(MapLdsT<12, kSpillBucketsHi>) <= 160 * 1024, "map LDS budget (high-cardinality)");
@@ -68,15 +73,25 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
 }
 
-// The two candidate dictionary sets of a key (hash h; mid = key of 9-16 bytes).
+// The two candidate dictionary sets of a key (hash h; mid = key of 9-16 bytes),
+// as byte offsets of dset (16-byte sets at LDS offset 0): short keys take set
+// a = h >> 20 and a ^ x, x = ((h >> 4) & 4095) | 1; mid keys the same bits
+// masked to 8 (a = (h >> 20) & 255), in the 256 sets after the 4096 short ones.
+// Computed pre-scaled by 16 with two masks, not three selects and two shifts.
+__device__ __forceinline__ void dict_set_addrs(uint32_t h, bool mid, uint32_t& a1, uint32_t& a2) {
+    static_assert(kDictShortSets == 4096 && kDictMidSets == 256, "set index = 12 / 8 hash bits");
+    const uint32_t m = mid ? 0x0FF0u : 0xFFF0u;
+    const uint32_t off = mid ? (uint32_t)kDictShortSets * 16u : 0u;
+    const uint32_t A = h >> 16;           // a << 4 in bits 4..15
+    const uint32_t X = (h & ~15u) | 16u;  // x << 4 in bits 4..15 (bit 4 forced: a2 != a1)
+    a1 = (A & m) | off;
+    a2 = ((A ^ X) & m) | off;
+}
 __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, uint32_t& s2) {
-    static_assert(kDictShortSets == 4096 && kDictMidSets == 256, "set index = top 12 / 8 bits");
-    const uint32_t sh = mid ? 24u : 20u;
-    const uint32_t m = mid ? (uint32_t)(kDictMidSets - 1) : (uint32_t)(kDictShortSets - 1);
-    const uint32_t off = mid ? (uint32_t)kDictShortSets : 0u;
-    const uint32_t a = h >> sh;
-    s1 = off + a;
-    s2 = off + (a ^ (((h >> 4) & m) | 1u));
+    uint32_t a1, a2;
+    dict_set_addrs(h, mid, a1, a2);
+    s1 = a1 >> 4;
+    s2 = a2 >> 4;
 }
 
 // Spill bucket of a key: bits 11..18 (256 buckets), 11..19 (512) or 10..20 (2048) of its hash.
@@ -202,7 +217,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         else if (resume && b < 2u * NB) v = t.sp.counts[(uint64_t)(b - NB) * t.sp.nwg + blockIdx.x];
         curs[b] = v;
     }
-    if (tid < 17 * 4) {  // byte masks: dword d of kmask[len] keeps clamp(len - 4d, 0, 4) bytes
+    if (tid < kMaskLens * 4) {  // byte masks: dword d of kmask[len] keeps clamp(len - 4d, 0, 4) bytes
         const int nb = min(max((int)(tid >> 2) - 4 * (int)(tid & 3), 0), 4);
         ((uint32_t*)L.kmask)[tid] = nb == 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
     }
@@ -234,6 +249,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     for (uint32_t c = c0; c < cend; c += stride, cs += cstep, k = k == kRing - 1 ? 0 : k + 1) {
         wait_vmem_iter();  // chunk c's DMA (issued two iterations ago) has landed
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
+        const uint32_t bufa = ring0 + k * kSlotBytes;  // = lds_addr(buf), 1 KiB-aligned
         lds_uint4* b4 = (lds_uint4*)buf;
         const uint32_t kf = k == 0 ? kRing - 1 : k - 1;  // free slot: the word list now, chunk c + 2*stride next
         lds_u16* list = (lds_u16*)L.ring[wv][kf];
@@ -269,8 +285,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint32_t pv = wave_shr1(mA, 0u);
             // Non-letters of this lane's 16 bytes and the next lane's.  A word starts at
             // bit <= 15, so one of <= 16 bytes ends by bit 31; the length is the
-            // distance to the next non-letter, capped at 31 by a forced bit (a word
-            // without a terminator in the window has more than 16 bytes).
+            // distance to the next non-letter, capped at 17 by a forced bit (17 = more
+            // than 16 bytes: a word without a terminator in the window has more than
+            // 16, and 17 indexes the mask table directly, no clamp).
             const uint32_t nl = ~(mA | (x1 << 16));
             // lanes 1..kOwnLanes as a constant lane mask (a compare result is
             // loop-invariant: hoisted, it was spilled to VGPR lanes and reloaded)
@@ -284,7 +301,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint32_t pos0 = 16 * lane;
             while (SA) {
                 const uint32_t bit = __builtin_ctz(SA);
-                const uint32_t len = __builtin_ctz((nl >> bit) | 0x80000000u);
+                const uint32_t len = __builtin_ctz((nl >> bit) | (1u << 17));
                 list[j++] = (uint16_t)((pos0 + bit) | (len << 10));
                 SA &= SA - 1;
             }
@@ -316,9 +333,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     u32x4 km[kBatch];  // the key's byte mask, from the length (same round trip)
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        const lds_u32* p4 = (const lds_u32*)(buf + ((e[u] & 0x3FFu) & ~3u));
+                        // the slot is 1 KiB-aligned: base | offset (one v_and_or_b32)
+                        const lds_u32* p4 = (const lds_u32*)(uintptr_t)(bufa | (e[u] & 0x3FCu));
                         g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
-                        km[u] = kmask4[min(e[u] >> 10, 16u)];
+                        km[u] = kmask4[__builtin_amdgcn_ubfe(e[u], 10, 5)];  // len <= 17 (the tokenizer's cap)
                     }
                     uint64_t k0[kBatch], k1[kBatch];
                     uint32_t hh[kBatch];
@@ -362,12 +380,12 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     uint64_t mHit[kBatch];  // lane mask of hit[]
                     if (use_dict) {
                         u32x4 A[kBatch], B[kBatch];
-                        uint32_t s1[kBatch], s2[kBatch];
+                        uint32_t a1[kBatch], a2[kBatch];  // byte offsets of the two sets
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
-                            dict_sets(hh[u], __builtin_amdgcn_inverse_ballot_w64(mMid[u]), s1[u], s2[u]);
-                            A[u] = dset[s1[u]];
-                            B[u] = dset[s2[u]];
+                            dict_set_addrs(hh[u], __builtin_amdgcn_inverse_ballot_w64(mMid[u]), a1[u], a2[u]);
+                            A[u] = *(const lds_uint4*)((const lds_u8*)dset + a1[u]);
+                            B[u] = *(const lds_uint4*)((const lds_u8*)dset + a2[u]);
                         }
                         __builtin_amdgcn_sched_barrier(0);  // all 2 * kBatch set reads in flight before the compares
         #pragma unroll
@@ -393,8 +411,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             hit[u] = __builtin_amdgcn_inverse_ballot_w64(mHit[u]);
                             // way within the hit set (scalar mask logic), then one select of the set
                             const uint64_t mWay = ~mMidU & ((mHa & ~mA0) | (~mHa & ~mB0));
-                            const uint32_t hset = __builtin_amdgcn_inverse_ballot_w64(mHa) ? s1[u] : s2[u];
-                            const uint32_t slot = 2 * hset + (__builtin_amdgcn_inverse_ballot_w64(mWay) ? 1u : 0u);
+                            const uint32_t hset = __builtin_amdgcn_inverse_ballot_w64(mHa) ? a1[u] : a2[u];
+                            const uint32_t slot = (hset >> 3) + (__builtin_amdgcn_inverse_ballot_w64(mWay) ? 1u : 0u);  // 2 set + way
                             bool cnt_lds = hit[u];
                             if constexpr ((mode & 8) != 0) cnt_lds = false;  // ablation: counters not updated
                             const uint32_t ci = cnt_lds ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
