@@ -78,10 +78,10 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t c, uint32_t* total) 
 // 2 VALU + 2 mbcnt per bit.  Lanes whose DPP source is outside the row read the
 // old value 0.
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x111, 0xF, 0xF, false);  // row_shr:1
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x112, 0xF, 0xF, false);  // row_shr:2
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x114, 0xF, 0xF, false);  // row_shr:4
-    v += __builtin_amdgcn_update_dpp(0u, v, 0x118, 0xF, 0xF, false);  // row_shr:8
+    v += __builtin_amdgcn_mov_dpp(v, 0x111, 0xF, 0xF, true);  // row_shr:1 (BOUND_CTRL: 0 from outside the row)
+    v += __builtin_amdgcn_mov_dpp(v, 0x112, 0xF, 0xF, true);  // row_shr:2
+    v += __builtin_amdgcn_mov_dpp(v, 0x114, 0xF, 0xF, true);  // row_shr:4
+    v += __builtin_amdgcn_mov_dpp(v, 0x118, 0xF, 0xF, true);  // row_shr:8
     v += __builtin_amdgcn_update_dpp(0u, v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
     v += __builtin_amdgcn_update_dpp(0u, v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
     return v;
@@ -169,6 +169,9 @@ __device__ __forceinline__ uint32_t wave_shr1(uint32_t v, uint32_t fill) {
 __device__ __forceinline__ uint32_t wave_shl1(uint32_t v, uint32_t fill) {
     return __builtin_amdgcn_update_dpp(fill, v, 0x130, 0xf, 0xf, false);
 }
+// The same with 0 shifted in, by BOUND_CTRL (no copy of a fill value first).
+__device__ __forceinline__ uint32_t wave_shr1_z(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x138, 0xf, 0xf, true); }
+__device__ __forceinline__ uint32_t wave_shl1_z(uint32_t v) { return __builtin_amdgcn_mov_dpp(v, 0x130, 0xf, 0xf, true); }
 
 // 4 ASCII bytes -> 4-bit letter mask ([A-Za-z]); requires every byte < 0x80.
 __device__ __forceinline__ uint32_t ascii_letters4(uint32_t x) {
@@ -176,8 +179,21 @@ __device__ __forceinline__ uint32_t ascii_letters4(uint32_t x) {
     const uint32_t t = (y + 0x1F1F1F1Fu) & ~(y + 0x05050505u) & 0x80808080u;
     return ((t >> 7) * 0x10204080u) >> 28;
 }
+// 0x80 in each [A-Za-z] byte of 4 ASCII bytes, else 0 (the SWAR test above, the
+// three-input and as one v_bitop3_b32: a & ~b & c = truth table 0x20).
+__device__ __forceinline__ uint32_t ascii_flags4(uint32_t x) {
+    const uint32_t y = x | 0x20202020u;
+    return __builtin_amdgcn_bitop3_b32(y + 0x1F1F1F1Fu, y + 0x05050505u, 0x80808080u, 0x20);
+}
+// 16 ASCII bytes -> 16-bit letter mask.  The flag bytes are gathered by byte dot
+// products (v_dot4_u32_u8) with weights 1,2,4,8 / 16,32,64,128: the 8-bit masks
+// of two dwords, times 0x80, in one accumulate chain; no 32-bit multiplies.
 __device__ __forceinline__ uint32_t ascii_mask16(uint4 v) {
-    return ascii_letters4(v.x) | (ascii_letters4(v.y) << 4) | (ascii_letters4(v.z) << 8) | (ascii_letters4(v.w) << 12);
+    const uint32_t lo = __builtin_amdgcn_udot4(ascii_flags4(v.y), 0x80402010u,
+                                               __builtin_amdgcn_udot4(ascii_flags4(v.x), 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(ascii_flags4(v.w), 0x80402010u,
+                                               __builtin_amdgcn_udot4(ascii_flags4(v.z), 0x08040201u, 0u, false), false);
+    return (lo | (hi << 8)) >> 7;
 }
 
 __device__ __forceinline__ bool is_letter_cp(uint32_t cp, LetterTables lt) {

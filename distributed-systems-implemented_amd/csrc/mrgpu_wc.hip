@@ -246,12 +246,14 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn + cstep, lane, ring0 + kSlotBytes);
     uint32_t k = 0;  // ring slot of the current chunk
     uint64_t cs = (uint64_t)c0 * kOwn;  // the current chunk's first own byte = slot byte 16 (slot byte i = input cs - 16 + i)
-    for (uint32_t c = c0; c < cend; c += stride, cs += cstep, k = k == kRing - 1 ? 0 : k + 1) {
+    // kf = the free slot (the word list now, chunk c + 2*stride next) = the slot
+    // before k; both rotate as loop-carried scalars
+    uint32_t kf = kRing - 1;
+    for (uint32_t c = c0; c < cend; c += stride, cs += cstep, kf = k, k = k == kRing - 1 ? 0 : k + 1) {
         wait_vmem_iter();  // chunk c's DMA (issued two iterations ago) has landed
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
         const uint32_t bufa = ring0 + k * kSlotBytes;  // = lds_addr(buf), 1 KiB-aligned
         lds_uint4* b4 = (lds_uint4*)buf;
-        const uint32_t kf = k == 0 ? kRing - 1 : k - 1;  // free slot: the word list now, chunk c + 2*stride next
         lds_u16* list = (lds_u16*)L.ring[wv][kf];
         if (c >= ctail) {  // the window reaches the split's last n % 4 bytes (ctail = ~0u: none)
             // the split's last n % 4 bytes sit in a dword the range check zero-filled
@@ -281,8 +283,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             // Word starts (a letter byte whose predecessor is not one) in the owned lanes
             // and lengths (ctz over this lane's mask and the next two lanes'), packed into
             // the list as slot position | min(len, 31) << 10.  Neighbour masks by DPP.
-            const uint32_t x1 = wave_shl1(mA, 0u);
-            const uint32_t pv = wave_shr1(mA, 0u);
+            const uint32_t x1 = wave_shl1_z(mA);
+            const uint32_t pv = wave_shr1_z(mA);
             // Non-letters of this lane's 16 bytes and the next lane's.  A word starts at
             // bit <= 15, so one of <= 16 bytes ends by bit 31; the length is the
             // distance to the next non-letter, capped at 17 by a forced bit (17 = more
