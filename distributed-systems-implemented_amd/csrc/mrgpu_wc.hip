@@ -349,12 +349,12 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         const uint32_t w = base + lane + 64u * u;
-                        const uint32_t s = e[u] & 0x3FFu, len = e[u] >> 10;
+                        const uint32_t len = e[u] >> 10;
                         const uint64_t mValid = __ballot(w < total), mLe16 = __ballot(len <= 16);
                         mOk[u] = mValid & mLe16;
                         mLng[u] = mValid & ~mLe16;
                         // 16 key bytes at [s, s+16)
-                        const uint32_t sh = s & 3u;
+                        const uint32_t sh = e[u] & 3u;
                         const uint32_t a0 = g0[u], a1 = g1[u], a2 = g2[u], a3 = g3[u], a4 = g4[u];
                         const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
                         const uint32_t w1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
@@ -414,11 +414,14 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             // way within the hit set (scalar mask logic), then one select of the set
                             const uint64_t mWay = ~mMidU & ((mHa & ~mA0) | (~mHa & ~mB0));
                             const uint32_t hset = __builtin_amdgcn_inverse_ballot_w64(mHa) ? a1[u] : a2[u];
-                            const uint32_t slot = (hset >> 3) + (__builtin_amdgcn_inverse_ballot_w64(mWay) ? 1u : 0u);  // 2 set + way
+                            // counter byte offset: 4 (2 set + way) = (set offset >> 1) + 4 way
+                            const uint32_t cofs = (hset >> 1) + (__builtin_amdgcn_inverse_ballot_w64(mWay) ? 4u : 0u);
                             bool cnt_lds = hit[u];
                             if constexpr ((mode & 8) != 0) cnt_lds = false;  // ablation: counters not updated
-                            const uint32_t ci = cnt_lds ? slot : (uint32_t)kDictSlots + lane;  // per-lane dummy on a miss
-                            __hip_atomic_fetch_add(&dcnt[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            // only the hit lanes add (exec-masked: two scalar ops, where a
+                            // per-lane dummy counter for the misses cost a select)
+                            if (cnt_lds)
+                                __hip_atomic_fetch_add((lds_u32*)((lds_u8*)dcnt + cofs), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     } else {
         #pragma unroll
