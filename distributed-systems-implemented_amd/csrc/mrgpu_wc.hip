@@ -50,21 +50,21 @@ static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot"
 // for an XCD's 4 MB L2 than 512 buckets' 1024: C2 map 8.64 -> 8.29 ms);
 // high-cardinality splits use 2048 buckets, whose cursors take the LDS of 4
 // waves' rings (12 waves per workgroup).
-// Field order keeps the ring slots 1 KiB-aligned and the mask table 512-byte
-// aligned (dset is 68 KiB), so addresses inside them are one v_and_or_b32.
+// The mask table sits at LDS offset 0 (its address is (entry >> 6) & 0x1F0, no
+// base); the dictionary's set offsets are then constant-displaced, which the
+// ds_read offset field absorbs.
 constexpr int kMaskLens = 18;  // kmask[len], len = 0..17 (17 = "more than 16 bytes", never used as a key)
 template <int NW, int NB>
 struct alignas(16) MapLdsT {
-    uint4 dset[kDictSets];                      // dictionary image (LDS offset 0: set addresses are plain offsets)
-    uint8_t ring[NW][kRing][kSlotBytes];
     uint4 kmask[kMaskLens];                     // kmask[len]: the first min(len, 16) of 16 key bytes
+    uint4 dset[kDictSets];                      // dictionary image
+    uint8_t ring[NW][kRing][kSlotBytes];
     uint32_t dcnt[kDictSlots + kWave];          // dictionary counts of this workgroup (+ per-lane miss dummies)
     // spill cursors: [0, NB) 8-byte streams, [NB, 2 NB) 16-byte streams, then per-lane dummies for hits
     uint32_t curs[2 * NB + kWave];
     unsigned long long red[4 * kWavesPerWG];    // block_add4 scratch
 };
-static_assert(sizeof(uint4) * kDictSets % 1024 == 0, "ring slots 1 KiB-aligned");
-static_assert(kSlotBytes == 1024 && kMaskLens * 16 <= 512, "kmask 512-byte aligned, index fits 0x1F0");
+static_assert(kSlotBytes == 1024 && kMaskLens * 16 <= 512, "kmask index fits 0x1F0");
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBuckets>) <= 160 * 1024, "map LDS budget");
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBucketsLo>) <= 160 * 1024, "map LDS budget (256 buckets)");
 static_assert(sizeof(MapLdsT<12, kSpillBucketsHi>) <= 160 * 1024, "map LDS budget (high-cardinality)");
@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     for (uint32_t c = c0; c < cend; c += stride, cs += cstep, kf = k, k = k == kRing - 1 ? 0 : k + 1) {
         wait_vmem_iter();  // chunk c's DMA (issued two iterations ago) has landed
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
-        const uint32_t bufa = ring0 + k * kSlotBytes;  // = lds_addr(buf), 1 KiB-aligned
+        const uint32_t bufa = ring0 + k * kSlotBytes;  // = lds_addr(buf)
         lds_uint4* b4 = (lds_uint4*)buf;
         lds_u16* list = (lds_u16*)L.ring[wv][kf];
         if (c >= ctail) {  // the window reaches the split's last n % 4 bytes (ctail = ~0u: none)
@@ -335,8 +335,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     u32x4 km[kBatch];  // the key's byte mask, from the length (same round trip)
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        // the slot is 1 KiB-aligned: base | offset (one v_and_or_b32)
-                        const lds_u32* p4 = (const lds_u32*)(uintptr_t)(bufa | (e[u] & 0x3FCu));
+                        const lds_u32* p4 = (const lds_u32*)(uintptr_t)(bufa + (e[u] & 0x3FCu));
                         g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
                         km[u] = kmask4[__builtin_amdgcn_ubfe(e[u], 10, 5)];  // len <= 17 (the tokenizer's cap)
                     }
@@ -348,13 +347,14 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     uint64_t mOk[kBatch], mLng[kBatch], mMid[kBatch];
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
-                        const uint32_t w = base + lane + 64u * u;
+                        // w = base + 64 u + lane < total <=> lane + 64 u < total - base (lane + 64 u
+                        // is loop-invariant, total - base a scalar; passes cover total: no wrap)
                         const uint32_t len = e[u] >> 10;
-                        const uint64_t mValid = __ballot(w < total), mLe16 = __ballot(len <= 16);
+                        const uint64_t mValid = __ballot(lane + 64u * u < total - base), mLe16 = __ballot(len <= 16);
                         mOk[u] = mValid & mLe16;
                         mLng[u] = mValid & ~mLe16;
                         // 16 key bytes at [s, s+16)
-                        const uint32_t sh = e[u] & 3u;
+                        const uint32_t sh = e[u];  // v_alignbyte uses only the low 2 bits of its shift
                         const uint32_t a0 = g0[u], a1 = g1[u], a2 = g2[u], a3 = g3[u], a4 = g4[u];
                         const uint32_t w0 = __builtin_amdgcn_alignbyte(a1, a0, sh);
                         const uint32_t w1 = __builtin_amdgcn_alignbyte(a2, a1, sh);
