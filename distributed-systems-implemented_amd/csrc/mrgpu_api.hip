@@ -193,6 +193,7 @@ struct mrg_ctx {
     int spill_buckets_opt = 0;
     uint64_t spill_hi_keys = 6000ull * kSpillBuckets;  // aggregated keys above which the next split uses 2048
     int64_t spill_force_sub = 0;
+    int spill_mid_div = 2;  // 16-byte streams hold sub8 / spill_mid_div records (option spill_mid_div)
     int map_mode = 0;  // benchmark ablation of wc_map_kernel phases (0 = normal)
     // mrg_run_job without the shuffle even with a communicator (bench.py's
     // same-process T(1) for the weak-scaling efficiency: the rank's own split,
@@ -331,9 +332,9 @@ static Recs rec_view(mrg_ctx* c) {
 static int ensure_spill(mrg_ctx* c, uint64_t n) {
     const uint32_t nwg = wc_map_grid(n, c->grid);
     const uint64_t nb = c->spill_nb;
-    uint64_t sub = (uint64_t)((double)((n - n / 4) / 16 / (nb * nwg)) * c->spill_scale) + 64;
-    sub = (sub + 63) & ~63ull;
-    uint64_t sub8 = 2 * sub;
+    uint64_t sub8 = 2 * ((uint64_t)((double)((n - n / 4) / 16 / (nb * nwg)) * c->spill_scale) + 64);
+    sub8 = (sub8 + 63) & ~63ull;
+    uint64_t sub = (sub8 / (uint64_t)std::max(1, c->spill_mid_div) + 63) & ~63ull;
     // test knob: tiny streams (even: the aggregator reads 8-byte records in pairs)
     if (c->spill_force_sub > 0) sub = sub8 = ((uint64_t)c->spill_force_sub + 1) & ~1ull;
     // a workgroup's streams are addressed by 32-bit byte offsets in the map kernel
@@ -1076,6 +1077,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "map_grid")) c->grid = v > 0 ? (int)v : map_grid_size(c->device);
     else if (!strcmp(name, "map_mode")) c->map_mode = (int)v;
     else if (!strcmp(name, "spill_stream_keys")) c->spill_force_sub = v > 0 ? v : 0;
+    else if (!strcmp(name, "spill_mid_div")) c->spill_mid_div = v > 0 ? (int)v : 2;
     else if (!strcmp(name, "agg_rounds")) c->agg_rounds = v > 0 ? (int)v : 8;
     else if (!strcmp(name, "agg_big_later")) c->agg_big_later = v >= 0;  // -1: off
     else if (!strcmp(name, "agg_big0")) c->agg_big0 = v > 0 ? 1 : v < 0 ? -1 : 0;  // 0: by layout
