@@ -36,9 +36,11 @@ def edge_cases() -> dict[str, list[bytes]]:
         # splits whose last bytes are a word, for every n % 4 (the map streams the
         # split with range-checked 16-byte loads and patches its last n % 4 bytes)
         "tail_bytes": [b"a", b"ab", b"abc", b"abcd", b"abcde", b"xy z", b"q r st", b"  uvw"],
-        # words of 1..20 letters at every offset around 944-byte chunk seams, 16-byte
-        # lanes and the 1 KiB windows, split lengths of every residue mod 4
-        "mixed_lengths": [mixed_words(n, seed) for seed, n in enumerate([12345, 7777, 2002, 945, 944, 943, 1889, 5000])],
+        # words of 1..20 letters at every offset around the 976-byte wc chunk seams
+        # (and the 944/960-byte ones of earlier layouts / grep), 16-byte lanes and the
+        # 1 KiB windows, split lengths of every residue mod 4
+        "mixed_lengths": [mixed_words(n, seed) for seed, n in
+                          enumerate([12345, 7777, 2002, 945, 944, 943, 1889, 5000, 977, 976, 975, 1953, 2929, 961])],
         # > 64 distinct keys with one 8-byte prefix: the reduce's long tied run (sort
         # falls back to the k1 pass), plus prefix-of-another-key orderings
         "shared_prefix": [b" ".join(b"abcdefgh" + bytes([97 + i % 26, 97 + i // 26 % 26]) * (1 + i % 3)
