@@ -697,7 +697,7 @@ struct Ingest {
 };
 
 static int ingest_start(mrg_ctx* c, Ingest& g, const uint8_t* host, uint8_t* dev, uint64_t len) {
-    constexpr uint64_t kUnit = 58560;  // lcm(kWcChunkBytes, kGrepChunkBytes)
+    constexpr uint64_t kUnit = 29760;  // lcm(kWcChunkBytes, kGrepChunkBytes)
     static_assert(kUnit % kWcChunkBytes == 0 && kUnit % kGrepChunkBytes == 0, "piece unit");
     g.c = c;
     g.piece = std::max<uint64_t>(kUnit, c->ingest_piece / kUnit * kUnit);

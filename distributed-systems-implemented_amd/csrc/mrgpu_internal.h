@@ -162,11 +162,11 @@ struct LetterTables {
 void clear_tables(const Tables& t, bool short_table, hipStream_t s);
 // ---- wc pipeline (mrgpu_wc.hip) ----
 uint32_t wc_map_grid(uint64_t n, int grid);
-// Chunks [cbeg, cend) of the split (kOwn = 976 input bytes each; default: all);
+// Chunks [cbeg, cend) of the split (kOwn = 992 input bytes each; default: all);
 // resume: a previous launch of this map already ran over chunks < cbeg.
 bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, int grid, int mode,
                    hipStream_t s, uint64_t cbeg = 0, uint64_t cend = ~0ull, bool resume = false);
-constexpr uint64_t kWcChunkBytes = 976;   // input bytes a wc map chunk owns
+constexpr uint64_t kWcChunkBytes = 992;   // input bytes a wc map chunk owns
 constexpr uint64_t kGrepChunkBytes = 960; // input bytes a grep map chunk owns
 // emit: 0 = flush every bucket table into the HBM table (legacy),
 //       1 = emit records directly unless the bucket overflowed (then merge through HBM),

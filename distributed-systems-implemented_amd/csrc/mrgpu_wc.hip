@@ -36,14 +36,15 @@ constexpr int kBatchWords = kBatch * kWave;   // 192 words of a chunk per pass
 constexpr int kAggThreads = 512;
 
 // A chunk owns kOwn input bytes; its LDS slot is one 1 KiB DMA of the bytes
-// [start - 16, start + 1008): 16 bytes of look-back (lane 0), the 976 owned
-// bytes (lanes 1-61) and 32 bytes of look-ahead (lanes 62-63: a word starting in
-// lane 61 ends, or is known to exceed 16 bytes, within lane 62; lane 62's UTF-8
-// runes end within lane 63).  Neighbouring slots overlap by 48 bytes (re-read
-// from L2, not HBM).
+// [start - 16, start + 1008): 16 bytes of look-back (lane 0), the 992 owned
+// bytes (lanes 1-62) and 16 bytes of look-ahead (lane 63: a word starting in
+// lane 62 ends, or is known to exceed 16 bytes, within lane 63; a UTF-8 rune
+// starting in lane 63's last 3 bytes is completed from global memory on the
+// rare non-ASCII path).  Neighbouring slots overlap by 32 bytes (re-read from
+// L2, not HBM).
 constexpr int kSlotBytes = 1024;
-constexpr int kOwnLanes = 61;
-constexpr uint64_t kOwn = 16 * kOwnLanes;  // 976
+constexpr int kOwnLanes = 62;
+constexpr uint64_t kOwn = 16 * kOwnLanes;  // 992
 constexpr int kRing = 3;                    // LDS slots per wave: current, in flight, free (the word list)
 static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot");
 
@@ -70,6 +71,20 @@ static_assert(kSlotBytes == 1024 && kMaskLens * 16 <= 512, "kmask index fits 0x1
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBuckets>) <= 160 * 1024, "map LDS budget");
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBucketsLo>) <= 160 * 1024, "map LDS budget (256 buckets)");
 static_assert(sizeof(MapLdsT<12, kSpillBucketsHi>) <= 160 * 1024, "map LDS budget (high-cardinality)");
+
+// A slot's bytes with the 3 input bytes after it: utf8_letter_mask over lane 63
+// reads up to slot byte 1026 (a rune starting in the last 3 bytes).
+struct SlotTail {
+    const lds_u8* b;
+    uint32_t tail;  // input bytes [slot end, +3), zero at or past the split's end
+    __device__ uint32_t operator[](int q) const { return q < kSlotBytes ? (uint32_t)b[q] : (tail >> (8 * (q - kSlotBytes))) & 0xFFu; }
+};
+__device__ __forceinline__ uint32_t slot_tail(const uint8_t* in, uint64_t n, uint64_t p) {
+    uint32_t t = 0;
+    for (int i = 0; i < 3; i++)
+        if (p + i < n) t |= (uint32_t)in[p + i] << (8 * i);
+    return t;
+}
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
     return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
@@ -109,10 +124,10 @@ __device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
 }
 
 // ------------------------------------------------------------ wc map kernel
-// One wave per 976-byte chunk at a time, every wave independent.  The input is
+// One wave per 992-byte chunk at a time, every wave independent.  The input is
 // streamed into a private ring of three 1 KiB LDS slots with one
 // buffer_load_dwordx4...lds per chunk (lane l: bytes [start-16+16l, +16): lane 0
-// = look-back, lanes 1-61 = the 976 owned bytes, lanes 62-63 = look-ahead; the
+// = look-back, lanes 1-62 = the 992 owned bytes, lane 63 = look-ahead; the
 // descriptor's range check zero-fills before/after the split), issued two
 // chunks ahead.  gfx9 counts loads and stores on one in-order vmcnt, and hipcc
 // waits vmcnt(0) as soon as a loop's VMEM count is not static, so the loop's
@@ -267,8 +282,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         if constexpr ((mode & 1) != 0) {
             acc += buf[16 + lane];
         } else {
-            // lane l holds slot bytes [16l, 16l+16): lane 0 = look-back, lanes 1-61 the
-            // chunk's own 976 bytes, lanes 62-63 = look-ahead
+            // lane l holds slot bytes [16l, 16l+16): lane 0 = look-back, lanes 1-62 the
+            // chunk's own 992 bytes, lane 63 = look-ahead
             const uint4 ca = from_v4(b4[lane]);
             const uint32_t hi = (ca.x | ca.y | ca.z | ca.w) & 0x80808080u;
             const bool ascii = __ballot(hi != 0) == 0;
@@ -279,7 +294,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 utf8_chunks++;
                 if (lane == 0) mA = utf8_letter_mask<8>(buf, 8, lt) << 8;  // bytes 8-15 (rune starts need 3 back)
                 else if (lane < 63) mA = utf8_letter_mask<16>(buf, 16 * lane, lt);
-                else mA = 0;  // lane 63: never needed (lengths look one lane past lane 61)
+                else mA = utf8_letter_mask<16>(SlotTail{buf, slot_tail(in, n, cs - kBack + kSlotBytes)}, 16 * lane, lt);
                 wait_vmem_all();
             }
             // Word starts (a letter byte whose predecessor is not one) in the owned lanes
@@ -295,8 +310,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint32_t nl = ~(mA | (x1 << 16));
             // lanes 1..kOwnLanes as a constant lane mask (a compare result is
             // loop-invariant: hoisted, it was spilled to VGPR lanes and reloaded)
-            static_assert(kOwnLanes == 61, "owned-lane mask");
-            const bool owned = __builtin_amdgcn_inverse_ballot_w64(0x3FFFFFFFFFFFFFFEull);
+            static_assert(kOwnLanes == 62, "owned-lane mask");
+            const bool owned = __builtin_amdgcn_inverse_ballot_w64(0x7FFFFFFFFFFFFFFEull);
             uint32_t SA = owned ? (mA & ~((mA << 1) | ((pv >> 15) & 1u)) & 0xFFFFu) : 0u;
             const uint32_t nsa = __popc(SA);
             const uint32_t incl = wave_incl_scan_dpp(nsa);
@@ -313,7 +328,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             if constexpr ((mode & 2) != 0) {
                 acc += total;
             } else {
-                // passes of kBatchWords words: a 976-byte chunk of text has ~165; a chunk
+                // passes of kBatchWords words: a 992-byte chunk of text has ~170; a chunk
                 // with more words drains after each extra pass (its VMEM count differs)
                 const uint32_t passes = total == 0 ? 1u : (total + kBatchWords - 1) / kBatchWords;
                 for (uint32_t pass = 0; pass < passes; pass++) {

@@ -9,6 +9,20 @@ from mrgpu import corpus as C
 W16 = b"abcdefghijklmnop"  # exactly 16 letters (the inline-key limit)
 
 
+
+def utf8_slot_tail(rune):
+    """Words of 16 ASCII letters starting at the last owned byte of chunks 0..3 (992
+    bytes each), followed by `rune` (a letter, or U+00D7, a non-letter), so the rune
+    straddles the end of the chunk's 1 KiB window."""
+    r = rune.encode()
+    out = bytearray()
+    for c in range(4):
+        start = 992 * c + 991 - (len(r) - 2 if len(r) > 2 else 0)
+        out += b"ab " * ((start - len(out)) // 3)
+        out += b" " * (start - len(out))
+        out += b"q" * 16 + r + b"z " + b"tail words "
+    return bytes(out)
+
 def edge_cases() -> dict[str, list[bytes]]:
     """name -> list of files (each file = one map split)."""
     big_word = b"Z" * 5000
@@ -31,16 +45,22 @@ def edge_cases() -> dict[str, list[bytes]]:
         "utf8_mix": [utf8_mix],
         "invalid_utf8": [b"ab\xffcd\xc0\xafef\xe2\x82gh\xed\xa0\x80ij\xf4\x90\x80\x80kl\xc3mn\x80op\xce\xbb\xce"],
         "truncated_at_eof": [b"word \xe2\x82", b"x\xf0\x9f\x98"],
+        # a word starting in the last owned lane of a 992-byte wc chunk whose 17th
+        # byte begins a multi-byte letter ending past the 1 KiB window (slot byte 1024
+        # = input byte chunk start + 1008): only the input bytes after the window tell
+        # that the word is longer than 16 bytes
+        "utf8_slot_tail": [utf8_slot_tail(rune) for rune in ("\u00e9", "\u4e2d", "\U00010400", "\u00d7")],
         "multi_file": [b"one two three\n", b"two three\n", b"three"],
         "apostrophes": [b"don't can't won't it's O'Neil rock'n'roll"],
         # splits whose last bytes are a word, for every n % 4 (the map streams the
         # split with range-checked 16-byte loads and patches its last n % 4 bytes)
         "tail_bytes": [b"a", b"ab", b"abc", b"abcd", b"abcde", b"xy z", b"q r st", b"  uvw"],
-        # words of 1..20 letters at every offset around the 976-byte wc chunk seams
-        # (and the 944/960-byte ones of earlier layouts / grep), 16-byte lanes and the
+        # words of 1..20 letters at every offset around the 992-byte wc chunk seams
+        # (and the 944/976/960-byte ones of earlier layouts / grep), 16-byte lanes and the
         # 1 KiB windows, split lengths of every residue mod 4
         "mixed_lengths": [mixed_words(n, seed) for seed, n in
-                          enumerate([12345, 7777, 2002, 945, 944, 943, 1889, 5000, 977, 976, 975, 1953, 2929, 961])],
+                          enumerate([12345, 7777, 2002, 945, 944, 943, 1889, 5000, 977, 976, 975, 1953, 2929, 961,
+                                     993, 992, 991, 1985, 2977])],
         # > 64 distinct keys with one 8-byte prefix: the reduce's long tied run (sort
         # falls back to the k1 pass), plus prefix-of-another-key orderings
         "shared_prefix": [b" ".join(b"abcdefgh" + bytes([97 + i % 26, 97 + i // 26 % 26]) * (1 + i % 3)
