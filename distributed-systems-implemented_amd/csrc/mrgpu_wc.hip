@@ -56,7 +56,7 @@ static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot"
 // The mask table sits at LDS offset 0 (its address is (entry >> 6) & 0x1F0, no
 // base); the dictionary's set offsets are then constant-displaced, which the
 // ds_read offset field absorbs.
-constexpr int kMaskLens = 18;  // kmask[len], len = 0..17 (17 = "more than 16 bytes", never used as a key)
+constexpr int kMaskLens = 32;  // kmask[len], len = 0..31 (> 16 = "more than 16 bytes", never used as a key)
 template <int NW, int NB>
 struct alignas(16) MapLdsT {
     uint4 kmask[kMaskLens];                     // kmask[len]: the first min(len, 16) of 16 key bytes
@@ -84,6 +84,14 @@ __device__ __forceinline__ uint32_t slot_tail(const uint8_t* in, uint64_t n, uin
     for (int i = 0; i < 3; i++)
         if (p + i < n) t |= (uint32_t)in[p + i] << (8 * i);
     return t;
+}
+
+// v_ffbl_b32 as the hardware defines it: index of the lowest set bit, 0xFFFFFFFF for 0
+// (__builtin_ctz(0) is undefined and the defined variants add a compare and select)
+__device__ __forceinline__ uint32_t ffbl_raw(uint32_t x) {
+    uint32_t r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
 }
 
 __device__ __forceinline__ uint32_t lds_addr(const void* p) {
@@ -298,15 +306,17 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 wait_vmem_all();
             }
             // Word starts (a letter byte whose predecessor is not one) in the owned lanes
-            // and lengths (ctz over this lane's mask and the next two lanes'), packed into
-            // the list as slot position | min(len, 31) << 10.  Neighbour masks by DPP.
+            // and lengths (ctz over this lane's mask and the next lane's), packed into the
+            // list as slot position | len << 10 (a u16: len > 16 means a long word; no
+            // terminator in the window gives ctz = -1, i.e. 63 in the u16's top bits and
+            // 31 in the 5-bit mask-table index).  Neighbour masks by DPP.
             const uint32_t x1 = wave_shl1_z(mA);
             const uint32_t pv = wave_shr1_z(mA);
             // Non-letters of this lane's 16 bytes and the next lane's.  A word starts at
             // bit <= 15, so one of <= 16 bytes ends by bit 31; the length is the
-            // distance to the next non-letter, capped at 17 by a forced bit (17 = more
-            // than 16 bytes: a word without a terminator in the window has more than
-            // 16, and 17 indexes the mask table directly, no clamp).
+            // distance to the next non-letter (v_ffbl: -1 when there is none, a word of
+            // more than 16 bytes; the mask table has 32 entries, so any length indexes
+            // it without a clamp).
             const uint32_t nl = ~(mA | (x1 << 16));
             // lanes 1..kOwnLanes as a constant lane mask (a compare result is
             // loop-invariant: hoisted, it was spilled to VGPR lanes and reloaded)
@@ -320,7 +330,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint32_t pos0 = 16 * lane;
             while (SA) {
                 const uint32_t bit = __builtin_ctz(SA);
-                const uint32_t len = __builtin_ctz((nl >> bit) | (1u << 17));
+                const uint32_t len = ffbl_raw(nl >> bit);  // -1 when no terminator in the window
                 list[j++] = (uint16_t)((pos0 + bit) | (len << 10));
                 SA &= SA - 1;
             }
@@ -354,7 +364,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     for (int u = 0; u < kBatch; u++) {
                         const lds_u32* p4 = (const lds_u32*)(uintptr_t)(bufa + (e[u] & 0x3FCu));
                         g0[u] = p4[0]; g1[u] = p4[1]; g2[u] = p4[2]; g3[u] = p4[3]; g4[u] = p4[4];
-                        km[u] = kmask4[__builtin_amdgcn_ubfe(e[u], 10, 5)];  // len <= 17 (the tokenizer's cap)
+                        km[u] = kmask4[__builtin_amdgcn_ubfe(e[u], 10, 5)];  // 32 entries: any 5-bit length
                     }
                     uint64_t k0[kBatch], k1[kBatch];
                     uint32_t hh[kBatch];
