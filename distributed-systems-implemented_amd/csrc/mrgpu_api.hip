@@ -148,6 +148,8 @@ struct mrg_ctx {
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
+    DevBuf spool_alt;     // diagnostic option spill_alt_pools: a second spill pool, the two alternate per split
+    int spill_alt = 0;
     DevBuf bflag, dict, dict_cnt, sample, recbuf, recarena, sortbuf, dbg;
     DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
@@ -764,6 +766,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
     int rc;
     c->lo_log2_cur = c->lo_log2;
     c->spill_nb = c->spill_buckets_opt ? (uint32_t)c->spill_buckets_opt : c->next_nb;
+    if (c->spill_alt) std::swap(c->spool.p, c->spool_alt.p), std::swap(c->spool.cap, c->spool_alt.cap);
     Ingest ing;
     if (host && (rc = ingest_start(c, ing, host, (uint8_t*)in, len))) return rc;
     if ((rc = ensure_spill(c, len))) return rc;
@@ -1047,7 +1050,7 @@ void mrg_close(mrg_ctx* c) {
     hipSetDevice(c->device);
     if (c->s) hipStreamSynchronize(c->s);
     if (c->comm) ncclCommDestroy(c->comm);
-    DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spmeta,
+    DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spool_alt, &c->spmeta,
                     &c->bflag, &c->dict, &c->dict_cnt, &c->sample, &c->recbuf, &c->recarena, &c->sortbuf,
                     &c->segmeta, &c->seg8[0], &c->seg8[1], &c->seg16[0], &c->seg16[1]};
     for (DevBuf* b : bs) b->release();
@@ -1078,6 +1081,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "map_mode")) c->map_mode = (int)v;
     else if (!strcmp(name, "spill_stream_keys")) c->spill_force_sub = v > 0 ? v : 0;
     else if (!strcmp(name, "spill_mid_div")) c->spill_mid_div = v > 0 ? (int)v : 2;
+    else if (!strcmp(name, "spill_alt_pools")) c->spill_alt = v > 0;  // diagnostic: two pools, alternating per split
     else if (!strcmp(name, "agg_rounds")) c->agg_rounds = v > 0 ? (int)v : 8;
     else if (!strcmp(name, "agg_big_later")) c->agg_big_later = v >= 0;  // -1: off
     else if (!strcmp(name, "agg_big0")) c->agg_big0 = v > 0 ? 1 : v < 0 ? -1 : 0;  // 0: by layout

@@ -1540,15 +1540,26 @@ __global__ void dict_cands_kernel(Recs r, const uint32_t* order, uint64_t lim, u
 
 // One workgroup places the candidates in order, 1024 at a time, each into the
 // first of its two sets with a free way; a key whose two sets are full stays out
-// (it is then counted through the spill path).
+// (it is then counted through the spill path).  Within a batch the 1024
+// placements race, so which keys lose out varied from run to run; when one of the
+// few hundred hottest lost (~3e5 words of C2), its bucket's aggregator workgroup
+// ended last and the whole aggregation took ~1.25 instead of ~1.02 ms in that
+// process (the kept dictionary made it last for the process).  So the kDictHot
+// hottest candidates get a fix-up pass in rank order: one that lost takes the
+// way of the coldest key in its two sets when that key is colder.
+constexpr uint32_t kDictHot = 1024;
 __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uint64_t lim, uint4* dict) {
     __shared__ uint4 S[kDictSets];
     __shared__ uint32_t fill[kDictSets];
+    __shared__ uint32_t rk[kDictSets][2];    // candidate index (rank) of the key in each way, ~0u = empty
+    __shared__ uint32_t hot[kDictHot / 32];  // placed bits of the kDictHot hottest candidates
     const uint32_t tid = threadIdx.x;
     for (uint32_t i = tid; i < (uint32_t)kDictSets; i += 1024) {
         S[i] = make_uint4(0, 0, 0, 0);
         fill[i] = 0;
+        rk[i][0] = rk[i][1] = ~0u;
     }
+    if (tid < kDictHot / 32) hot[tid] = 0;
     __syncthreads();
     uint4 nx = tid < lim ? cand[tid] : make_uint4(0, 0, 0, 0);
     for (uint64_t base = 0; base < lim; base += 1024) {
@@ -1567,10 +1578,54 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uin
                 if (mid) S[s] = c;
                 else if (w == 0) { S[s].x = c.x; S[s].y = c.y; }
                 else { S[s].z = c.x; S[s].w = c.y; }
+                const uint32_t i = (uint32_t)(base + tid);
+                rk[s][w] = i;
+                if (i < kDictHot) atomicOr(&hot[i >> 5], 1u << (i & 31));
             }
         }
         __syncthreads();
     }
+    // Fix-up, wave 0, lowest rank first (an evicted key is colder than its evictor,
+    // so it is met again later in this pass if it is one of the kDictHot).
+    if (tid < kWave) {
+        const uint32_t nh = (uint32_t)(lim < kDictHot ? lim : kDictHot);
+        for (uint32_t g = 0; g < nh; g += kWave) {
+            const uint32_t i = g + tid;
+            const uint4 c = i < nh ? cand[i] : make_uint4(0, 0, 0, 0);
+            bool tried = false;  // this lane's candidate already had its fix-up
+            for (;;) {
+                const bool want = i < nh && (c.x | c.y) != 0 && !tried && !((hot[i >> 5] >> (i & 31)) & 1u);
+                const uint64_t m = __ballot(want);
+                if (m == 0) break;
+                if (tid == (uint32_t)__builtin_ctzll(m)) {
+                    tried = true;
+                    const bool mid = (c.z | c.w) != 0;
+                    uint32_t s1, s2;
+                    dict_sets(fold32(c.x, c.y, c.z, c.w), mid, s1, s2);
+                    const uint32_t ways = mid ? 1u : 2u;
+                    uint32_t bs = s1, bw = 0, br = rk[s1][0];  // the coldest way of the two sets
+                    for (uint32_t k = 0; k < 2 * ways; k++) {
+                        const uint32_t ss = k < ways ? s1 : s2, ww = k < ways ? k : k - ways;
+                        const uint32_t r = rk[ss][ww];
+                        if (r > br || (r == br && k == 0)) { bs = ss; bw = ww; br = r; }
+                    }
+                    if (br > i) {  // colder (or empty): this candidate takes the way
+                        if (br < kDictHot) atomicAnd(&hot[br >> 5], ~(1u << (br & 31)));
+                        if (mid) S[bs] = c;
+                        else if (bw == 0) { S[bs].x = c.x; S[bs].y = c.y; }
+                        else { S[bs].z = c.x; S[bs].w = c.y; }
+                        rk[bs][bw] = i;
+                        atomicOr(&hot[i >> 5], 1u << (i & 31));
+                    }
+                }
+                // the next ballot reads what this lane wrote
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+            }
+        }
+    }
+    __syncthreads();
     for (uint32_t i = tid; i < (uint32_t)kDictSets; i += 1024) dict[i] = S[i];
 }
 
