@@ -1542,12 +1542,12 @@ __global__ void dict_cands_kernel(Recs r, const uint32_t* order, uint64_t lim, u
 // first of its two sets with a free way; a key whose two sets are full stays out
 // (it is then counted through the spill path).  Within a batch the 1024
 // placements race, so which keys lose out varied from run to run; when one of the
-// few hundred hottest lost (~3e5 words of C2), its bucket's aggregator workgroup
+// few thousand hottest lost (~3e5 words of C2), its bucket's aggregator workgroup
 // ended last and the whole aggregation took ~1.25 instead of ~1.02 ms in that
 // process (the kept dictionary made it last for the process).  So the kDictHot
 // hottest candidates get a fix-up pass in rank order: one that lost takes the
 // way of the coldest key in its two sets when that key is colder.
-constexpr uint32_t kDictHot = 1024;
+constexpr uint32_t kDictHot = 4096;
 __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uint64_t lim, uint4* dict) {
     __shared__ uint4 S[kDictSets];
     __shared__ uint32_t fill[kDictSets];
