@@ -12,6 +12,8 @@ workload (configs[1] = SURVEY.md §8d C2): 10 GB synthetic Zipf(s=1.07, V=1e6)
          bytes x steps / max-over-ranks time.
 
 Other §8d workloads (evidence runs; the default is C2):
+  --workload c2u wc on 10 GB of mixed ASCII/UTF-8 Zipf text (north_star's mixed corpus: the
+                 tokenizer's non-ASCII path), nReduce = 10
   --workload c3  grep "distributed" over 10 GB of valid mixed ASCII/UTF-8 lines
   --workload c4  wc, 12.5 GB per GPU, nReduce = 64 (the 8-GPU 100 GB config)
   --workload c5  wc, 25 GB per GPU, Zipf(s=0.8, V=1e7) with every vocabulary word
@@ -51,6 +53,9 @@ GREP_METRIC = "grep input GB/s (map+shuffle+reduce) at 1/2/4/8 MI355X; % HBM roo
 WORKLOADS = {
     "c2": dict(app="wc", kind=C.KIND_ASCII, s=1.07, V=10**6, seed=2, files=40, file_mb=250, nreduce=10,
                desc="C2: wc, Zipf s=1.07 over 1e6 ASCII words"),
+    "c2u": dict(app="wc", kind=C.KIND_UTF8, s=1.07, V=10**6, seed=6, files=40, file_mb=250, nreduce=10,
+                desc="C2u: wc, Zipf s=1.07 over 1e6 mixed-script words (~30 % non-ASCII: Greek, Cyrillic, CJK, "
+                     "Deseret, CJK ext. B), valid UTF-8"),
     "c3": dict(app="grep", kind=C.KIND_UTF8, s=1.07, V=10**6, seed=3, files=40, file_mb=250, nreduce=10,
                desc="C3: grep 'distributed' (0.5 % of lines, 20 % of those repeated), valid UTF-8, "
                     "~30 % non-ASCII words, lines 40-120 B"),
@@ -214,6 +219,195 @@ def cpu_baseline(w: dict, sample_files: int, sample_mb: int, seq_files: int, nre
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def _oracle():
+    """The C oracle (tests/_oracle.py -> oracle/_build/liboracle.so): the checker
+    of the full-size output, used outside the timed region only."""
+    tdir = os.path.join(ROOT, "tests")
+    if tdir not in sys.path:
+        sys.path.insert(0, tdir)
+    import _oracle as O
+    return O
+
+
+def oracle_exact_check(w: dict, host: np.ndarray, gpu_parts: list[bytes], nreduce: int, rank: int, world: int) -> dict:
+    """Byte equality of every mr-out-r of the full-size job with the C oracle's
+    (oracle/mrcount.c: the reference's wc / grep job restated, counted by host
+    threads over the same split; main/mrsequential.go:59-84, mrapps/wc.go:21-34,
+    mrapps/dgrep.go:18-46).  N > 1: every rank counts its own split, the
+    partitions travel to their owners (r % N) over gloo and are merged there
+    (the reduce over all splits' intermediates, worker.go:123-146), and each
+    owner compares its partitions; non-owned partitions must be empty."""
+    O = _oracle()
+    app = "wc" if w["app"] == "wc" else "grep:" + PATTERN.decode()
+    threads = min(16, os.cpu_count() or 1)
+    t0 = time.time()
+    mine = O.c_count_mt(app, host, nreduce, threads)
+    if world > 1:
+        from mrgpu import dist as D
+        send = []
+        for o in range(world):
+            blob = b"".join(len(mine[r]).to_bytes(8, "little") + mine[r] if r % world == o else (0).to_bytes(8, "little")
+                            for r in range(nreduce))
+            send.append(blob)
+        recv = D.alltoallv_bytes(send)
+        outs = []
+        for b in recv:
+            parts, off = [], 0
+            for r in range(nreduce):
+                n = int.from_bytes(b[off:off + 8], "little")
+                parts.append(b[off + 8:off + 8 + n])
+                off += 8 + n
+            outs.append(parts)
+        want = O.c_merge_parts(app, outs)
+    else:
+        want = mine
+    ok = all(gpu_parts[r] == (want[r] if r % world == rank else b"") for r in range(nreduce))
+    bad = [r for r in range(nreduce) if gpu_parts[r] != (want[r] if r % world == rank else b"")]
+    res = {"exact_vs_oracle": ok, "oracle_s": round(time.time() - t0, 1), "oracle_threads": threads,
+           "oracle_output_bytes": sum(len(want[r]) for r in range(nreduce) if r % world == rank)}
+    if bad:
+        res["mismatched_partitions"] = bad[:16]
+    if world > 1:
+        t = torch.tensor([0 if ok else 1], dtype=torch.int64)
+        dist.all_reduce(t)
+        res["exact_vs_oracle"] = int(t.item()) == 0
+        res["exact_vs_oracle_rank_failures"] = int(t.item())
+    return res
+
+
+def upload(host: np.ndarray, local: int):
+    """The split, resident in HBM before the timed region (a torch tensor: the
+    independent word count reads it with plain torch ops)."""
+    nbytes = int(host.size)
+    dev = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{local}")
+    step = 1 << 30
+    for off in range(0, nbytes, step):
+        n = min(step, nbytes - off)
+        dev[off:off + n].copy_(torch.from_numpy(host[off:off + n]))
+    torch.cuda.synchronize()
+    return dev
+
+
+def timed_steps(ctx: Context, run_step, steps: int, warmup: int, world: int):
+    """W untimed warmup steps (the first one's wall time is reported as the cold
+    split: fresh dictionary, first allocations), then exactly K steps between a
+    barrier + synchronize on both sides; returns (max-over-ranks seconds, per-step stats, cold ms)."""
+    cold_ms, cold_st = None, None
+    for i in range(warmup):
+        ctx.sync()
+        t0 = time.perf_counter()
+        run_step()
+        ctx.sync()
+        if i == 0:
+            cold_ms = (time.perf_counter() - t0) * 1e3
+            cold_st = ctx.stats()
+    stats = []
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ctx.sync()
+    t_start = time.perf_counter()
+    for _ in range(steps):
+        run_step()
+        stats.append(ctx.stats())
+    ctx.sync()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    t_max = elapsed
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+    return t_max, stats, cold_ms, cold_st
+
+
+def no_shuffle_time(ctx: Context, run_step, steps: int, shared: bool) -> float:
+    """T(1) of the weak-scaling efficiency: the same per-GPU splits with no
+    shuffle (every partition reduced locally), in this process; max over ranks."""
+    ctx.set_option("skip_exchange", 1)
+    dist.barrier()
+    ctx.sync()
+    t1 = time.perf_counter()
+    for _ in range(steps):
+        run_step()
+    ctx.sync()
+    t1 = time.perf_counter() - t1
+    dist.barrier()
+    ctx.set_option("skip_exchange", 1 if shared else 0)
+    v = torch.tensor([t1], dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    return float(v.item())
+
+
+def multi_fields(stats: list[dict], t_max: float, t1: float, world: int, shared: bool, ndev: int) -> dict:
+    ex_ms = sum(st["exchange_ms"] for st in stats) / len(stats)
+    snd = sum(st["shuffle_send_bytes"] for st in stats) / len(stats)
+    v = torch.tensor([ex_ms, snd], dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.MAX)
+    ex_max, snd_max = float(v[0]), float(v[1])
+    links = min(world - 1, 7)
+    per_gpu_bw = snd / (ex_ms / 1e3) / 1e9 if ex_ms > 0 else 0.0
+    m = {"exchange_ms": round(ex_max, 3), "shuffle_bytes_per_gpu": int(snd_max),
+         "xgmi_achieved_GBps": round(per_gpu_bw, 2), "xgmi_peak_GBps": links * XGMI_LINK_GBS,
+         "xgmi_frac": round(per_gpu_bw / (links * XGMI_LINK_GBS), 4),
+         "t1_ms_per_step": round(t1 / len(stats) * 1e3, 3), "tP_ms_per_step": round(t_max / len(stats) * 1e3, 3),
+         "weak_scaling_efficiency": round(t1 / t_max, 4)}
+    if shared:
+        m["rehearsal"] = f"{world} ranks shared {ndev} device(s): no RCCL exchange ran (not a measurement)"
+    return m
+
+
+def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: bool, ndev: int) -> dict:
+    """SURVEY.md §8(d) defines E(P) on C5 (25 GB per GPU, 1e7 distinct keys,
+    R = 64): the same timed-step / T(1) measurement on that workload, in this
+    run, after the headline workload's buffers are released."""
+    w = WORKLOADS[wname]
+    t0 = time.time()
+    host = gen_corpus(w, rank, w["file_mb"], w["files"])
+    nbytes = int(host.size)
+    log(f"[{wname}] generated {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
+    dev = upload(host, local)
+    del host
+    ctx = Context(local)
+    for o in args.opt:
+        k, v = o.split("=")
+        ctx.set_option(k, int(v))
+    if not shared:
+        obj = [Context.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        ctx.comm_init(obj[0], world, rank)
+    else:
+        ctx.set_option("skip_exchange", 1)
+    dptr = dev.data_ptr()
+
+    def run_step():
+        return ctx.run_job(MRG_APP_WC, device_ptr=dptr, nbytes=nbytes, nreduce=w["nreduce"], copy_out=False)
+
+    steps = max(1, args.scaling_steps)
+    t_max, stats, _, _ = timed_steps(ctx, run_step, steps, 1, world)
+    p, n, offs = run_step()
+    import ctypes
+    out = ctypes.string_at(p, n) if n else b""
+    parts = [out[offs[i]:offs[i + 1]] for i in range(w["nreduce"])]
+    chk = check_output(parts, w["nreduce"], "wc")
+    owned_ok = all(not parts[r] for r in range(w["nreduce"]) if r % world != rank) or shared
+    tw = torch.tensor([chk["total_words"]], dtype=torch.int64)
+    dist.all_reduce(tw)
+    t1 = no_shuffle_time(ctx, run_step, steps, shared)
+    res = {"workload": f"{w['desc']}; {nbytes / 1e9:.2f} GB per GPU", "nreduce": w["nreduce"],
+           "value": round(nbytes * world * steps / t_max / 1e9, 3), "unit": "GB/s", "steps": steps,
+           "ms_per_step": round(t_max / steps * 1e3, 3),
+           **multi_fields(stats, t_max, t1, world, shared, ndev),
+           "checks": {"sorted_unique": chk["sorted_unique"], "partition_ok": chk["partition_ok"],
+                      "non_owned_empty": owned_ok, "total_words": int(tw.item())}}
+    ctx.close()
+    del dev
+    torch.cuda.empty_cache()
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -228,6 +422,11 @@ def main():
     ap.add_argument("--cpu-seq-files", type=int, default=2, help="files of the sample the single-process mrseq times")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive (host-input) job")
+    ap.add_argument("--no-oracle", action="store_true", help="skip the full-size exact check against the C oracle")
+    ap.add_argument("--scaling-workload", default="c5", help="N > 1: workload of the E(P) sub-run ('none' to skip)")
+    ap.add_argument("--scaling-steps", type=int, default=2)
+    ap.add_argument("--rehearsal", action="store_true",
+                    help="allow more ranks than visible GPUs (ranks share devices, no RCCL exchange: not a measurement)")
     ap.add_argument("--opt", action="append", default=[], help="library option name=value (experiments; repeatable)")
     args = ap.parse_args()
     w = WORKLOADS[args.workload]
@@ -242,11 +441,17 @@ def main():
     if world != args.gpus:
         log(f"--gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     if world > 1:
-        dist.init_process_group("gloo")  # control plane only; the shuffle is RCCL inside libmrgpu
-    # one GPU per rank; ranks beyond the visible devices share them (a rehearsal of
-    # the N > 1 path on a smaller box — the driver's N-GPU runs have one each)
+        import datetime
+        # control plane only (the shuffle is RCCL inside libmrgpu); a lost rank
+        # ends the job in minutes rather than gloo's default half hour
+        dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
+    # one GPU per rank; more ranks than devices only as an explicit rehearsal of
+    # the N > 1 path on a smaller box (the driver's N-GPU runs have one each)
     ndev = max(1, torch.cuda.device_count())
     shared = world > ndev  # rehearsal: RCCL refuses two ranks on one device, so no exchange
+    if shared and not args.rehearsal:
+        log(f"{world} ranks but {ndev} visible GPU(s): refusing (pass --rehearsal to run without the RCCL exchange)")
+        sys.exit(2)
     local = local % ndev
     torch.cuda.set_device(local)
     # torch initializes its CUDA runtime lazily on first use; do it now, so it can
@@ -270,14 +475,7 @@ def main():
     if shared:
         log(f"{world} ranks on {ndev} device(s): rehearsal without the RCCL exchange")
         ctx.set_option("skip_exchange", 1)
-    # the split, resident in HBM before the timed region (a torch tensor: the
-    # independent word count below reads it with plain torch ops)
-    dev = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{local}")
-    step = 1 << 30
-    for off in range(0, nbytes, step):
-        n = min(step, nbytes - off)
-        dev[off:off + n].copy_(torch.from_numpy(host[off:off + n]))
-    torch.cuda.synchronize()
+    dev = upload(host, local)
     dptr = dev.data_ptr()
     ctx.sync()
 
@@ -287,36 +485,12 @@ def main():
                                copy_out=False)
         return ctx.run_job(MRG_APP_WC, device_ptr=dptr, nbytes=nbytes, nreduce=args.nreduce, copy_out=False)
 
-    for _ in range(args.warmup):
-        run_step()
-
-    digests, kern_ms, stats = [], [], []
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    ctx.sync()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        p, n, offs = run_step()
-        st = ctx.stats()
-        kern_ms.append(st["map_kernel_ms"])
-        stats.append(st)
-        digests.append((p, n))
-    ctx.sync()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    t_max, stats, cold_ms, cold_st = timed_steps(ctx, run_step, args.steps, args.warmup, world)
+    kern_ms = [st["map_kernel_ms"] for st in stats]
     log("map kernel ms per timed step: " + " ".join(f"{k:.2f}" for k in kern_ms))
     log("aggregation ms per timed step: " + " ".join(f"{st['agg_ms']:.2f}" for st in stats))
 
-    t_max = elapsed
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        t_max = float(t.item())
-
-    # output of the last step (context-owned buffer) -> properties at full size
+    # output of one more step (context-owned buffer) -> checks at full size, outside the timed region
     import ctypes
     p, n, offs = run_step()
     out = ctypes.string_at(p, n) if n else b""
@@ -339,39 +513,21 @@ def main():
             dist.all_reduce(ti)
             checks["total_words_independent"] = int(ti.item())
             checks["total_words_match"] = checks["total_words_independent"] == checks[key]
+    if not args.no_oracle and not shared:
+        checks.update(oracle_exact_check(w, host, parts, args.nreduce, rank, world))
+    del out, parts
 
     # N > 1: the shuffle's share and the weak-scaling efficiency against the
     # same ranks running their splits with no shuffle (T(1) of the same per-GPU
     # work, measured in this process, every partition reduced locally)
     multi = None
     if world > 1:
-        ex_ms = sum(st["exchange_ms"] for st in stats) / len(stats)
-        snd = sum(st["shuffle_send_bytes"] for st in stats) / len(stats)
-        ctx.set_option("skip_exchange", 1)
-        dist.barrier()
-        ctx.sync()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            run_step()
-        ctx.sync()
-        t1 = time.perf_counter() - t1
-        dist.barrier()
-        ctx.set_option("skip_exchange", 1 if shared else 0)
-        v = torch.tensor([ex_ms, snd, t1], dtype=torch.float64)
-        vmax = v.clone()
-        dist.all_reduce(vmax, op=dist.ReduceOp.MAX)
-        links = min(world - 1, 7)
-        per_gpu_bw = snd / (ex_ms / 1e3) / 1e9 if ex_ms > 0 else 0.0
-        multi = {"exchange_ms": round(float(vmax[0]), 3), "shuffle_bytes_per_gpu": int(snd),
-                 "xgmi_achieved_GBps": round(per_gpu_bw, 2), "xgmi_peak_GBps": links * XGMI_LINK_GBS,
-                 "xgmi_frac": round(per_gpu_bw / (links * XGMI_LINK_GBS), 4),
-                 "t1_ms_per_step": round(float(vmax[2]) / args.steps * 1e3, 3),
-                 "weak_scaling_efficiency": round(float(vmax[2]) / t_max, 4),
-                 "note": "shuffle bytes = wire bytes a rank sends to the other ranks (max over ranks of the mean over timed "
-                         "steps); xgmi_frac = those bytes / exchange time / (min(P-1,7) x 153 GB/s); "
-                         "E(P) = T(1) / T(P), T(1) = the same per-GPU splits run with no shuffle in this process"}
-        if shared:
-            multi["rehearsal"] = f"{world} ranks shared {ndev} device(s): no RCCL exchange ran (not a measurement)"
+        t1 = no_shuffle_time(ctx, run_step, args.steps, shared)
+        multi = multi_fields(stats, t_max, t1, world, shared, ndev)
+        multi["note"] = ("shuffle bytes = wire bytes a rank sends to the other ranks (max over ranks of the mean over "
+                         "timed steps; 24-byte wire records + long-key bytes); xgmi_frac = those bytes / exchange time / "
+                         "(min(P-1,7) x 153 GB/s); E(P) = T(1) / T(P), T(1) = the same per-GPU splits run with no "
+                         "shuffle in this process")
 
     total_bytes = nbytes * world * args.steps
     value = total_bytes / t_max / 1e9
@@ -379,19 +535,22 @@ def main():
     achieved = nbytes / (avg_kern / 1e3) / 1e9
     last = stats[-1]
 
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "traffic_r02.json")
+    traffic, traffic_src = None, None
+    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.workload}.json")
     if os.path.exists(tpath):
         try:
             tj = json.load(open(tpath))
             if tj.get("input_bytes") == nbytes and tj.get("workload", "c2") == args.workload:
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_src = (f"profiled, not this run: {os.path.relpath(tpath, ROOT)} (rocprofv3 --pmc FETCH_SIZE / "
+                               f"WRITE_SIZE passes over the same launch, {tj.get('round', '?')})")
         except Exception:
             traffic = None
 
     # PCIe-inclusive rate (never `value`): one whole job with the split in pageable
     # host memory, so the H2D copy is inside the job (mrg_run_job, MRG_INPUT_HOST)
     pcie = None
+    step = 1 << 30
     if world == 1 and not args.no_pcie:
         ctx.sync()
         t0 = time.perf_counter()  # the copy alone (pageable host -> HBM), for comparison
@@ -417,6 +576,13 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(w, args.cpu_sample_files, args.cpu_sample_mb, args.cpu_seq_files, args.nreduce, ctx)
 
+    ctx.close()
+    del dev, host
+    torch.cuda.empty_cache()
+    scaling = None
+    if world > 1 and args.scaling_workload not in ("", "none") and args.scaling_workload != args.workload:
+        scaling = scaling_subrun(args.scaling_workload, args, rank, world, local, shared, ndev)
+
     if rank == 0:
         line = {
             "metric": GREP_METRIC if grep else METRIC,
@@ -435,10 +601,11 @@ def main():
                                    f"{args.file_mb} MB), device-resident input",
                        "nreduce": args.nreduce, "input_bytes_per_gpu": nbytes, "parallelism": f"dp{world}", **({"options": args.opt} if args.opt else {}),
                        "shuffle": "RCCL all-to-all" if world > 1 else "none (single GPU)"},
+            **({"rehearsal": True} if shared else {}),
             "roofline": {"bound": "hbm", "kernel": "grep_map_kernel" if grep else "wc_map_kernel",
                          "achieved": round(achieved, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                         "traffic": traffic,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "frac_of_measured_copy": round(achieved / HBM_COPY_GBS, 4),
                          "map_kernel_ms_median": round(sorted(kern_ms)[len(kern_ms) // 2], 3),
                          "note": "achieved = input bytes per launch / mean HIP-event duration of the map kernel "
@@ -448,6 +615,12 @@ def main():
                           "dict": round(last["dict_ms"], 3), "agg": round(last["agg_ms"], 3),
                           "exchange": round(last["exchange_ms"], 3), "reduce": round(last["reduce_ms"], 3),
                           "d2h": round(last["d2h_ms"], 3)},
+            "cold_split": {"ms": round(cold_ms, 3) if cold_ms is not None else None,
+                           "dict_ms": round(cold_st["dict_ms"], 3) if cold_st else None,
+                           "map_kernel_ms": round(cold_st["map_kernel_ms"], 3) if cold_st else None,
+                           "note": "the first warmup step: a fresh context (dictionary built from the split's "
+                                   "sample, first allocations); the timed steps re-map the same split with the "
+                                   "context's dictionary and buffers kept, as a worker's later map tasks do"},
             "staged_input_bytes": int(last["staged_bytes"]),
             "distinct_keys": int(last["distinct_keys"]),
             "dict_hit_words": int(last["dict_hits"]),
@@ -460,11 +633,10 @@ def main():
             "checks": checks,
             "pcie_inclusive": pcie,
             "multi_gpu": multi,
+            "multi_gpu_scaling_workload": scaling,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    del dev
-    ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

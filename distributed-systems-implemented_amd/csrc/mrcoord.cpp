@@ -31,6 +31,15 @@
 // files skipped, worker.go:102-108), merges, formats mr-out-r (temp + rename)
 // and removes its inputs (worker.go:150-154).  The GPU is initialised only in
 // the worker processes (the coordinator never touches it, so forking is safe).
+//
+// Duplicate tasks (a slow worker and its re-issued replacement) are safe here,
+// unlike in the reference: temp files are unique (mkstemp); every map task
+// writes all nReduce mr-X-r, so a reduce task that finds one missing (or sees
+// it vanish mid-read) abandons the task without writing mr-out-r; and a reduce
+// worker removes its inputs only when the coordinator accepted its completion
+// as the first (the reply's CReduce field is 1), so a late duplicate never reads
+// a half-deleted input set.  A duplicate that read every input writes the same
+// mr-out-r bytes, so its rename is harmless.
 #include <errno.h>
 #include <poll.h>
 #include <signal.h>
@@ -140,16 +149,19 @@ struct Coordinator {
         r.fname_len = (uint32_t)fname->size();
         return r;
     }
-    // coordinator.go:27-41, counted once per task
-    void map_complete(int64_t x) {
-        if (x < 0 || x >= nmap || map_log[x] == 2) return;
+    // coordinator.go:27-41, counted once per task; true if this completion is
+    // the first (accepted)
+    bool map_complete(int64_t x) {
+        if (x < 0 || x >= nmap || map_log[x] == 2) return false;
         map_log[x] = 2;
         cmap++;
+        return true;
     }
-    void reduce_complete(int64_t x) {
-        if (x < 0 || x >= nreduce || reduce_log[x] == 2) return;
+    bool reduce_complete(int64_t x) {
+        if (x < 0 || x >= nreduce || reduce_log[x] == 2) return false;
         reduce_log[x] = 2;
         creduce++;
+        return true;
     }
     bool done() const { return creduce == nreduce; }  // coordinator.go:138-142
 };
@@ -170,13 +182,19 @@ int listen_sock(const std::string& path) {
 void serve_one(Coordinator& co, int lfd) {
     int fd = accept(lfd, nullptr, nullptr);
     if (fd < 0) return;
+    // a client that connects and never sends must not stall the loop (and with
+    // it expire() and every other worker): bounded reads and writes
+    timeval tv{0, 500000};  // a worker sends its request right after connecting
+    setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof tv);
+    setsockopt(fd, SOL_SOCKET, SO_SNDTIMEO, &tv, sizeof tv);
     Request q{};
     if (read_all(fd, &q, sizeof q) && q.magic == kMagic) {
         std::string fname;
         ReplyHdr r{kMagic, kWait, co.nmap, 0, co.nreduce, 0, 0};
+        // completion replies: CMap / CReduce = 1 if this completion was accepted
         if (q.method == kRequestTask) r = co.request_task(&fname);
-        else if (q.method == kMapComplete) co.map_complete(q.task);
-        else if (q.method == kReduceComplete) co.reduce_complete(q.task);
+        else if (q.method == kMapComplete) r.cmap = co.map_complete(q.task) ? 1 : 0;
+        else if (q.method == kReduceComplete) r.creduce = co.reduce_complete(q.task) ? 1 : 0;
         if (write_all(fd, &r, sizeof r)) write_all(fd, fname.data(), fname.size());
     }
     close(fd);
@@ -229,13 +247,21 @@ void do_map(mrg_ctx* c, const App& app, const WorkerOpts& o, const ReplyHdr& r, 
     mrg_parts_free(p);
 }
 
-void do_reduce(mrg_ctx* c, const App& app, const WorkerOpts& o, const ReplyHdr& r) {
+// false: an input is missing (a duplicate of this task finished and removed
+// them): the task is abandoned, nothing is written
+bool do_reduce(mrg_ctx* c, const App& app, const WorkerOpts& o, const ReplyHdr& r) {
     mrg_parts* acc = nullptr;
     char name[64];
     for (int i = 0; i < r.nmap; i++) {  // worker.go:102-122
         snprintf(name, sizeof name, "mr-%d-%d", i, r.creduce);
         std::vector<uint8_t> b;
-        if (!read_file_opt(name, &b)) continue;  // missing intermediate: skipped (worker.go:105-108)
+        // every map task writes all nReduce files (do_map), so in the reduce
+        // phase a missing one was removed by an accepted duplicate of this task
+        // (the reference skips it, worker.go:105-108, and writes a short mr-out)
+        if (!read_file_try(name, &b)) {
+            if (acc) mrg_parts_free(acc);
+            return false;
+        }
         mrg_parts* q = nullptr;
         if (o.json) check(c, mrg_parts_import_json(c, app.id, (uint32_t)r.nreduce, b.data(), b.size(), &q), "import_json");
         else check(c, mrg_parts_import(c, b.data(), b.size(), &q), "mrg_parts_import");
@@ -254,8 +280,14 @@ void do_reduce(mrg_ctx* c, const App& app, const WorkerOpts& o, const ReplyHdr& 
     snprintf(name, sizeof name, "mr-out-%d", r.creduce);
     write_file_atomic(name, out, n);  // an empty partition still gets its file (worker.go:126-148)
     mrg_free(out);
-    for (int i = 0; i < r.nmap; i++) {  // worker.go:150-154
-        snprintf(name, sizeof name, "mr-%d-%d", i, r.creduce);
+    return true;
+}
+
+// worker.go:150-154, once the coordinator accepted this task's completion
+void remove_reduce_inputs(int nmap, int part) {
+    char name[64];
+    for (int i = 0; i < nmap; i++) {
+        snprintf(name, sizeof name, "mr-%d-%d", i, part);
         remove(name);
     }
 }
@@ -269,8 +301,10 @@ int worker_main(const App& app, WorkerOpts o) {
     if (mrg_open(dev, &c) != MRG_OK) fatalf("%s: cannot open a GPU context", "mrworker_gpu");
     // test hook: die (no completion RPC) after receiving this many tasks, so the
     // coordinator's re-issue path runs (coordinator.go:70-77)
+    // (MRG_WORKER_CRASH_INDEX: only the forked worker with that index, -w mode)
     const char* crash = getenv("MRG_WORKER_CRASH_AFTER");
-    long crash_after = crash ? atol(crash) : -1;
+    const char* crash_idx = getenv("MRG_WORKER_CRASH_INDEX");
+    long crash_after = crash && (!crash_idx || atoi(crash_idx) == o.index) ? atol(crash) : -1;
     long tasks = 0;
     for (;;) {  // worker.go:46-54
         ReplyHdr r{};
@@ -285,9 +319,11 @@ int worker_main(const App& app, WorkerOpts o) {
             do_map(c, app, o, r, fname);
             call(o.sock, kMapComplete, r.cmap, &r, &fname);  // worker.go:93-97
         } else if (r.status == kReduce) {
-            const int x = r.creduce;
-            do_reduce(c, app, o, r);
-            call(o.sock, kReduceComplete, x, &r, &fname);  // worker.go:157-161
+            const int x = r.creduce, nmap = r.nmap;
+            if (!do_reduce(c, app, o, r)) continue;  // abandoned (a duplicate already finished it)
+            ReplyHdr a{};
+            if (call(o.sock, kReduceComplete, x, &a, &fname) && a.creduce == 1)  // worker.go:157-161
+                remove_reduce_inputs(nmap, x);
         }
     }
     mrg_close(c);
@@ -356,15 +392,19 @@ int main_coord(int argc, char** argv) {
     }
     close(lfd);
     unlink(wo.sock.c_str());
+    // the job's status is Done() (every reduce task completed); a worker that
+    // crashed and whose tasks were re-issued and finished by others is the
+    // fault tolerance working, reported but not a failure
     int bad = 0;
     for (size_t k = 0; k < kids.size(); k++) {
         int st = kid_status[k];
         if (st == -1 && waitpid(kids[k], &st, 0) != kids[k]) st = 1 << 8;
         if (!(WIFEXITED(st) && WEXITSTATUS(st) == 0)) bad++;
     }
-    printf("{\"nmap\": %d, \"nreduce\": %d, \"workers\": %d, \"reissued\": %llu}\n", co.nmap, co.nreduce, nworkers,
-           (unsigned long long)co.reissued);
-    return bad ? 1 : 0;
+    printf("{\"nmap\": %d, \"nreduce\": %d, \"workers\": %d, \"reissued\": %llu, \"workers_failed\": %d, "
+           "\"done\": %s}\n", co.nmap, co.nreduce, nworkers, (unsigned long long)co.reissued, bad,
+           co.done() ? "true" : "false");
+    return co.done() ? 0 : 1;
 }
 
 int main_worker(int argc, char** argv) {

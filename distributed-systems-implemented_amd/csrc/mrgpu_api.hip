@@ -17,8 +17,10 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unistd.h>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
 #include <mutex>
 #include <thread>
 #include <string>
@@ -27,6 +29,7 @@
 #include "../../include/mrgpu.h"
 #include "letter_table.inc"
 #include "mrgpu_device.h"
+#include "mrgpu_exch.h"
 
 using namespace mrg;
 
@@ -139,6 +142,67 @@ constexpr uint64_t kHostMagic = 0x4D524748424F5354ull;  // "MRGHBOST"
 struct ExchSide;
 static void exch_free(ExchSide* x);
 
+// Deadline of the collective phases (communicator setup, the shuffle).  A rank
+// that never joins leaves the others blocked inside RCCL or a stream sync with
+// no error to return; the watchdog thread then names the phase on stderr and
+// ends the process with status 124, so a launcher sees a failed rank instead of
+// a hang.  One thread per context, idle (on a condition variable) outside the
+// guarded phases.
+struct Watchdog {
+    std::mutex mu;
+    std::condition_variable cv;
+    const char* phase = nullptr;
+    std::chrono::steady_clock::time_point deadline;
+    int64_t limit_ms = 0;
+    bool stop = false;
+    int rank = 0, nranks = 1;
+    std::thread th;
+    void run() {
+        std::unique_lock<std::mutex> lk(mu);
+        while (!stop) {
+            if (!phase) {
+                cv.wait(lk);
+                continue;
+            }
+            cv.wait_until(lk, deadline);
+            if (!stop && phase && std::chrono::steady_clock::now() >= deadline) {
+                fprintf(stderr, "mrgpu: rank %d of %d: collective phase '%s' did not finish within %lld ms; exiting\n",
+                        rank, nranks, phase, (long long)limit_ms);
+                fflush(stderr);
+                _exit(124);
+            }
+        }
+    }
+    // Start guarding (the deadline runs from here); nested phases keep it.
+    void enter(const char* p, int64_t ms, int r, int n) {
+        std::lock_guard<std::mutex> g(mu);
+        if (!th.joinable()) th = std::thread([this] { run(); });
+        phase = p;
+        limit_ms = ms;
+        rank = r;
+        nranks = n;
+        deadline = std::chrono::steady_clock::now() + std::chrono::milliseconds(ms);
+        cv.notify_one();
+    }
+    void set(const char* p) {
+        std::lock_guard<std::mutex> g(mu);
+        phase = p;
+    }
+    void leave() {
+        std::lock_guard<std::mutex> g(mu);
+        phase = nullptr;
+        cv.notify_one();
+    }
+    ~Watchdog() {
+        {
+            std::lock_guard<std::mutex> g(mu);
+            stop = true;
+            cv.notify_one();
+        }
+        if (th.joinable()) th.join();
+    }
+};
+
 struct mrg_ctx {
     ExchSide* exch = nullptr;  // RCCL shuffle buffers, kept across calls (no hipMalloc / hipFree per step)
     int device = 0;
@@ -225,6 +289,9 @@ struct mrg_ctx {
     size_t h_out_cap = 0;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
+    // collective deadline (option exchange_timeout_ms; comm init gets 4x)
+    int64_t exch_timeout_ms = 120000;
+    Watchdog wd;
 };
 
 struct mrg_parts {
@@ -1106,6 +1173,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);
     else if (!strcmp(name, "rec_cap")) c->rec_cap = v > 0 ? (uint64_t)v : (1u << 21);
     else if (!strcmp(name, "skip_exchange")) c->skip_exchange = v > 0;
+    else if (!strcmp(name, "exchange_timeout_ms")) c->exch_timeout_ms = v > 0 ? v : 120000;
     else if (!strcmp(name, "ingest_piece")) c->ingest_piece = v > 0 ? (uint64_t)v : (256ull << 20);
     else if (!strcmp(name, "ingest_min")) c->ingest_min = v > 0 ? (uint64_t)v : (64ull << 20);
     else return fail(c, MRG_EINVAL, "unknown option %s", name);
@@ -1649,7 +1717,10 @@ int mrg_comm_init(mrg_ctx* c, const uint8_t id[128], int nranks, int rank) {
     if (c->comm) { ncclCommDestroy(c->comm); c->comm = nullptr; }
     ncclUniqueId u;
     memcpy(&u, id, 128);
-    NCHK(c, ncclCommInitRank(&c->comm, nranks, u, rank));
+    c->wd.enter("ncclCommInitRank", 4 * c->exch_timeout_ms, rank, nranks);
+    const ncclResult_t ir = ncclCommInitRank(&c->comm, nranks, u, rank);
+    c->wd.leave();
+    if (ir != ncclSuccess) return fail(c, MRG_ECOMM, "ncclCommInitRank: %s", ncclGetErrorString(ir));
     c->nranks = nranks;
     c->rank = rank;
     return MRG_OK;
@@ -1682,12 +1753,8 @@ __global__ void __launch_bounds__(kExchThreads) owner_count_kernel(Recs r, uint3
         if (h[i]) atomicAdd(&cnt[i], h[i]);
 }
 
-// Pack into per-destination segments: records at rec_base[o] (AoS 40 B), arena at ar_base[o].
-struct WireRec {
-    uint64_t k0, k1, cnt, koff;
-    uint32_t len, part;
-};
-
+// Pack into per-destination segments: 24-byte wire records (mrgpu_exch.h) at
+// rec_base[o], long keys' bytes at ar_base[o].
 __global__ void __launch_bounds__(kExchThreads) pack_kernel(Recs r, uint32_t nranks, const uint64_t* rec_base,
                                                             const uint64_t* ar_base,
                                                             unsigned long long* cur /*[2*nranks]*/, WireRec* wrec,
@@ -1716,7 +1783,7 @@ __global__ void __launch_bounds__(kExchThreads) pack_kernel(Recs r, uint32_t nra
         for (uint32_t k = threadIdx.x; k < 2 * nranks; k += blockDim.x) gbase[k] = h[k] ? atomicAdd(&cur[k], h[k]) : 0;
         __syncthreads();
         if (valid) {
-            WireRec w{r.k0[i], r.k1[i], r.cnt[i], ~0ull, r.len[i], r.part[i]};
+            WireRec w{r.k0[i], r.k1[i], r.cnt[i]};
             if (koff != ~0ull) {
                 const unsigned long long a = gbase[2 * o + 1] + aoff;  // relative to owner o's segment from this source
                 uint4* dst = (uint4*)(war + ar_base[o] + a);           // 16-byte aligned (padded lengths)
@@ -1727,7 +1794,7 @@ __global__ void __launch_bounds__(kExchThreads) pack_kernel(Recs r, uint32_t nra
                     load16u(src + q, len - q, lo, hi);
                     dst[q >> 4] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
                 }
-                w.koff = a;
+                w = WireRec{a, len, r.cnt[i] | kWireLong};
             }
             wrec[rec_base[o] + gbase[2 * o] + slot] = w;
         }
@@ -1735,51 +1802,37 @@ __global__ void __launch_bounds__(kExchThreads) pack_kernel(Recs r, uint32_t nra
     }
 }
 
-// Unpack received wire records; koff rebased by the source's arena displacement
-// (the source segment of record i by binary search over the P record offsets).
+// Unpack received wire records into the Recs the owner's aggregation reads
+// (insert_recs: k0 / k1 / cnt of short keys, arena bytes / len / cnt of long
+// ones; the partition is recomputed there from the key).  A long key's arena
+// offset is rebased by its source's arena displacement (the source segment of
+// record i by binary search over the P record offsets).
 __global__ void unpack_kernel(const WireRec* wrec, uint64_t n, const uint64_t* src_rec_begin, const uint64_t* src_ar_begin,
                               uint32_t nsrc, Recs r) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint32_t lo = 0, hi = nsrc - 1;  // last s with src_rec_begin[s] <= i
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi + 1) >> 1;
-            if (src_rec_begin[mid] <= i) lo = mid;
-            else hi = mid - 1;
-        }
         const WireRec w = wrec[i];
-        r.k0[i] = w.k0;
-        r.k1[i] = w.k1;
-        r.cnt[i] = w.cnt;
-        r.len[i] = w.len;
-        r.part[i] = w.part;
-        r.koff[i] = w.koff == ~0ull ? ~0ull : src_ar_begin[lo] + w.koff;
+        if (w.c & kWireLong) {
+            uint32_t lo = 0, hi = nsrc - 1;  // last s with src_rec_begin[s] <= i
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (src_rec_begin[mid] <= i) lo = mid;
+                else hi = mid - 1;
+            }
+            r.k0[i] = 0;
+            r.k1[i] = 0;
+            r.cnt[i] = w.c & ~kWireLong;
+            r.len[i] = (uint32_t)w.b;
+            r.koff[i] = src_ar_begin[lo] + w.a;
+        } else {
+            r.k0[i] = w.a;
+            r.k1[i] = w.b;
+            r.cnt[i] = w.c;
+            r.len[i] = key_len_short(w.a, w.b);
+            r.koff[i] = ~0ull;
+        }
+        r.part[i] = 0;  // not read by the aggregation
     }
-}
-
-// Host-side layout of one rank's exchange: byte counts / displacements of its
-// send segments (per owner rank) and of its receive segments (per source rank).
-struct ExchPlan {
-    std::vector<size_t> sc, sd, rc, rd, asc, asd, arc, ard;  // records (bytes) and arena bytes
-    std::vector<uint64_t> hbase;                             // [P] record base, [P] arena base (send side)
-    size_t srec = 0, sar = 0, rrec = 0, rar = 0;
-};
-
-// snd[2*o] / snd[2*o+1]: records / arena bytes this rank sends to owner o;
-// rcv[2*s] / rcv[2*s+1]: what it receives from source s.
-static ExchPlan exch_plan(int P, const unsigned long long* snd, const unsigned long long* rcv) {
-    ExchPlan x;
-    for (auto* v : {&x.sc, &x.sd, &x.rc, &x.rd, &x.asc, &x.asd, &x.arc, &x.ard}) v->assign(P, 0);
-    x.hbase.assign(2 * P, 0);
-    for (int o = 0; o < P; o++) {
-        x.hbase[o] = x.srec;
-        x.hbase[P + o] = x.sar;
-        x.sc[o] = snd[2 * o] * sizeof(WireRec); x.sd[o] = x.srec * sizeof(WireRec); x.srec += snd[2 * o];
-        x.asc[o] = snd[2 * o + 1]; x.asd[o] = x.sar; x.sar += snd[2 * o + 1];
-        x.rc[o] = rcv[2 * o] * sizeof(WireRec); x.rd[o] = x.rrec * sizeof(WireRec); x.rrec += rcv[2 * o];
-        x.arc[o] = rcv[2 * o + 1]; x.ard[o] = x.rar; x.rar += rcv[2 * o + 1];
-    }
-    return x;
 }
 
 // Per-rank device state of one exchange.  scratch: [2P] send counts, [2P] receive
@@ -1861,6 +1914,8 @@ static void exch_bytes(const ExchPlan& pl, int P, int me, mrg_stats* st) {
     st->shuffle_recv_bytes = rcv;
 }
 
+static int exchange_rccl(mrg_ctx* c, const mrg_parts* local, int P, mrg_parts** owned);
+
 int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     if (!c || !local || !owned) return MRG_EINVAL;
     int rc;
@@ -1870,6 +1925,15 @@ int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
         return aggregate(c, {local->r}, local->app, local->nreduce, owned);
     }
     HCHK(c, hipEventRecord(c->ev[6], c->s));
+    c->wd.enter("count all-to-all", c->exch_timeout_ms, c->rank, P);
+    rc = exchange_rccl(c, local, P, owned);
+    c->wd.leave();
+    return rc;
+}
+
+// mrg_exchange's steps, under the watchdog (c->wd names the phase).
+static int exchange_rccl(mrg_ctx* c, const mrg_parts* local, int P, mrg_parts** owned) {
+    int rc;
     const Recs& r = local->r;
     if (!c->exch) c->exch = new ExchSide();
     ExchSide& x = *c->exch;
@@ -1879,23 +1943,31 @@ int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     x.rcv.assign(2 * P, 0);
     HCHK(c, hipMemcpyAsync(x.snd.data(), x.d_cnt(P), 16 * P, hipMemcpyDeviceToHost, c->s));
     HCHK(c, hipMemcpyAsync(x.rcv.data(), x.d_rcv(P), 16 * P, hipMemcpyDeviceToHost, c->s));
+    // ncclAllToAllv takes host counts: one round trip for the P x 2 matrix row
+    c->wd.set("count sync");
     HCHK(c, hipStreamSynchronize(c->s));
+    c->wd.set("pack");
     if ((rc = exch_pack(c, r, P, x))) return rc;
     const ExchPlan& pl = x.plan;
-    NCHK(c, ncclAllToAllv(x.sbuf.p, pl.sc.data(), pl.sd.data(), x.rbuf.p, pl.rc.data(), pl.rd.data(), ncclUint8,
-                          c->comm, c->s));
-    NCHK(c, ncclAllToAllv(x.sar_b.p, pl.asc.data(), pl.asd.data(), x.rar_b.p, pl.arc.data(), pl.ard.data(),
-                          ncclUint8, c->comm, c->s));
+    // records and long-key bytes as ONE grouped collective (one launch, both
+    // streams of every peer pair in flight together)
+    c->wd.set("payload all-to-all");
+    NCHK(c, ncclGroupStart());
+    ncclResult_t e1 = ncclAllToAllv(x.sbuf.p, pl.sc.data(), pl.sd.data(), x.rbuf.p, pl.rc.data(), pl.rd.data(),
+                                    ncclUint8, c->comm, c->s);
+    ncclResult_t e2 = ncclAllToAllv(x.sar_b.p, pl.asc.data(), pl.asd.data(), x.rar_b.p, pl.arc.data(), pl.ard.data(),
+                                    ncclUint8, c->comm, c->s);
+    ncclResult_t e3 = ncclGroupEnd();
+    if (e1 != ncclSuccess || e2 != ncclSuccess || e3 != ncclSuccess)
+        return fail(c, MRG_ECOMM, "payload all-to-all: %s", ncclGetErrorString(e1 != ncclSuccess ? e1 : e2 != ncclSuccess ? e2 : e3));
     HCHK(c, hipEventRecord(c->ev[7], c->s));
+    c->wd.set("unpack + aggregate");
     rc = exch_finish(c, local, P, x, owned);
     c->stats.exchange_ms = ev_ms(c->ev[6], c->ev[7]);
     exch_bytes(pl, P, c->rank, &c->stats);
     return rc;
 }
 
-// The same exchange with P contexts driven by one host thread (one per GPU, or
-// several on one device): count / pack on every context, then the all-to-all
-// is peer copies, then unpack + aggregate on every owner.
 int mrg_exchange_group(mrg_ctx* const* ctxs, int P, const mrg_parts* const* local, mrg_parts** owned) {
     if (!ctxs || !local || !owned || P < 1) return MRG_EINVAL;
     for (int i = 0; i < P; i++) {

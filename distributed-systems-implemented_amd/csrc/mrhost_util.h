@@ -4,6 +4,8 @@
 // and the APP argument ("wc" | "grep:<literal>"), the plugin choice of
 // main/mrworker.go:34-51.
 #pragma once
+#include <unistd.h>
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -40,13 +42,49 @@ inline bool read_file_opt(const std::string& path, std::vector<uint8_t>* out) {
     return true;
 }
 
-inline void write_file_atomic(const std::string& name, const void* p, size_t n) {
-    std::string tmp = name + ".tmp";  // temp + rename, as worker.go:83,91
-    FILE* f = fopen(tmp.c_str(), "wb");
-    if (!f) fatalf("cannot create %s", tmp.c_str());
-    if (n && fwrite(p, 1, n, f) != n) fatalf("cannot write into %s", name.c_str());
+// All of a file, or false if it cannot be opened or read to the end (a reduce
+// input that another worker removed meanwhile: the caller abandons the task).
+inline bool read_file_try(const std::string& path, std::vector<uint8_t>* out) {
+    FILE* f = fopen(path.c_str(), "rb");
+    if (!f) return false;
+    out->clear();
+    uint8_t tmp[1 << 16];
+    size_t n;
+    while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) out->insert(out->end(), tmp, tmp + n);
+    const bool ok = !ferror(f);
     fclose(f);
-    if (rename(tmp.c_str(), name.c_str()) != 0) fatalf("cannot rename %s", tmp.c_str());
+    return ok;
+}
+
+// Temp + rename, as worker.go:83,91 (ioutil.TempFile + os.Rename): the temp file
+// gets a unique name in the output's directory (mkstemp), so a re-issued task
+// and the slow worker it replaced never write one inode or rename each other's
+// file away; the data is flushed to disk before the rename publishes it.
+inline void write_file_atomic(const std::string& name, const void* p, size_t n) {
+    std::string tmpl = name + ".tmp-XXXXXX";
+    std::vector<char> path(tmpl.begin(), tmpl.end());
+    path.push_back('\0');
+    const int fd = mkstemp(path.data());
+    if (fd < 0) fatalf("cannot create %s", tmpl.c_str());
+    const char* b = (const char*)p;
+    size_t left = n;
+    while (left) {
+        const ssize_t k = write(fd, b, left);
+        if (k <= 0) {
+            unlink(path.data());
+            fatalf("cannot write into %s", name.c_str());
+        }
+        b += k;
+        left -= (size_t)k;
+    }
+    if (fsync(fd) != 0 || close(fd) != 0) {
+        unlink(path.data());
+        fatalf("cannot write into %s", name.c_str());
+    }
+    if (rename(path.data(), name.c_str()) != 0) {
+        unlink(path.data());
+        fatalf("cannot rename %s", path.data());
+    }
 }
 
 struct App {

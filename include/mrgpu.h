@@ -91,7 +91,7 @@ typedef struct {
     uint64_t shuffle_recv_bytes; /* exchange: wire bytes this rank received from other ranks */
     uint64_t staged_bytes;    /* map: bytes copied into the context's staging buffer first (host input,
                                  or a device pointer not 16-byte aligned) */
-    uint64_t spill_buckets;   /* wc: hash buckets of the map's spill (512; 2048 for high-cardinality splits) */
+    uint64_t spill_buckets;   /* wc: hash buckets of the map's spill (256 by default; 2048 for high-cardinality splits; 512 by option) */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);
@@ -164,19 +164,26 @@ int mrg_sync(mrg_ctx* ctx);
 int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
 
 /* Tuning knobs (0 = default); for benchmarks and tests of the overflow paths.
- * Results never depend on them (every path is exact); unknown names -> MRG_EINVAL.
+ * Results never depend on them (every path is exact), except skip_exchange, which
+ * changes what mrg_run_job computes (benchmark timing only); unknown names -> MRG_EINVAL.
  *   short_table_log2, long_table_log2, list_cap, rec_cap   HBM table / buffer sizes
  *   map_grid, map_mode                   map workgroups; ablation modes (benchmarks)
  *   spill_stream_keys                    force tiny spill streams (overflow tests)
- *   spill_buckets (0, 512, 2048)         spill buckets; 0 = chosen per split from the
- *                                        previous split's aggregated keys
+ *   spill_buckets (0, 256, 512, 2048)    spill buckets; 0 = chosen per split from the
+ *                                        previous split's aggregated keys (256 default,
+ *                                        2048 high-cardinality; 512 the earlier default)
  *   spill_hi_keys                        aggregated keys above which 2048 are chosen
  *   agg_rounds, agg_carry_min, agg_big0 (0: by layout, 1 big, -1 small tables),
  *                                        agg_big_later   bucket aggregation rounds
  *   dict (-1: off), dict_warm (-1: off), dict_keep (permille; -1: always rebuild),
  *                                        dict_min_bytes, dict_sample_bytes
  *   ingest_piece, ingest_min             host input streamed in pieces of this size
- *   skip_exchange                        mrg_run_job: no shuffle (per-rank timing)
+ *   skip_exchange                        CHANGES RESULTS: mrg_run_job with nranks > 1 skips
+ *                                        the shuffle and reduces only this rank's own split
+ *                                        (bench.py's same-process T(1); never for real jobs)
+ *   exchange_timeout_ms                  deadline of a collective phase (mrg_exchange;
+ *                                        mrg_comm_init gets 4x; default 120000): past it the
+ *                                        process prints the phase and exits with status 124
  *   sort_digit_bits (8, 10), sort_fold_part (-1: off), grep_sort_k1 (-1: 8-byte
  *                                        prefix passes only), sort_compact_ties (-1:
  *                                        off)   reduce sort variants */

@@ -46,6 +46,12 @@ def lib():
                                           POINTER(c_void_p), POINTER(c_size_t)]
         L.oracle_mr_partitioned.argtypes = [c_int, c_void_p, c_size_t, POINTER(c_void_p), POINTER(c_size_t), c_size_t,
                                             c_uint32, POINTER(c_void_p), POINTER(c_size_t), POINTER(c_uint64)]
+        L.oracle_count_mt.argtypes = [c_int, c_void_p, c_size_t, c_void_p, c_size_t, c_int, c_uint32,
+                                      POINTER(c_void_p), POINTER(c_size_t), POINTER(c_uint64)]
+        L.oracle_count_mt.restype = c_int
+        L.oracle_merge_parts.argtypes = [c_int, c_uint32, POINTER(c_void_p), POINTER(c_uint64), c_uint32,
+                                         POINTER(c_void_p), POINTER(c_size_t), POINTER(c_uint64)]
+        L.oracle_merge_parts.restype = c_int
         L.oracle_free.argtypes = [c_void_p]
         L.oracle_free.restype = None
         _lib = L
@@ -96,6 +102,47 @@ def c_partitioned(app: str, files, nreduce: int) -> list[bytes]:
     r = ctypes.string_at(out, n.value)
     L.oracle_free(out)
     return [r[offs[i]:offs[i + 1]] for i in range(nreduce)]
+
+
+def c_count_mt(app: str, split, nreduce: int, threads: int = 8) -> list[bytes]:
+    """The whole job over ONE split (bytes or a numpy uint8 array, no copy), counted
+    by `threads` threads (oracle/mrcount.c): mr-out-r for r < nreduce."""
+    L = lib()
+    a, pat = _app(app)
+    out, n = c_void_p(), c_size_t()
+    offs = (c_uint64 * (nreduce + 1))()
+    rc = L.oracle_count_mt(a, _ptr(pat) if pat else None, len(pat), _ptr(split), len(split), threads, nreduce,
+                           ctypes.byref(out), ctypes.byref(n), offs)
+    if rc != 0:
+        raise MemoryError("oracle_count_mt failed")
+    r = ctypes.string_at(out, n.value)
+    L.oracle_free(out)
+    return [r[offs[i]:offs[i + 1]] for i in range(nreduce)]
+
+
+def c_merge_parts(app: str, outs: list[list[bytes]]) -> list[bytes]:
+    """Reduce over the union of several splits' partitioned outputs (each a list of
+    R sorted mr-out-r texts): wc counts of equal keys summed, grep lines deduplicated."""
+    L = lib()
+    a, _ = _app(app)
+    R = len(outs[0]) if outs else 0
+    joined = [b"".join(o) for o in outs]
+    offs = (c_uint64 * (len(outs) * (R + 1)))()
+    for i, o in enumerate(outs):
+        acc = 0
+        for r in range(R):
+            offs[i * (R + 1) + r] = acc
+            acc += len(o[r])
+        offs[i * (R + 1) + R] = acc
+    ptrs = (c_void_p * max(1, len(outs)))(*[_ptr(j) for j in joined])
+    out, n = c_void_p(), c_size_t()
+    roffs = (c_uint64 * (R + 1))()
+    rc = L.oracle_merge_parts(a, len(outs), ptrs, offs, R, ctypes.byref(out), ctypes.byref(n), roffs)
+    if rc != 0:
+        raise ValueError("oracle_merge_parts: malformed input")
+    r = ctypes.string_at(out, n.value)
+    L.oracle_free(out)
+    return [r[roffs[i]:roffs[i + 1]] for i in range(R)]
 
 
 def c_ihash(key: bytes) -> int:

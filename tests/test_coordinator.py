@@ -73,8 +73,8 @@ def test_handout_order_wait_reissue_and_done(tmp_path):
         assert [g[0] for g in got] == [MAP] * 3 and [g[2] for g in got] == [0, 1, 2]
         assert [g[5] for g in got] == [str(f) for f in files] and all(g[3] == 2 for g in got)
         assert call(sock, REQUEST)[0] == WAIT            # every map task in progress
-        call(sock, MAP_DONE, 0)
-        call(sock, MAP_DONE, 0)                          # a duplicate completion counts once
+        assert call(sock, MAP_DONE, 0)[2] == 1           # completion accepted: CMap = 1
+        assert call(sock, MAP_DONE, 0)[2] == 0           # a duplicate completion counts once, not accepted
         call(sock, MAP_DONE, 1)
         assert call(sock, REQUEST)[0] == WAIT            # map 2 not completed: no reduce task yet
         time.sleep(1.3)                                  # map 2 held past the timeout -> untouched again
@@ -84,13 +84,21 @@ def test_handout_order_wait_reissue_and_done(tmp_path):
         r0, r1 = call(sock, REQUEST), call(sock, REQUEST)
         assert (r0[0], r0[4], r1[0], r1[4]) == (REDUCE, 0, REDUCE, 1) and r0[1] == 3
         assert call(sock, REQUEST)[0] == WAIT
-        call(sock, REDUCE_DONE, 1)
+        # a client that connects and never sends must not stall the coordinator
+        # (accepted sockets time out after 0.5 s)
+        idle = socket.socket(socket.AF_UNIX, socket.SOCK_STREAM)
+        idle.connect(sock)
+        t0 = time.time()
+        assert call(sock, REDUCE_DONE, 1)[4] == 1        # accepted: the worker may remove its inputs
+        assert call(sock, REDUCE_DONE, 1)[4] == 0        # a late duplicate: it must not
+        assert time.time() - t0 < 3
+        idle.close()
         call(sock, REDUCE_DONE, 0)
         assert call(sock, REQUEST)[0] == DONE
         out, err = p.communicate(timeout=10)
         assert p.returncode == 0, err
         info = json.loads(out.decode().strip().splitlines()[-1])
-        assert info["reissued"] == 1 and info["nmap"] == 3 and info["nreduce"] == 2
+        assert info["reissued"] == 1 and info["nmap"] == 3 and info["nreduce"] == 2 and info["done"]
     finally:
         if p.poll() is None:
             p.kill()
@@ -149,3 +157,20 @@ def test_coordinator_reissues_a_crashed_workers_task(tmp_path):
     assert coord.returncode == 0, err.decode()
     assert json.loads(out.decode().strip().splitlines()[-1])["reissued"] >= 1
     assert [(tmp_path / f"mr-out-{k}").read_bytes() for k in range(4)] == O.c_partitioned("wc", files, 4)
+
+
+@pytest.mark.gpu
+def test_coordinator_forked_worker_crash_still_succeeds(tmp_path):
+    """-w 2 with forked worker 0 dying while it holds its second task: the task
+    is re-issued to worker 1 (coordinator.go:70-77); the job's status follows
+    Done(), so it exits 0 and reports the crash as information."""
+    files = cases.synthetic(C.KIND_ASCII, 5000, [200_000, 150_000, 100_000, 120_000], 64)
+    paths = _write(tmp_path, files)
+    env = dict(os.environ, MRG_WORKER_CRASH_AFTER="1", MRG_WORKER_CRASH_INDEX="0")
+    r = subprocess.run([COORD, "-n", "4", "-w", "2", "--sock", str(tmp_path / "s"), "--task-timeout", "2", "wc"]
+                       + paths, cwd=tmp_path, env=env, capture_output=True, timeout=240)
+    assert r.returncode == 0, r.stderr.decode()[-2000:]
+    info = json.loads(r.stdout.decode().strip().splitlines()[-1])
+    assert info["done"] and info["workers_failed"] == 1 and info["reissued"] >= 1
+    assert [(tmp_path / f"mr-out-{k}").read_bytes() for k in range(4)] == O.c_partitioned("wc", files, 4)
+    assert not list(tmp_path.glob("mr-*.tmp-*"))  # unique temp files, all renamed
