@@ -32,6 +32,8 @@
 #include "mrgpu_exch.h"
 
 using namespace mrg;
+static_assert(MRG_LETTER_LDS_PAGES == kLetterLdsPages && MRG_LETTER_NUNIQUE == kLetterUnique,
+              "regenerate letter_table.inc and update kLetterLdsPages / kLetterUnique");
 
 namespace {
 

@@ -255,6 +255,68 @@ __device__ uint32_t utf8_letter_mask(P b, int q0, LetterTables lt) {
     return mask;
 }
 
+// ---------------------------------------------------------------- UTF-8 letter mask (LDS tables)
+typedef __attribute__((address_space(3))) uint32_t lds_u32_unaligned __attribute__((aligned(1)));
+struct LdsLetters {
+    const lds_u8* l1;   // [kLetterLdsPages]
+    const lds_u32* l2;  // [kLetterUnique * 8]
+};
+__device__ __forceinline__ bool is_letter_lds(uint32_t cp, LdsLetters L) {
+    if (cp >= ((uint32_t)kLetterLdsPages << 8)) return false;
+    const uint32_t idx = L.l1[cp >> 8];
+    return (L.l2[idx * 8 + ((cp >> 5) & 7)] >> (cp & 31)) & 1u;
+}
+
+// 0x80 in each byte of x that is an ASCII letter [A-Za-z] (any byte values)
+__device__ __forceinline__ uint32_t ascii_flags4_any(uint32_t x) { return ascii_flags4(x & 0x7F7F7F7Fu) & ~x; }
+// 0x80 in each byte >= 0xC0 (a UTF-8 lead byte or an invalid one; validated later)
+__device__ __forceinline__ uint32_t lead_flags4(uint32_t x) { return x & (x << 1) & 0x80808080u; }
+// four flag dwords (0x80 per flagged byte) -> 16-bit mask, byte k of dword d -> bit 4d + k
+__device__ __forceinline__ uint32_t flags_to_bits16(uint32_t f0, uint32_t f1, uint32_t f2, uint32_t f3) {
+    const uint32_t lo = __builtin_amdgcn_udot4(f1, 0x80402010u, __builtin_amdgcn_udot4(f0, 0x08040201u, 0u, false), false);
+    const uint32_t hi = __builtin_amdgcn_udot4(f3, 0x80402010u, __builtin_amdgcn_udot4(f2, 0x08040201u, 0u, false), false);
+    return (lo | (hi << 8)) >> 7;
+}
+
+// Letter mask of the 16 slot bytes [q0, q0 + 16) with Go's decoding semantics
+// (strings.FieldsFunc's range loop + unicode.IsLetter, mrapps/wc.go:23,26;
+// SURVEY.md Appendix A.1), for a slot in LDS whose bytes [q0 - 4, q0 + 19) are
+// readable:
+//   - ASCII letters by SWAR;
+//   - every lead byte (>= 0xC0) in [q0 - 3, q0 + 16) starts a rune: a lead is
+//     never a continuation byte, so no valid sequence can cover it (the local
+//     rune-start rule always holds); its sequence is checked with Go's
+//     acceptance ranges and, if valid and a letter, marks all its bytes;
+//   - continuation bytes outside a valid sequence and invalid leads are
+//     U+FFFD, not letters (nothing to do).
+// Work is one loop turn per lead byte of the lane (LDS reads only).  first: the
+// look-back lane (q0 = 0), whose bytes before the slot read as 0 (only its bit
+// 15 is used, which depends on bytes >= 9).
+__device__ __forceinline__ uint32_t utf8_mask16(const lds_u8* slot, uint32_t q0, bool first, LdsLetters L) {
+    const lds_u32* s4 = (const lds_u32*)(slot + q0);
+    const uint32_t w0 = first ? 0u : s4[-1], w1 = s4[0], w2 = s4[1], w3 = s4[2], w4 = s4[3];
+    uint32_t m = flags_to_bits16(ascii_flags4_any(w1), ascii_flags4_any(w2), ascii_flags4_any(w3), ascii_flags4_any(w4));
+    // lead bytes at positions q0 - 3 + i, i = 0..18 (bits 0-2: bytes 1-3 of w0)
+    uint32_t leads = (flags_to_bits16(lead_flags4(w0), lead_flags4(w1), lead_flags4(w2), lead_flags4(w3)) >> 1) |
+                     (flags_to_bits16(lead_flags4(w4), 0u, 0u, 0u) << 15);
+    while (leads) {
+        const uint32_t i = __builtin_ctz(leads);
+        leads &= leads - 1;
+        const uint32_t w = *(const lds_u32_unaligned*)(slot + q0 + i - 3);
+        const uint32_t c0 = w & 0xFFu, c1 = (w >> 8) & 0xFFu, c2 = (w >> 16) & 0xFFu, c3 = w >> 24;
+        const uint32_t need = c0 >= 0xF0u ? 3u : c0 >= 0xE0u ? 2u : 1u;  // continuation bytes
+        const uint32_t lo = c0 == 0xE0u ? 0xA0u : c0 == 0xF0u ? 0x90u : 0x80u;
+        const uint32_t hi = c0 == 0xEDu ? 0x9Fu : c0 == 0xF4u ? 0x8Fu : 0xBFu;
+        const bool valid = c0 >= 0xC2u && c0 <= 0xF4u && c1 >= lo && c1 <= hi && (need < 2u || (c2 & 0xC0u) == 0x80u) &&
+                           (need < 3u || (c3 & 0xC0u) == 0x80u);
+        const uint32_t cp = need == 1u ? ((c0 & 0x1Fu) << 6) | (c1 & 0x3Fu)
+                          : need == 2u ? ((c0 & 0x0Fu) << 12) | ((c1 & 0x3Fu) << 6) | (c2 & 0x3Fu)
+                                       : ((c0 & 0x07u) << 18) | ((c1 & 0x3Fu) << 12) | ((c2 & 0x3Fu) << 6) | (c3 & 0x3Fu);
+        if (valid && is_letter_lds(cp, L)) m |= ((((2u << need) - 1u) << i) >> 3) & 0xFFFFu;
+    }
+    return m;
+}
+
 // 32-bit mix of a <= 16-byte key given as four little-endian words.
 __device__ __forceinline__ uint32_t fold32(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
     // (three-input xor as one v_bitop3_b32, truth table 0x96; same value as the plain xors)

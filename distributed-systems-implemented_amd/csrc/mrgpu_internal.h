@@ -18,6 +18,7 @@
 namespace mrg {
 
 constexpr uint64_t kUnwritten = ~0ull;
+constexpr uint64_t kListHole = ~0ull;  // an unused entry of the long-word list
 constexpr int kWave = 64;
 
 // status word bits (device -> host)
@@ -157,6 +158,11 @@ struct LetterTables {
     const uint8_t* l1;
     const uint32_t* l2;
 };
+// The map kernels' LDS copy of the letter tables (letter_table.inc): l1 of the
+// first kLetterLdsPages 256-code-point pages (no letter lies above them in
+// Unicode 13.0.0; the generator asserts it) and every distinct l2 page.
+constexpr int kLetterLdsPages = 788;
+constexpr int kLetterUnique = 111;
 
 // ---- launchers (mrgpu_map.hip) ----
 void clear_tables(const Tables& t, bool short_table, hipStream_t s);

@@ -13,21 +13,94 @@
 
 namespace mrg {
 
-// Words longer than 16 bytes: decode forward from the start (one lane per word).
-__global__ void wc_long_kernel(const uint8_t* __restrict__ in, uint64_t n, Tables t, LetterTables lt, uint64_t nlist) {
-    uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nlist) return;
-    const uint64_t s = t.list[i];
-    uint64_t q = s, h = kFnv64Off;
-    while (q < n) {
-        uint32_t c0 = in[q];
-        uint32_t c1 = q + 1 < n ? in[q + 1] : 0, c2 = q + 2 < n ? in[q + 2] : 0, c3 = q + 3 < n ? in[q + 3] : 0;
-        int vl = utf8_valid_len(c0, c1, c2, c3);
-        if (vl == 0 || !is_letter_cp(utf8_decode(c0, c1, c2, c3, vl), lt)) break;
-        for (int k = 0; k < vl; k++) h = fnv1a64_step(h, in[q + k]);
-        q += vl;
+// Words longer than 16 bytes (wc.go:21-34 for the words the map kernel's 16-byte
+// keys cannot hold): one lane per occurrence decodes the word forward from its
+// start (Go acceptance ranges, IsLetter from LDS tables) and hashes its bytes
+// (FNV-1a-64).  Occurrences are then counted in a per-workgroup LDS table keyed
+// by the hash and confirmed by a bytewise compare against the slot's first
+// occurrence, so the HBM LongTable sees one insert per (workgroup, distinct
+// word) instead of one per occurrence: a Zipf-hot long word otherwise serializes
+// on its slot's atomics (mixed-script text has many words over 16 bytes: C2u's
+// 31 M occurrences took 136 ms that way).  Lost claim races and a full table
+// fall back to a direct HBM insert (exact either way).
+constexpr int kLongWG = 512;
+constexpr int kLongSlots = 2048;
+constexpr unsigned long long kRepUnpub = ~0ull;
+struct alignas(16) LongLds {
+    unsigned long long h[kLongSlots];    // hash | 1 (0: empty)
+    unsigned long long rep[kLongSlots];  // input offset of the slot's first occurrence (kRepUnpub until published)
+    uint32_t len[kLongSlots];
+    uint32_t cnt[kLongSlots];
+    uint32_t l2[kLetterUnique * 8];
+    uint8_t l1[kLetterLdsPages];
+};
+
+__global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restrict__ in, uint64_t n, Tables t,
+                                                          LetterTables lt, uint64_t nlist) {
+    __shared__ LongLds A;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLongSlots; i += kLongWG) {
+        A.h[i] = 0;
+        A.rep[i] = kRepUnpub;
+        A.cnt[i] = 0;
     }
-    long_insert(t, h, in + s, q - s, 1);
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLetterUnique * 8; i += kLongWG) A.l2[i] = lt.l2[i];
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLetterLdsPages; i += kLongWG) A.l1[i] = lt.l1[i];
+    __syncthreads();
+    const LdsLetters L{(const lds_u8*)A.l1, (const lds_u32*)A.l2};
+    // this workgroup's contiguous share of the list
+    const uint64_t per = (nlist + gridDim.x - 1) / gridDim.x;
+    const uint64_t b = (uint64_t)blockIdx.x * per, e = b + per < nlist ? b + per : nlist;
+    for (uint64_t i = b + threadIdx.x; i < e; i += kLongWG) {
+        const uint64_t s = t.list[i];
+        if (s == kListHole) continue;  // the unused rest of a map wave's reserved range
+        uint64_t q = s, h = kFnv64Off;
+        while (q < n) {
+            const uint32_t c0 = in[q];
+            uint32_t vl = 1;
+            bool let;
+            if (c0 < 0x80u) {
+                let = ((c0 | 0x20u) - 0x61u) < 26u;
+            } else {
+                const uint32_t c1 = q + 1 < n ? in[q + 1] : 0, c2 = q + 2 < n ? in[q + 2] : 0, c3 = q + 3 < n ? in[q + 3] : 0;
+                vl = (uint32_t)utf8_valid_len(c0, c1, c2, c3);
+                let = vl != 0 && is_letter_lds(utf8_decode(c0, c1, c2, c3, (int)vl), L);
+            }
+            if (!let) break;
+            for (uint32_t k = 0; k < vl; k++) h = fnv1a64_step(h, in[q + k]);
+            q += vl;
+        }
+        const uint32_t len = (uint32_t)(q - s);
+        const unsigned long long hk = h | 1ull;
+        bool done = false;
+        uint32_t slot = (uint32_t)(hk >> 20) & (kLongSlots - 1);
+        for (int probe = 0; probe < 16 && !done; probe++, slot = (slot + 1) & (kLongSlots - 1)) {
+            unsigned long long cur = __hip_atomic_load(&A.h[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (cur == 0) {
+                cur = atomicCAS(&A.h[slot], 0ull, hk);
+                if (cur == 0) {  // claimed: publish the representative, then count
+                    A.len[slot] = len;
+                    __hip_atomic_store(&A.rep[slot], (unsigned long long)s, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    atomicAdd(&A.cnt[slot], 1u);
+                    done = true;
+                    break;
+                }
+            }
+            if (cur == hk) {
+                const unsigned long long r = __hip_atomic_load(&A.rep[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (r == kRepUnpub) break;  // being published: never wait here, insert directly
+                if (A.len[slot] == len && bytes_equal(in + r, in + s, len)) {
+                    atomicAdd(&A.cnt[slot], 1u);
+                    done = true;
+                }
+            }
+        }
+        if (!done) long_insert(t, h, in + s, len, 1);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLongSlots; i += kLongWG) {
+        const uint32_t c = A.cnt[i];
+        if (c) long_insert(t, A.h[i], in + A.rep[i], A.len[i], c);
+    }
 }
 
 // ------------------------------------------------------------ grep kernels
@@ -696,7 +769,10 @@ void clear_tables(const Tables& t, bool short_table, hipStream_t s) {
 
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s) {
     if (nlist == 0) return;
-    wc_long_kernel<<<(unsigned)((nlist + 255) / 256), 256, 0, s>>>(in, n, t, lt, nlist);
+    // about 16 occurrences per lane, at most 4 workgroups per CU's worth
+    uint64_t g = (nlist + kLongWG * 16 - 1) / (kLongWG * 16);
+    if (g > 1024) g = 1024;
+    wc_long_kernel<<<(unsigned)g, kLongWG, 0, s>>>(in, n, t, lt, nlist);
 }
 
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,

@@ -43,6 +43,11 @@ constexpr int kAggThreads = 512;
 // rare non-ASCII path).  Neighbouring slots overlap by 32 bytes (re-read from
 // L2, not HBM).
 constexpr int kSlotBytes = 1024;
+// A slot is followed by the 4 input bytes after its window (a second, one-lane
+// DMA): a UTF-8 rune starting in the look-ahead lane's last 3 bytes is decoded
+// exactly.  Slots are 16-byte aligned.
+constexpr int kSlotTail = 4;
+constexpr int kSlotStride = kSlotBytes + 16;
 constexpr int kOwnLanes = 62;
 constexpr uint64_t kOwn = 16 * kOwnLanes;  // 992
 constexpr int kRing = 3;                    // LDS slots per wave: current, in flight, free (the word list)
@@ -61,30 +66,17 @@ template <int NW, int NB>
 struct alignas(16) MapLdsT {
     uint4 kmask[kMaskLens];                     // kmask[len]: the first min(len, 16) of 16 key bytes
     uint4 dset[kDictSets];                      // dictionary image
-    uint8_t ring[NW][kRing][kSlotBytes];
+    uint8_t ring[NW][kRing][kSlotStride];
     uint32_t dcnt[kDictSlots + kWave];          // dictionary counts of this workgroup (+ per-lane miss dummies)
     // spill cursors: [0, NB) 8-byte streams, [NB, 2 NB) 16-byte streams, then per-lane dummies for hits
     uint32_t curs[2 * NB + kWave];
-    unsigned long long red[4 * kWavesPerWG];    // block_add4 scratch
+    uint32_t lt2[kLetterUnique * 8];            // letter tables (non-ASCII chunks): l2 pages
+    uint8_t lt1[kLetterLdsPages];               // l1 of the pages that hold letters
 };
 static_assert(kSlotBytes == 1024 && kMaskLens * 16 <= 512, "kmask index fits 0x1F0");
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBuckets>) <= 160 * 1024, "map LDS budget");
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBucketsLo>) <= 160 * 1024, "map LDS budget (256 buckets)");
 static_assert(sizeof(MapLdsT<12, kSpillBucketsHi>) <= 160 * 1024, "map LDS budget (high-cardinality)");
-
-// A slot's bytes with the 3 input bytes after it: utf8_letter_mask over lane 63
-// reads up to slot byte 1026 (a rune starting in the last 3 bytes).
-struct SlotTail {
-    const lds_u8* b;
-    uint32_t tail;  // input bytes [slot end, +3), zero at or past the split's end
-    __device__ uint32_t operator[](int q) const { return q < kSlotBytes ? (uint32_t)b[q] : (tail >> (8 * (q - kSlotBytes))) & 0xFFu; }
-};
-__device__ __forceinline__ uint32_t slot_tail(const uint8_t* in, uint64_t n, uint64_t p) {
-    uint32_t t = 0;
-    for (int i = 0; i < 3; i++)
-        if (p + i < n) t |= (uint32_t)in[p + i] << (8 * i);
-    return t;
-}
 
 // v_ffbl_b32 as the hardware defines it: index of the lowest set bit, 0xFFFFFFFF for 0
 // (__builtin_ctz(0) is undefined and the defined variants add a compare and select)
@@ -147,7 +139,7 @@ __device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
 // other memory operations (words > 16 bytes, chunks of more than kBatchWords
 // words, HBM-table overflow, UTF-8 table lookups) drain with vmcnt(0).
 constexpr uint32_t kOutOfRange = 0xFFFFFFF0u;
-constexpr int kVmemPerIter = 3;  // per chunk: one 8-byte and one 16-byte spill store, one DMA
+constexpr int kVmemPerIter = 4;  // per chunk: one 8-byte and one 16-byte spill store, the DMA and its 4-byte tail
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -178,10 +170,38 @@ __device__ __forceinline__ void dma_chunk(i32x4 rsrc, uint32_t voff, uint32_t ld
     else
         asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
                      : "memory", "m0");
+    // the 4 bytes after the window -> LDS [lds_base + 1024, +4): lane 0 alone
+    // (exec saved and restored inside the statement)
+#ifdef MRG_AB_NO_TAIL_DMA  // A/B only: ASCII splits exact, UTF-8 look-ahead wrong
+    return;
+#endif
+    unsigned long long saved;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\ts_mov_b64 exec, 1\n\ts_mov_b32 m0, %3\n\t"
+        "buffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b64 exec, %0"
+        : "=&s"(saved)
+        : "v"(voff + (uint32_t)kSlotBytes), "s"(rsrc), "s"(lds_base + (uint32_t)kSlotBytes)
+        : "memory", "m0");
 }
 __device__ __forceinline__ void wait_vmem_iter() {
-    static_assert(kVmemPerIter == 3, "update the immediate");
+    static_assert(kVmemPerIter == 4, "update the immediate");
+#ifdef MRG_AB_NO_TAIL_DMA
     asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+#else
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+#endif
+}
+// The same after an iteration that issued kVmemWide spill stores (a chunk with
+// more than 64 dictionary misses appends from its word slots: 2 stores per
+// batch slot, no drain), + its DMA and tail.
+constexpr int kVmemWide = 2 * kBatch;
+__device__ __forceinline__ void wait_vmem_iter_wide() {
+    static_assert(kVmemWide + 2 == 8, "update the immediate");
+#ifdef MRG_AB_NO_TAIL_DMA
+    asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+#else
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+#endif
 }
 __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -198,6 +218,15 @@ __device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uin
     const uint32_t rhi = (uint32_t)(r >> 32), rlo = (uint32_t)r;
     const uint32_t nrec = (int32_t)rhi < 0 ? 0u : (rhi != 0 || rlo > 0xFFFFFF00u) ? 0xFFFFFF00u : rlo;
     dma_chunk<kPol>(raw_rsrc(in + base, nrec), (uint32_t)(cs - base) - kBack + 16u * lane, lds_base);
+}
+
+// Long-word list: each map wave reserves kLongReserve entries at a time; the
+// unused rest of a range is closed with kListHole entries (skipped by
+// wc_long_kernel).
+constexpr uint32_t kLongReserve = 256;
+__device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint32_t lleft, uint32_t lane) {
+    for (uint32_t g = 0; g < lleft; g += kWave)
+        if (g + lane < lleft && lbase + g + lane < t.list_cap) t.list[lbase + g + lane] = kListHole;
 }
 
 // input loads are non-temporal (measured ~2 % faster than the default policy);
@@ -242,6 +271,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         else if (resume && b < 2u * NB) v = t.sp.counts[(uint64_t)(b - NB) * t.sp.nwg + blockIdx.x];
         curs[b] = v;
     }
+    for (uint32_t i = tid; i < (uint32_t)kLetterUnique * 8; i += kT) L.lt2[i] = lt.l2[i];
+    for (uint32_t i = tid; i < (uint32_t)kLetterLdsPages; i += kT) L.lt1[i] = lt.l1[i];
+    const LdsLetters lds_lt{(const lds_u8*)L.lt1, (const lds_u32*)L.lt2};
     if (tid < kMaskLens * 4) {  // byte masks: dword d of kmask[len] keeps clamp(len - 4d, 0, 4) bytes
         const int nb = min(max((int)(tid >> 2) - 4 * (int)(tid & 3), 0), 4);
         ((uint32_t*)L.kmask)[tid] = nb == 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
@@ -261,29 +293,41 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         (void*)(t.sp.pool + (uint64_t)blockIdx.x * NB * sub), (short)0, (int)(NB * sub * 16u),
         0x00020000);
     uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
+    // this wave's reserved range of the long-word list: [lbase, lbase + lleft)
+    uint64_t lbase = 0;
+    uint32_t lleft = 0;
+    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+        (void*)t.list, (short)0, (int)(t.list_cap * 8u < 0xFFFFFF00ull ? t.list_cap * 8u : 0xFFFFFF00ull), 0x00020000);
     const uint32_t ring0 = lds_addr(L.ring[wv][0]);
+    static_assert(sizeof(L.ring) >= 4 * kWavesPerWG * sizeof(unsigned long long), "block_add4 scratch aliases the ring");
 
     // prologue: chunk c0 landed before the loop, chunk c0 + stride in flight
     // byte offsets advance by addition (64-bit scalar multiplies per iteration are not free)
     const uint64_t cstep = (uint64_t)stride * kOwn;
     dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn, lane, ring0);
     wait_vmem_all();
-    dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn + cstep, lane, ring0 + kSlotBytes);
+    dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn + cstep, lane, ring0 + kSlotStride);
     uint32_t k = 0;  // ring slot of the current chunk
     uint64_t cs = (uint64_t)c0 * kOwn;  // the current chunk's first own byte = slot byte 16 (slot byte i = input cs - 16 + i)
     // kf = the free slot (the word list now, chunk c + 2*stride next) = the slot
     // before k; both rotate as loop-carried scalars
     uint32_t kf = kRing - 1;
+    // spill store instructions the previous iteration issued after the DMA now
+    // awaited: 2 (staged appends) or kVmemWide (appends from the word slots)
+    bool wide_prev = false;
     for (uint32_t c = c0; c < cend; c += stride, cs += cstep, kf = k, k = k == kRing - 1 ? 0 : k + 1) {
-        wait_vmem_iter();  // chunk c's DMA (issued two iterations ago) has landed
+        // chunk c's DMA (issued two iterations ago) has landed
+        if (wide_prev) wait_vmem_iter_wide();
+        else wait_vmem_iter();
+        wide_prev = false;
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
-        const uint32_t bufa = ring0 + k * kSlotBytes;  // = lds_addr(buf)
+        const uint32_t bufa = ring0 + k * kSlotStride;  // = lds_addr(buf)
         lds_uint4* b4 = (lds_uint4*)buf;
         lds_u16* list = (lds_u16*)L.ring[wv][kf];
         if (c >= ctail) {  // the window reaches the split's last n % 4 bytes (ctail = ~0u: none)
             // the split's last n % 4 bytes sit in a dword the range check zero-filled
             const int64_t p = (int64_t)(n & ~3ull) + lane - ((int64_t)cs - kBack);
-            if (lane < (uint32_t)(n & 3) && p >= 0 && p < kSlotBytes) buf[p] = in[(n & ~3ull) + lane];
+            if (lane < (uint32_t)(n & 3) && p >= 0 && p < kSlotBytes + kSlotTail) buf[p] = in[(n & ~3ull) + lane];
             wait_vmem_all();
             wave_sync();
         }
@@ -299,11 +343,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             if (ascii) {
                 mA = ascii_mask16(ca);
             } else {
+                // UTF-8: ASCII letters by SWAR, one loop turn per lead byte, letter
+                // tables in LDS (no memory operation: the counted DMA wait holds)
                 utf8_chunks++;
-                if (lane == 0) mA = utf8_letter_mask<8>(buf, 8, lt) << 8;  // bytes 8-15 (rune starts need 3 back)
-                else if (lane < 63) mA = utf8_letter_mask<16>(buf, 16 * lane, lt);
-                else mA = utf8_letter_mask<16>(SlotTail{buf, slot_tail(in, n, cs - kBack + kSlotBytes)}, 16 * lane, lt);
-                wait_vmem_all();
+                mA = utf8_mask16(buf, 16 * lane, lane == 0, lds_lt);
             }
             // Word starts (a letter byte whose predecessor is not one) in the owned lanes
             // and lengths (ctz over this lane's mask and the next lane's), packed into the
@@ -393,12 +436,49 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         hh[u] = fold32((uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32));
                         mMid[u] = __ballot(k1[u] != 0);
                     }
-                    // words of more than 16 bytes: resolved by wc_long_kernel from the input (rare)
-                    if (mLng[0] | mLng[1] | mLng[2]) {  // rare: a global atomic, then drain
+                    // words of more than 16 bytes: their starts go to the list, resolved by
+                    // wc_long_kernel from the input.  Mixed-script text has them in most
+                    // chunks (C2u: ~3 per chunk), so each wave appends into its own
+                    // reserved range of the list (one device atomic per kLongReserve
+                    // words: a same-address atomic per chunk serialized the whole kernel,
+                    // 207 ms per 10 GB), with one store per chunk: the starts are staged
+                    // in the list slot, whose entries are all read by now (one pass).
+                    // The extra store only lengthens the next counted wait.
+                    if (mLng[0] | mLng[1] | mLng[2]) {
+                        if (passes == 1) {
+                            lds_u64* lst = (lds_u64*)L.ring[wv][kf];
+                            uint32_t nlong = 0;
         #pragma unroll
-                        for (int u = 0; u < kBatch; u++)
-                            if (__builtin_amdgcn_inverse_ballot_w64(mLng[u])) list_append(t, cs - kBack + (e[u] & 0x3FFu));
-                        wait_vmem_all();
+                            for (int u = 0; u < kBatch; u++) {
+                                if (__builtin_amdgcn_inverse_ballot_w64(mLng[u]))
+                                    lst[nlong + mbcnt64(mLng[u])] = cs - kBack + (e[u] & 0x3FFu);
+                                nlong += (uint32_t)__popcll(mLng[u]);
+                            }
+                            if (nlong > lleft) {  // a fresh range (rare): close the old one, one atomic, drain
+                                list_close(t, lbase, lleft, lane);
+                                const uint32_t want = kLongReserve;
+                                unsigned long long b0 = 0;
+                                if (lane == 0) b0 = atomicAdd(&t.ctr->nlist, (unsigned long long)want);
+                                lbase = __builtin_amdgcn_readfirstlane((uint32_t)b0) |
+                                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b0 >> 32)) << 32);
+                                lleft = want;
+                                if (lbase + want > t.list_cap && lane == 0) set_status(t.ctr, kStListFull);
+                                wait_vmem_all();
+                            }
+                            const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
+                            const uint64_t at = lbase + lane;
+                            __builtin_amdgcn_raw_buffer_store_b64(
+                                (u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
+                                lane < nlong && at < t.list_cap && at < (1ull << 29) ? (uint32_t)(at * 8u) : kOutOfRange,
+                                0, 0);
+                            lbase += nlong;
+                            lleft -= nlong;
+                        } else {  // several passes (> 192 words): the list slot is still needed
+        #pragma unroll
+                            for (int u = 0; u < kBatch; u++)
+                                if (__builtin_amdgcn_inverse_ballot_w64(mLng[u])) list_append(t, cs - kBack + (e[u] & 0x3FFu));
+                            wait_vmem_all();
+                        }
                     }
                     if constexpr ((mode & 4) != 0) {
         #pragma unroll
@@ -545,20 +625,31 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             (u32x4){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32)},
                             rs16, o16, 0, 0);
                         const uint64_t mOver = mMiss[u] & ((mBig[u] & ~mFit16) | (~mBig[u] & ~mFit8));
-                        if (__builtin_amdgcn_inverse_ballot_w64(mOver)) {
-                            short_insert(t, k0[u], k1[u], 1);
-                            t.bflag[b] = 1u;
-                            ovf++;
+                        if (mOver) {  // rare: HBM-table inserts, then drain (the counted wait assumes stores only)
+                            if (__builtin_amdgcn_inverse_ballot_w64(mOver)) {
+                                short_insert(t, k0[u], k1[u], 1);
+                                t.bflag[b] = 1u;
+                                ovf++;
+                            }
+                            wait_vmem_all();
                         }
                     }
-                    wait_vmem_all();  // this pass issued a different number of VMEM instructions
+                    // one pass (<= kBatchWords words, > 64 misses: high-cardinality text):
+                    // exactly kVmemWide stores, counted by the next iteration's wait (a
+                    // drain here would also wait for the DMA issued one chunk ahead);
+                    // several passes: a different count, drain
+                    // (2048 buckets: drained — the 4096 streams per workgroup then leave
+                    // L2 less fragmented: C5 map 39.8 ms counted vs 35.5 drained)
+                    if (passes == 1 && NB != kSpillBucketsHi) wide_prev = true;
+                    else wait_vmem_all();
                 }
             }
         }
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
-        dma_for_chunk<dma_policy(mode)>(in, n, cs + 2 * cstep, lane, ring0 + kf * kSlotBytes);
+        dma_for_chunk<dma_policy(mode)>(in, n, cs + 2 * cstep, lane, ring0 + kf * kSlotStride);
     }
+    list_close(t, lbase, lleft, lane);
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
 
     __syncthreads();
@@ -580,7 +671,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         }
     if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
     block_add4<NW>(&t.ctr->spilled, &t.ctr->dict_hits, &t.ctr->spill_ovf, &t.ctr->chunks_utf8, spilled, hits,
-                            ovf, lane == 0 ? utf8_chunks : 0, L.red);
+                            ovf, lane == 0 ? utf8_chunks : 0, (unsigned long long*)&L.ring[0][0][0]);
     if (t.dbg && tid == 0) t.dbg[2 * (NB + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -1647,9 +1738,9 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     if (cbeg >= cend) return true;
     const uint32_t cb = (uint32_t)cbeg, ce = (uint32_t)cend;
     const int rs = resume ? 1 : 0;
-    // first chunk whose window [cs - 16, cs + 1008) reaches the dword holding the
+    // first chunk whose window [cs - 16, cs + 1012) reaches the dword holding the
     // split's last n % 4 bytes (the range check zero-fills that partial dword)
-    const uint64_t n4 = n & ~3ull, reach = kSlotBytes - kBack;
+    const uint64_t n4 = n & ~3ull, reach = kSlotBytes + kSlotTail - kBack;
     const uint32_t ctail = (n & 3) == 0 ? 0xFFFFFFFFu : n4 < reach ? 0u : (uint32_t)((n4 - reach) / kOwn + 1);
     const uint64_t g = wc_map_grid(n, grid);
     if (t.sp.nb == kSpillBucketsHi) {  // high-cardinality layout (ablation modes apply to the default one only)

@@ -72,6 +72,25 @@ def edge_cases() -> dict[str, list[bytes]]:
     }
 
 
+def long_words(n: int, seed: int) -> bytes:
+    """About n bytes of words of 17-70 bytes (ASCII, Greek, Deseret letters) drawn
+    from a 300-word vocabulary with a skewed law (hot long words repeat across
+    chunks and workgroups), separated by 1-2 ASCII / U+3001 separators: chunks
+    holding only words over 16 bytes (the long-word list and kernel)."""
+    rnd = random.Random(3000 + seed)
+    alph = ["abcdefghijklmnopqrstuvwxyz", "αβγδεζηθικλμνξοπρστυφχψω", "".join(chr(0x10400 + i) for i in range(40))]
+    vocab = []
+    for k in range(300):
+        a = alph[k % 3]
+        ln = rnd.randint(17, 70) // len(a[0].encode()) + 1
+        vocab.append("".join(rnd.choice(a) for _ in range(ln)).encode())
+    out = bytearray()
+    while len(out) < n:
+        out += vocab[min(int(rnd.paretovariate(0.7)) - 1, 299)]
+        out += rnd.choice([b" ", b"\n", b", ", "\u3001".encode()])
+    return bytes(out)
+
+
 def mixed_words(n: int, seed: int) -> bytes:
     """Deterministic text of exactly n bytes ending in a letter: words of 1-20
     letters (some longer than the 16-byte inline key) and 1-3 byte separators."""

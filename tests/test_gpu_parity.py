@@ -74,6 +74,21 @@ def test_wc_synthetic(wctx, kind, V, seed, inv):
         assert wctx.stats()["dict_hits"] > 0
 
 
+@pytest.mark.parametrize("list_cap", [0, 300])
+def test_wc_long_words_many(wctx, list_cap):
+    """Mixed-script text with many words over 16 bytes, and splits made only of
+    17-70-byte words: the map waves' reserved ranges of the long-word list and
+    their closing holes, the list overflow + re-run (a 300-entry list), and the
+    long-word kernel's LDS pre-aggregation of hot long words."""
+    files = cases.synthetic(C.KIND_UTF8, 20000, [2_000_000, 1_000_001], 21, 0.0005) + \
+        [cases.long_words(3_000_000, 1), cases.long_words(70_000, 2)]
+    wctx.set_option("list_cap", list_cap)
+    try:
+        check(wctx, "wc", files, nreduces=(1, 10))
+    finally:
+        wctx.set_option("list_cap", 0)
+
+
 def test_grep_synthetic(ctx):
     files = cases.synthetic_grep(50000, [3_000_000, 1_000_001], 5)
     check(ctx, "grep:distributed", files, nreduces=(1, 10))

@@ -40,6 +40,19 @@ def test_product_bitmap_equals_ucd():
         assert bool(bit) == _is_l(cp), hex(cp)
 
 
+def test_lds_letter_pages_bound():
+    """The map kernels keep l1[0, MRG_LETTER_LDS_PAGES) in LDS and treat code
+    points above it as non-letters (csrc/mrgpu_device.h is_letter_lds)."""
+    txt = open(os.path.join(ROOT, "distributed-systems-implemented_amd", "csrc", "letter_table.inc")).read()
+    pages = int(re.search(r"#define MRG_LETTER_LDS_PAGES (\d+)", txt).group(1))
+    hdr = open(os.path.join(ROOT, "distributed-systems-implemented_amd", "csrc", "mrgpu_internal.h")).read()
+    assert int(re.search(r"kLetterLdsPages = (\d+);", hdr).group(1)) == pages
+    assert int(re.search(r"kLetterUnique = (\d+);", hdr).group(1)) == int(
+        re.search(r"#define MRG_LETTER_NUNIQUE (\d+)", txt).group(1))
+    assert not any(_is_l(cp) for cp in range(pages << 8, 0x110000))
+    assert any(_is_l(cp) for cp in range((pages - 1) << 8, pages << 8))
+
+
 def test_oracle_ranges_equal_ucd():
     L = O.lib()
     for cp in list(range(0, 0x3400)) + list(range(0x3400, 0x110000, 7)):
