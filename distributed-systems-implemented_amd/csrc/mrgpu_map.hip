@@ -23,8 +23,8 @@ namespace mrg {
 // on its slot's atomics (mixed-script text has many words over 16 bytes: C2u's
 // 31 M occurrences took 136 ms that way).  Lost claim races and a full table
 // fall back to a direct HBM insert (exact either way).
-constexpr int kLongWG = 512;
-constexpr int kLongSlots = 2048;
+constexpr int kLongWG = 1024;    // one workgroup per CU
+constexpr int kLongSlots = 4096;  // 96 KB of LDS table
 constexpr unsigned long long kRepUnpub = ~0ull;
 struct alignas(16) LongLds {
     unsigned long long h[kLongSlots];    // hash | 1 (0: empty)
@@ -34,6 +34,20 @@ struct alignas(16) LongLds {
     uint32_t l2[kLetterUnique * 8];
     uint8_t l1[kLetterLdsPages];
 };
+
+// Byte j (0..31) of a 32-byte register window (two 16-byte blocks).
+__device__ __forceinline__ uint32_t win_byte(const uint4& a, const uint4& b, uint32_t j) {
+    const uint32_t d = j >> 2;
+    const uint32_t w = d == 0 ? a.x : d == 1 ? a.y : d == 2 ? a.z : d == 3 ? a.w : d == 4 ? b.x : d == 5 ? b.y : d == 6 ? b.z : b.w;
+    return (w >> (8 * (j & 3))) & 0xFFu;
+}
+__device__ __forceinline__ uint4 ld16_bounded(const uint8_t* in, uint64_t n, uint64_t at) {  // at: 16-byte aligned
+    if (at + 16 <= n) return *(const uint4*)(in + at);
+    uint32_t w[4] = {0, 0, 0, 0};
+    for (uint32_t k = 0; k < 16; k++)
+        if (at + k < n) w[k >> 2] |= (uint32_t)in[at + k] << (8 * (k & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+}
 
 __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restrict__ in, uint64_t n, Tables t,
                                                           LetterTables lt, uint64_t nlist) {
@@ -53,20 +67,37 @@ __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restr
     for (uint64_t i = b + threadIdx.x; i < e; i += kLongWG) {
         const uint64_t s = t.list[i];
         if (s == kListHole) continue;  // the unused rest of a map wave's reserved range
+        // decode forward through a 32-byte register window of aligned 16-byte
+        // loads (the next block requested a block ahead), not a chain of byte loads
+        uint64_t wb = s & ~15ull;
+        uint4 w0 = ld16_bounded(in, n, wb), w1 = ld16_bounded(in, n, wb + 16);
         uint64_t q = s, h = kFnv64Off;
         while (q < n) {
-            const uint32_t c0 = in[q];
+            if (q - wb >= 16) {  // slide: the rune at q and its 3 successors stay inside the window
+                wb += 16;
+                w0 = w1;
+                w1 = ld16_bounded(in, n, wb + 16);
+            }
+            const uint32_t j = (uint32_t)(q - wb);
+            const uint32_t c0 = win_byte(w0, w1, j);
             uint32_t vl = 1;
             bool let;
             if (c0 < 0x80u) {
                 let = ((c0 | 0x20u) - 0x61u) < 26u;
+                if (let) h = fnv1a64_step(h, c0);
             } else {
-                const uint32_t c1 = q + 1 < n ? in[q + 1] : 0, c2 = q + 2 < n ? in[q + 2] : 0, c3 = q + 3 < n ? in[q + 3] : 0;
+                const uint32_t c1 = q + 1 < n ? win_byte(w0, w1, j + 1) : 0, c2 = q + 2 < n ? win_byte(w0, w1, j + 2) : 0,
+                               c3 = q + 3 < n ? win_byte(w0, w1, j + 3) : 0;
                 vl = (uint32_t)utf8_valid_len(c0, c1, c2, c3);
                 let = vl != 0 && is_letter_lds(utf8_decode(c0, c1, c2, c3, (int)vl), L);
+                if (let) {
+                    h = fnv1a64_step(h, c0);
+                    if (vl > 1) h = fnv1a64_step(h, c1);
+                    if (vl > 2) h = fnv1a64_step(h, c2);
+                    if (vl > 3) h = fnv1a64_step(h, c3);
+                }
             }
             if (!let) break;
-            for (uint32_t k = 0; k < vl; k++) h = fnv1a64_step(h, in[q + k]);
             q += vl;
         }
         const uint32_t len = (uint32_t)(q - s);
@@ -88,7 +119,7 @@ __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restr
             if (cur == hk) {
                 const unsigned long long r = __hip_atomic_load(&A.rep[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
                 if (r == kRepUnpub) break;  // being published: never wait here, insert directly
-                if (A.len[slot] == len && bytes_equal(in + r, in + s, len)) {
+                if (A.len[slot] == len && (r == s || bytes_equal(in + r, in + s, len))) {
                     atomicAdd(&A.cnt[slot], 1u);
                     done = true;
                 }
@@ -769,9 +800,10 @@ void clear_tables(const Tables& t, bool short_table, hipStream_t s) {
 
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s) {
     if (nlist == 0) return;
-    // about 16 occurrences per lane, at most 4 workgroups per CU's worth
-    uint64_t g = (nlist + kLongWG * 16 - 1) / (kLongWG * 16);
-    if (g > 1024) g = 1024;
+    // one workgroup per CU (LDS-bound), each with a contiguous share of the list
+    uint64_t g = (nlist + kLongWG * 4 - 1) / (kLongWG * 4);
+    const uint64_t ncu = (uint64_t)map_grid_size(0);
+    if (g > ncu) g = ncu;
     wc_long_kernel<<<(unsigned)g, kLongWG, 0, s>>>(in, n, t, lt, nlist);
 }
 

@@ -43,9 +43,10 @@ constexpr int kAggThreads = 512;
 // rare non-ASCII path).  Neighbouring slots overlap by 32 bytes (re-read from
 // L2, not HBM).
 constexpr int kSlotBytes = 1024;
-// A slot is followed by the 4 input bytes after its window (a second, one-lane
-// DMA): a UTF-8 rune starting in the look-ahead lane's last 3 bytes is decoded
-// exactly.  Slots are 16-byte aligned.
+// A slot is followed by room for the 4 input bytes after its window: a UTF-8
+// rune starting in the look-ahead lane's last 3 bytes needs them, and they are
+// read from global memory only for such a chunk (a one-lane DMA per chunk for
+// them measured +11 % on C5's store-bound map kernel).  Slots are 16-byte aligned.
 constexpr int kSlotTail = 4;
 constexpr int kSlotStride = kSlotBytes + 16;
 constexpr int kOwnLanes = 62;
@@ -139,7 +140,7 @@ __device__ __forceinline__ uint32_t spill_bucket(uint32_t h) {
 // other memory operations (words > 16 bytes, chunks of more than kBatchWords
 // words, HBM-table overflow, UTF-8 table lookups) drain with vmcnt(0).
 constexpr uint32_t kOutOfRange = 0xFFFFFFF0u;
-constexpr int kVmemPerIter = 4;  // per chunk: one 8-byte and one 16-byte spill store, the DMA and its 4-byte tail
+constexpr int kVmemPerIter = 3;  // per chunk: one 8-byte and one 16-byte spill store, one DMA
 
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -170,38 +171,18 @@ __device__ __forceinline__ void dma_chunk(i32x4 rsrc, uint32_t voff, uint32_t ld
     else
         asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff), "s"(rsrc), "s"(lds_base)
                      : "memory", "m0");
-    // the 4 bytes after the window -> LDS [lds_base + 1024, +4): lane 0 alone
-    // (exec saved and restored inside the statement)
-#ifdef MRG_AB_NO_TAIL_DMA  // A/B only: ASCII splits exact, UTF-8 look-ahead wrong
-    return;
-#endif
-    unsigned long long saved;
-    asm volatile(
-        "s_mov_b64 %0, exec\n\ts_mov_b64 exec, 1\n\ts_mov_b32 m0, %3\n\t"
-        "buffer_load_dword %1, %2, 0 offen lds\n\ts_mov_b64 exec, %0"
-        : "=&s"(saved)
-        : "v"(voff + (uint32_t)kSlotBytes), "s"(rsrc), "s"(lds_base + (uint32_t)kSlotBytes)
-        : "memory", "m0");
 }
 __device__ __forceinline__ void wait_vmem_iter() {
-    static_assert(kVmemPerIter == 4, "update the immediate");
-#ifdef MRG_AB_NO_TAIL_DMA
+    static_assert(kVmemPerIter == 3, "update the immediate");
     asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
-#else
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-#endif
 }
 // The same after an iteration that issued kVmemWide spill stores (a chunk with
 // more than 64 dictionary misses appends from its word slots: 2 stores per
-// batch slot, no drain), + its DMA and tail.
+// batch slot, no drain), + its DMA.
 constexpr int kVmemWide = 2 * kBatch;
 __device__ __forceinline__ void wait_vmem_iter_wide() {
-    static_assert(kVmemWide + 2 == 8, "update the immediate");
-#ifdef MRG_AB_NO_TAIL_DMA
+    static_assert(kVmemWide + 1 == 7, "update the immediate");
     asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
-#else
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-#endif
 }
 __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
@@ -292,12 +273,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     const __amdgpu_buffer_rsrc_t rs16 = __builtin_amdgcn_make_buffer_rsrc(
         (void*)(t.sp.pool + (uint64_t)blockIdx.x * NB * sub), (short)0, (int)(NB * sub * 16u),
         0x00020000);
-    uint64_t ovf = 0, utf8_chunks = 0, acc = 0;
+    uint32_t ovf = 0, utf8_chunks = 0;
+    uint64_t acc = 0;
     // this wave's reserved range of the long-word list: [lbase, lbase + lleft)
     uint64_t lbase = 0;
     uint32_t lleft = 0;
-    const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)t.list, (short)0, (int)(t.list_cap * 8u < 0xFFFFFF00ull ? t.list_cap * 8u : 0xFFFFFF00ull), 0x00020000);
     const uint32_t ring0 = lds_addr(L.ring[wv][0]);
     static_assert(sizeof(L.ring) >= 4 * kWavesPerWG * sizeof(unsigned long long), "block_add4 scratch aliases the ring");
 
@@ -344,8 +324,22 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 mA = ascii_mask16(ca);
             } else {
                 // UTF-8: ASCII letters by SWAR, one loop turn per lead byte, letter
-                // tables in LDS (no memory operation: the counted DMA wait holds)
+                // tables in LDS.  A lead in the window's last 3 bytes whose sequence
+                // runs past it needs the input bytes after the window: read then
+                // (one lane; drained, so the counted wait still holds), else no
+                // memory operation.
                 utf8_chunks++;
+                const uint32_t tl = lane == 63 ? ca.w >> 8 : 0u;  // slot bytes 1021..1023
+                const uint32_t cross = ((tl & 0xF8u) >= 0xF0u ? 1u : 0u) | ((tl >> 8 & 0xF0u) >= 0xE0u ? 1u : 0u) |
+                                       ((tl >> 16 & 0xE0u) >= 0xC0u ? 1u : 0u);
+                if (__ballot(cross != 0)) {
+                    if (lane < (uint32_t)kSlotTail) {
+                        const uint64_t p = cs - kBack + kSlotBytes + lane;
+                        buf[kSlotBytes + lane] = p < n ? in[p] : (uint8_t)0;
+                    }
+                    wait_vmem_all();
+                    wave_sync();
+                }
                 mA = utf8_mask16(buf, 16 * lane, lane == 0, lds_lt);
             }
             // Word starts (a letter byte whose predecessor is not one) in the owned lanes
@@ -465,6 +459,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                 if (lbase + want > t.list_cap && lane == 0) set_status(t.ctr, kStListFull);
                                 wait_vmem_all();
                             }
+                            const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+                                (void*)t.list, (short)0,
+                                (int)(t.list_cap * 8u < 0xFFFFFF00ull ? t.list_cap * 8u : 0xFFFFFF00ull), 0x00020000);
                             const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
                             const uint64_t at = lbase + lane;
                             __builtin_amdgcn_raw_buffer_store_b64(
