@@ -1168,6 +1168,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set(c->rws, 0, v >= 0 ? 1 : 0, -1);
     } else if (!strcmp(name, "sort_compact_ties")) {  // tied runs merge-sorted on key copies (-1: on the records)
         reduce_ws_set_compact_ties(c->rws, v >= 0);
+    } else if (!strcmp(name, "sort_bins")) {  // wc reduce: hand-written sample sort (1) or rocPRIM (0, -1: default)
+        reduce_ws_set_bin_sort(c->rws, v > 0);
     } else if (!strcmp(name, "grep_sort_k1")) {  // grep radix over 16 key bytes (default) or 8 (-1)
         reduce_ws_set(c->rws, 0, -1, v >= 0 ? 1 : 0);
     } else if (!strcmp(name, "spill_hi_keys")) c->spill_hi_keys = v > 0 ? (uint64_t)v : 6000ull * kSpillBuckets;

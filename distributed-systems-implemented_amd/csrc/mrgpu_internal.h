@@ -224,6 +224,8 @@ void reduce_ws_free(ReduceWs*);
 void reduce_ws_set(ReduceWs*, int digit_bits, int fold_part, int grep_k1);
 // Tied runs merge-sorted on compact key copies (default) or on the records.
 void reduce_ws_set_compact_ties(ReduceWs*, bool on);
+// The single-key wc sort pass by the hand-written bucketed sort (default) or rocPRIM onesweep.
+void reduce_ws_set_bin_sort(ReduceWs*, bool on);
 // Sort recs (optionally only partition `only_part`), format "key value\n" lines.
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
 // ascii_keys: every key byte is < 0x80 (the sort key then packs 7 bits per byte).

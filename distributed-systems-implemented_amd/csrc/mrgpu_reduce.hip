@@ -18,6 +18,8 @@
 #include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
+#include <algorithm>
+
 #include "mrgpu_device.h"
 
 namespace mrg {
@@ -45,12 +47,16 @@ struct DBuf {
 };
 
 struct ReduceWs {
-    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext, tiek;
+    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext, tiek, bins;
     uint64_t* h_pinned = nullptr;  // small pinned staging
     int digit_bits = 0;            // radix digit of the 64-bit key passes: 8, 10, 0 = by app (grep 10, wc 8)
     bool fold_part = true;         // wc: partition folded into the top bits of the k0 sort key
     bool grep_k1 = true;           // grep: radix passes over the first 16 key bytes (else 8, more ties)
     bool compact_ties = true;      // tied runs merge-sorted on compact key copies (TieKey)
+    // single-key wc sorts by the hand-written sample sort below instead of rocPRIM
+    // onesweep: exact, but measured slower (C2 reduce 0.70 vs 0.42 ms, C5 4.4 vs
+    // 2.5 ms: its LDS bitonic bin sorts and scattered writes), so off by default
+    bool bin_sort = false;
 };
 
 void reduce_ws_set(ReduceWs* w, int digit_bits, int fold_part, int grep_k1) {
@@ -62,6 +68,8 @@ void reduce_ws_set(ReduceWs* w, int digit_bits, int fold_part, int grep_k1) {
 void reduce_ws_set_compact_ties(ReduceWs* w, bool on) { w->compact_ties = on;
 }
 
+void reduce_ws_set_bin_sort(ReduceWs* w, bool on) { w->bin_sort = on; }
+
 ReduceWs* reduce_ws_new() {
     ReduceWs* w = new ReduceWs();
     if (hipHostMalloc((void**)&w->h_pinned, 4096 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) w->h_pinned = nullptr;
@@ -70,13 +78,14 @@ ReduceWs* reduce_ws_new() {
 
 void reduce_ws_free(ReduceWs* w) {
     if (!w) return;
-    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek};
+    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek, &w->bins};
     for (DBuf* b : bs) b->release();
     if (w->h_pinned) hipHostFree(w->h_pinned);
     delete w;
 }
 
-// flags[2]: tied runs found, flags[3]: long runs (flags[0], flags[1]: unused).
+// flags[1]: a bin of the bucketed sort was too large (the sort falls back to
+// rocPRIM), flags[2]: tied runs found, flags[3]: long runs (flags[0]: unused).
 
 __global__ void iota_kernel(uint32_t* p, uint64_t n) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -504,6 +513,218 @@ __global__ void select_kernel(Recs src, uint32_t mod, uint32_t want, Recs dst, u
     }
 }
 
+// ------------------------------------------------------------ bucketed sort
+// The wc reduce's single 64-bit key pass ((partition, packed or folded key
+// prefix) per distinct key; keys + record indices), hand-written for the sizes
+// that matter (1e6 - 1e7 keys), in place of rocPRIM's onesweep (six or seven
+// ~25 us digit passes, each with two look-back memsets).  A sample sort:
+//   1. bin_sample_kernel: one workgroup sorts an evenly spaced sample of S keys
+//      in LDS (bitonic) and keeps every (S / nbins)-th as a splitter: the
+//      partition and key-prefix bits are far from uniform (10 partitions of
+//      16 bit patterns, 52 letters of 128, Zipf), so bins are cut by rank;
+//   2. bin_count_kernel: each of G workgroups bins its contiguous range of keys
+//      by binary search over the splitters in LDS (a key's bin = the number of
+//      splitters <= it: equal keys share a bin), keeps the bin per key, and
+//      writes its LDS histogram as H[group][bin];
+//   3. bin_offsets_kernel: per bin, the exclusive prefix over the groups (a
+//      coalesced column walk) and the bin total; bin_starts_kernel: exclusive
+//      scan of the totals;
+//   4. bin_scatter_kernel: each group places its keys at its bins' cursors (an
+//      LDS atomic per key; order inside a bin is free);
+//   5. bin_sort_kernel: workgroups stride over the bins and sort each in LDS
+//      (bitonic network over (key, index)): bins of <= 2048 keys by 256-thread
+//      workgroups, larger ones (<= 8192) by 1024-thread ones.
+// Equal keys end up adjacent in any order: tie runs are ordered by full key
+// comparison afterwards (fix_ties), exactly as after the radix sort.  A bin of
+// more than 8192 keys (thousands of keys tied on their first 8 bytes) sets
+// flags[1], and the caller repeats the pass with rocPRIM.
+// Measured (MI355X, rocprofv3): C2 (1e6 keys) sample 81 us, count 12, offsets
+// 58, scatter 25, bin sorts 92 us = 0.70 ms reduce against onesweep's 0.42; C5
+// (1e7) 1.6 ms of sort kernels against ~1.8 ms.  Option sort_bins=1 (tests run
+// both); the default stays rocPRIM.
+constexpr uint32_t kBinMax = 8192;        // bins at most (LDS: splitters + histogram)
+constexpr uint32_t kBinGroups = 256;      // count / scatter workgroups at most
+constexpr uint32_t kBinSample = 16384;    // sample keys at most (one LDS bitonic sort)
+constexpr uint32_t kBinSmall = 2048, kBinBig = 8192;
+
+// Bitonic sort of P (a power of two) (key, value) pairs in LDS by NT threads.
+template <uint32_t NT, class KT>
+__device__ __forceinline__ void lds_bitonic(KT* K, uint32_t* V, uint32_t P) {
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < P / 2; i += NT) {
+                const uint32_t a = 2 * i - (i & (j - 1)), c = a + j;  // pair (a, a + j), a's bit j clear
+                const auto ka = K[a], kc = K[c];
+                if ((ka > kc) == ((a & k) == 0)) {
+                    K[a] = kc;
+                    K[c] = ka;
+                    if (V) {
+                        const uint32_t t = V[a];
+                        V[a] = V[c];
+                        V[c] = t;
+                    }
+                }
+            }
+        }
+    __syncthreads();
+}
+
+__global__ void __launch_bounds__(1024) bin_sample_kernel(const uint64_t* keys, uint64_t n, uint32_t S, uint32_t nbins,
+                                                          uint64_t* spl) {
+    __shared__ uint64_t K[kBinSample];
+    for (uint32_t i = threadIdx.x; i < S; i += 1024) K[i] = keys[(uint64_t)i * n / S];
+    lds_bitonic<1024, uint64_t>(K, nullptr, S);
+    for (uint32_t j = threadIdx.x; j + 1 < nbins; j += 1024) spl[j] = K[(uint64_t)(j + 1) * S / nbins];
+}
+
+// the number of splitters <= k (nbins - 1 splitters, sorted)
+__device__ __forceinline__ uint32_t bin_of(const uint64_t* sp, uint32_t nbins, uint64_t k) {
+    uint32_t lo = 0, cnt = nbins - 1;  // upper bound over sp[0, nbins - 1)
+    while (cnt) {
+        const uint32_t half = cnt >> 1;
+        if (sp[lo + half] <= k) {
+            lo += half + 1;
+            cnt -= half + 1;
+        } else {
+            cnt = half;
+        }
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(1024) bin_count_kernel(const uint64_t* keys, uint64_t n, const uint64_t* spl,
+                                                         uint32_t nbins, uint16_t* kbin, uint32_t* H) {
+    __shared__ uint64_t sp[kBinMax];
+    __shared__ uint32_t h[kBinMax];
+    for (uint32_t i = threadIdx.x; i < nbins; i += 1024) {
+        h[i] = 0;
+        if (i + 1 < nbins) sp[i] = spl[i];
+    }
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b = (uint64_t)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 1024) {
+        const uint32_t bin = bin_of(sp, nbins, keys[i]);
+        kbin[i] = (uint16_t)bin;
+        atomicAdd(&h[bin], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbins; i += 1024) H[(uint64_t)blockIdx.x * nbins + i] = h[i];
+}
+
+// H[g][bin] -> exclusive prefix over g (in place, a coalesced column walk); tot[bin] = the bin's size
+__global__ void bin_offsets_kernel(uint32_t* H, uint32_t G, uint32_t nbins, uint32_t* tot) {
+    const uint32_t bin = blockIdx.x * blockDim.x + threadIdx.x;
+    if (bin >= nbins) return;
+    uint32_t run = 0;
+    for (uint32_t g = 0; g < G; g++) {
+        uint32_t* p = H + (uint64_t)g * nbins + bin;
+        const uint32_t v = *p;
+        *p = run;
+        run += v;
+    }
+    tot[bin] = run;
+}
+
+// start[bin] = exclusive scan of tot (one workgroup)
+__global__ void __launch_bounds__(1024) bin_starts_kernel(const uint32_t* tot, uint32_t nbins, uint32_t* start) {
+    __shared__ uint32_t part[1024];
+    const uint32_t per = (nbins + 1023) / 1024, t = threadIdx.x;
+    uint32_t a = 0;
+    for (uint32_t q = 0; q < per; q++)
+        if (t * per + q < nbins) a += tot[t * per + q];
+    part[t] = a;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const uint32_t x = t >= d ? part[t - d] : 0u;
+        __syncthreads();
+        part[t] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[t] - a;
+    for (uint32_t q = 0; q < per; q++)
+        if (t * per + q < nbins) {
+            start[t * per + q] = run;
+            run += tot[t * per + q];
+        }
+}
+
+__global__ void __launch_bounds__(1024) bin_scatter_kernel(const uint64_t* keys, uint64_t n, const uint16_t* kbin,
+                                                           uint32_t nbins, const uint32_t* H, const uint32_t* start,
+                                                           uint64_t* kout, uint32_t* vout) {
+    __shared__ uint32_t cur[kBinMax];
+    for (uint32_t i = threadIdx.x; i < nbins; i += 1024) cur[i] = start[i] + H[(uint64_t)blockIdx.x * nbins + i];
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b = (uint64_t)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 1024) {
+        const uint32_t pos = atomicAdd(&cur[kbin[i]], 1u);
+        kout[pos] = keys[i];
+        vout[pos] = (uint32_t)i;  // the keys were gathered in record order
+    }
+}
+
+// Sort bins of size (lo, CAP] in place; workgroups stride over the bins.  Padding
+// keys are ~0, which no real key equals (key bytes are never 0xFF); a bin over
+// the largest CAP flags the fallback.
+template <uint32_t CAP, uint32_t NT>
+__global__ void __launch_bounds__(NT) bin_sort_kernel(uint64_t* keys, uint32_t* vals, const uint32_t* start,
+                                                      const uint32_t* tot, uint32_t nbins, uint32_t lo, bool flag_over,
+                                                      unsigned long long* flags) {
+    __shared__ uint64_t K[CAP];
+    __shared__ uint32_t V[CAP];
+    for (uint32_t bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
+        const uint32_t m = tot[bin];
+        if (m > CAP) {
+            if (flag_over && threadIdx.x == 0) atomicOr(&flags[1], 1ull);
+            continue;
+        }
+        if (m <= lo || m < 2) continue;
+        uint32_t P = 2;
+        while (P < m) P <<= 1;
+        const uint64_t s0 = start[bin];
+        for (uint32_t i = threadIdx.x; i < P; i += NT) {
+            K[i] = i < m ? keys[s0 + i] : ~0ull;
+            V[i] = i < m ? vals[s0 + i] : 0u;
+        }
+        lds_bitonic<NT, uint64_t>(K, V, P);
+        for (uint32_t i = threadIdx.x; i < m; i += NT) {
+            keys[s0 + i] = K[i];
+            vals[s0 + i] = V[i];
+        }
+        __syncthreads();  // LDS reused by the workgroup's next bin
+    }
+}
+
+// keys gathered in record order -> kout sorted, vout the record indices.
+// Scratch in ws->bins.
+static int bin_sort_pass(ReduceWs* ws, const uint64_t* keys, uint64_t* kout, uint32_t* vout, uint64_t n,
+                         unsigned long long* flags, hipStream_t s) {
+    uint32_t nbins = 256;
+    while (nbins < kBinMax && (uint64_t)nbins * 700 < n) nbins <<= 1;
+    uint32_t S = 4 * nbins;
+    if (S > kBinSample) S = kBinSample;
+    while (S > n && S > 2) S >>= 1;  // (tiny inputs: a sample of distinct positions)
+    const uint32_t G = (uint32_t)std::min<uint64_t>(kBinGroups, (n + 4095) / 4096);
+    const size_t hbytes = (size_t)G * nbins * 4, kb = (n * 2 + 15) & ~15ull;
+    if (hipError_t e = ws->bins.ensure(hbytes + 2 * (size_t)nbins * 4 + (size_t)nbins * 8 + kb + 64)) return (int)e;
+    uint32_t* H = ws->bins.as<uint32_t>();
+    uint32_t* tot = H + (size_t)G * nbins;
+    uint32_t* start = tot + nbins;
+    uint64_t* spl = (uint64_t*)(start + nbins);
+    uint16_t* kbin = (uint16_t*)(spl + nbins);
+    bin_sample_kernel<<<1, 1024, 0, s>>>(keys, n, S, nbins, spl);
+    bin_count_kernel<<<G, 1024, 0, s>>>(keys, n, spl, nbins, kbin, H);
+    bin_offsets_kernel<<<(nbins + 255) / 256, 256, 0, s>>>(H, G, nbins, tot);
+    bin_starts_kernel<<<1, 1024, 0, s>>>(tot, nbins, start);
+    bin_scatter_kernel<<<G, 1024, 0, s>>>(keys, n, kbin, nbins, H, start, kout, vout);
+    bin_sort_kernel<kBinSmall, 256><<<nbins < 2048 ? nbins : 2048, 256, 0, s>>>(kout, vout, start, tot, nbins, 0, false,
+                                                                                  flags);
+    bin_sort_kernel<kBinBig, 1024><<<256, 1024, 0, s>>>(kout, vout, start, tot, nbins, kBinSmall, true, flags);
+    return (int)hipGetLastError();
+}
+
 static inline unsigned grid_for(uint64_t n) {
     uint64_t g = (n + 255) / 256;
     if (g < 1) g = 1;
@@ -731,11 +952,20 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     // skipped at first: keys that share their first 8 bytes form short tied runs
     // that fix_ties orders by full comparison; if a run is long (many keys with
     // one 8-byte prefix), everything is sorted again with the k1 pass.
+    // the single-key pass by the hand-written bucketed sort (bins of the
+    // partition and the first key bits); rocPRIM when a bin overflowed
+    bool use_bins = ws->bin_sort;
+    auto bin_pass = [&](int which, uint32_t fold_bits) -> int {
+        gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, nullptr, n, which, ws->key_a.as<uint64_t>(), nullptr, fold_bits);
+        int e = bin_sort_pass(ws, ws->key_a.as<uint64_t>(), ws->key_b.as<uint64_t>(), pb, n, flags, s);
+        std::swap(pa, pb);
+        return e;
+    };
     auto sort_all = [&](bool with_k1) -> int {
         int e;
         keys_sorted = !with_k1 && (packed || fold);
-        if (!with_k1 && packed) return pass64(5, 0, true, 56 + pbits);
-        if (!with_k1 && fold) return pass64(4, fold, true);
+        if (!with_k1 && packed) return use_bins ? bin_pass(5, 0) : pass64(5, 0, true, 56 + pbits);
+        if (!with_k1 && fold) return use_bins ? bin_pass(4, fold) : pass64(4, fold, true);
         if (with_k1) {
             if ((e = pass64(1, 0, true))) return e;
             if ((e = pass64(2))) return e;
@@ -784,6 +1014,12 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         // 9-16-byte keys, or longer ones; <= 8-byte keys differ within 2^fold)
         bool any_long = false;
         if ((e = fix_ties(false, false, &any_long))) return e;
+        if (use_bins && keys_sorted && ws->h_pinned[1]) {  // a bin overflowed: the whole pass again with rocPRIM
+            use_bins = false;
+            RCHK(hipMemsetAsync(flags + 1, 0, 8, s));
+            if ((e = sort_all(false))) return e;
+            if ((e = fix_ties(false, false, &any_long))) return e;
+        }
         if (any_long) {
             if ((e = sort_all(true))) return e;
             if ((e = fix_ties(true, true, &any_long))) return e;

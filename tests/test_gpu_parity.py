@@ -223,6 +223,29 @@ def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact):
         ctx.set_option("sort_compact_ties", 0)
 
 
+@pytest.mark.parametrize("bins", [1, 0])
+def test_reduce_bucketed_sort(ctx, bins):
+    """The wc reduce's hand-written sample sort (option sort_bins=1) against
+    rocPRIM (the default): splitters from a sorted sample, a skewed input
+    (20 000 distinct words starting with 'q'), > 8192 keys tied on their first 8
+    bytes (an overflowing bin: the rocPRIM fallback), ties of the packed / folded key,
+    UTF-8 keys (the folded key), 1e5+ distinct keys."""
+    rnd = np.random.default_rng(7)
+    qwords = [b"q" + bytes(rnd.integers(97, 123, size=int(rnd.integers(1, 12))).astype(np.uint8)) for _ in range(20000)]
+    # 10 000 keys tied on their first 8 bytes: one sample-sort bin of > 8192 equal
+    # sort keys (the pass falls back to rocPRIM) and a long tied run
+    tied = [b"abcdefgh" + bytes(rnd.integers(97, 123, size=int(rnd.integers(1, 8))).astype(np.uint8)) for _ in range(10000)]
+    skew = b" ".join(qwords + tied) + b"\n"
+    files = [skew] + cases.synthetic(C.KIND_ASCII, 300000, [3_000_000], 43) + \
+        cases.synthetic(C.KIND_UTF8, 100000, [2_000_000], 44, 0.001)
+    ctx.set_option("sort_bins", bins)
+    try:
+        check(ctx, "wc", files, nreduces=(1, 10, 64))
+        check(ctx, "wc", [skew], nreduces=(1, 2))
+    finally:
+        ctx.set_option("sort_bins", 0)
+
+
 def test_wc_large_vs_oracle(wctx):
     """64 MB C2-style corpus: full bytes vs the C oracle."""
     voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
