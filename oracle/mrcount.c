@@ -277,7 +277,7 @@ int oracle_count_mt(int app, const uint8_t* pat, size_t pn, const uint8_t* s, si
     uint8_t* o = (uint8_t*)malloc(bytes ? bytes : 1);
     uint64_t on = 0;
     for (uint32_t r = 0; r < nreduce; r++) {
-        qsort(sorted + pc[r], pc[r + 1] - pc[r], sizeof(ckey), ckey_cmp);
+        if (pc[r + 1] - pc[r] > 1) qsort(sorted + pc[r], pc[r + 1] - pc[r], sizeof(ckey), ckey_cmp);
         offsets[r] = on;
         for (uint64_t i = pc[r]; i < pc[r + 1]; i++) {
             const ckey* k = &sorted[i];

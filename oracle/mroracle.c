@@ -179,7 +179,7 @@ static void ob_put(obuf* o, const void* p, size_t n) {
 
 /* sort + group + Reduce + Fprintf("%v %v\n") — worker.go:123-146, mrsequential.go:59-84. */
 static void group_reduce(int app, okey* v, size_t n, obuf* out) {
-    qsort(v, n, sizeof(okey), key_cmp);
+    if (n > 1) qsort(v, n, sizeof(okey), key_cmp);  /* (v may be NULL when n == 0) */
     size_t i = 0;
     char num[32];
     while (i < n) {
