@@ -201,6 +201,82 @@ __device__ __forceinline__ void dma_for_chunk(const uint8_t* in, uint64_t n, uin
     dma_chunk<kPol>(raw_rsrc(in + base, nrec), (uint32_t)(cs - base) - kBack + 16u * lane, lds_base);
 }
 
+// The map loop's rare paths (long words, full spill streams) read the Tables
+// fields they need through this laundered reference: hipcc cannot hoist those
+// kernarg loads out of the branch, so the pointers stay out of the SGPRs the
+// hot path needs (hoisted, they pushed the loop's DMA scalars into VGPR-lane
+// spills reloaded every chunk).
+// (The reference is formed from the kernarg segment pointer: the kernel's
+// arguments are laid out like the members of MapArgs; taking the parameter's
+// own address would copy the struct to scratch.)
+struct MapArgs {
+    const uint8_t* in;
+    uint64_t n;
+    uint32_t cbeg, cend, ctail;
+    int resume;
+    Tables t;
+    LetterTables lt;
+};
+// cold(): a generic reference (rare paths: flat loads, drained anyway);
+// cold_list(): the long-word list's base and capacity by scalar loads (the
+// single-pass long-word path runs on most chunks of mixed-script text, where a
+// flat load would drain the DMA pipeline).
+#ifndef MRG_NO_COLD_REF
+__device__ __forceinline__ const Tables& cold(const Tables&) {
+    const char* p = (const char*)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    return *(const Tables*)(p + offsetof(MapArgs, t));
+}
+__device__ __forceinline__ void cold_list(const Tables&, uint64_t*& list, uint64_t& cap) {
+    typedef const __attribute__((address_space(4))) char* kptr;
+    kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    const __attribute__((address_space(4))) Tables* tp = (const __attribute__((address_space(4))) Tables*)(p + offsetof(MapArgs, t));
+    list = tp->list;
+    cap = tp->list_cap;
+}
+#else
+__device__ __forceinline__ const Tables& cold(const Tables& t) { return t; }
+__device__ __forceinline__ void cold_list(const Tables& t, uint64_t*& list, uint64_t& cap) {
+    list = t.list;
+    cap = t.list_cap;
+}
+#endif
+// the split's address and size, for the loop's rare paths (scalar loads)
+__device__ __forceinline__ void cold_input(const uint8_t*& in, uint64_t& n) {
+    typedef const __attribute__((address_space(4))) char* kptr;
+    kptr p = (kptr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(p));
+    const __attribute__((address_space(4))) MapArgs* ap = (const __attribute__((address_space(4))) MapArgs*)p;
+    in = ap->in;
+    n = ap->n;
+}
+
+// The map loop's DMA stream, advanced incrementally: the descriptor (base =
+// the window start rounded down to 1 GiB, range = bytes to the split's end)
+// changes only when the window offset passes 3 GiB, so a chunk's DMA costs one
+// 32-bit add instead of recomputing the 64-bit base and range (~30 scalar
+// instructions per chunk).  rebase() reads the split's address and size from
+// the kernarg segment (a rare path: they need no SGPRs in the loop).
+struct DmaStream {
+    uint32_t base_lo, base_hi, nrec;  // descriptor words 0-2 (word 3 is constant)
+    uint32_t voff;                    // offset of the window start (chunk start - 16) from the base
+    __device__ __forceinline__ void set(const uint8_t* in, uint64_t n, uint64_t cs) {
+        const uint64_t base = cs == 0 ? 0 : ((cs - kBack) & ~((1ull << 30) - 1));
+        const uint64_t r = n - base;
+        const uint32_t rhi = (uint32_t)(r >> 32), rlo = (uint32_t)r;
+        nrec = (int32_t)rhi < 0 ? 0u : (rhi != 0 || rlo > 0xFFFFFF00u) ? 0xFFFFFF00u : rlo;
+        const uint64_t b = (uint64_t)(in + base);
+        base_lo = (uint32_t)b;
+        base_hi = (uint32_t)(b >> 32) & 0xFFFFu;
+        voff = (uint32_t)(cs - base) - kBack;
+    }
+    template <int kPol>
+    __device__ __forceinline__ void issue(uint32_t lane, uint32_t lds_base) const {
+        dma_chunk<kPol>((i32x4){(int)base_lo, (int)base_hi, (int)nrec, 0x00020000}, voff + 16u * lane, lds_base);
+    }
+};
+
 // Long-word list: each map wave reserves kLongReserve entries at a time; the
 // unused rest of a range is closed with kListHole entries (skipped by
 // wc_long_kernel).
@@ -287,6 +363,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn, lane, ring0);
     wait_vmem_all();
     dma_for_chunk<dma_policy(mode)>(in, n, (uint64_t)c0 * kOwn + cstep, lane, ring0 + kSlotStride);
+    // the stream of the chunk two strides ahead (the loop's DMA)
+    DmaStream ds;
+    ds.set(in, n, (uint64_t)c0 * kOwn + 2 * cstep);
+    const uint32_t cstep32 = (uint32_t)cstep;  // < 2^23: one add per chunk
     uint32_t k = 0;  // ring slot of the current chunk
     uint64_t cs = (uint64_t)c0 * kOwn;  // the current chunk's first own byte = slot byte 16 (slot byte i = input cs - 16 + i)
     // kf = the free slot (the word list now, chunk c + 2*stride next) = the slot
@@ -306,8 +386,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         lds_u16* list = (lds_u16*)L.ring[wv][kf];
         if (c >= ctail) {  // the window reaches the split's last n % 4 bytes (ctail = ~0u: none)
             // the split's last n % 4 bytes sit in a dword the range check zero-filled
-            const int64_t p = (int64_t)(n & ~3ull) + lane - ((int64_t)cs - kBack);
-            if (lane < (uint32_t)(n & 3) && p >= 0 && p < kSlotBytes + kSlotTail) buf[p] = in[(n & ~3ull) + lane];
+            const uint8_t* cin;
+            uint64_t cn;
+            cold_input(cin, cn);
+            const int64_t p = (int64_t)(cn & ~3ull) + lane - ((int64_t)cs - kBack);
+            if (lane < (uint32_t)(cn & 3) && p >= 0 && p < kSlotBytes + kSlotTail) buf[p] = cin[(cn & ~3ull) + lane];
             wait_vmem_all();
             wave_sync();
         }
@@ -334,8 +417,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                        ((tl >> 16 & 0xE0u) >= 0xC0u ? 1u : 0u);
                 if (__ballot(cross != 0)) {
                     if (lane < (uint32_t)kSlotTail) {
+                        const uint8_t* cin;
+                        uint64_t cn;
+                        cold_input(cin, cn);
                         const uint64_t p = cs - kBack + kSlotBytes + lane;
-                        buf[kSlotBytes + lane] = p < n ? in[p] : (uint8_t)0;
+                        buf[kSlotBytes + lane] = p < cn ? cin[p] : (uint8_t)0;
                     }
                     wait_vmem_all();
                     wave_sync();
@@ -448,32 +534,35 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                     lst[nlong + mbcnt64(mLng[u])] = cs - kBack + (e[u] & 0x3FFu);
                                 nlong += (uint32_t)__popcll(mLng[u]);
                             }
+                            const Tables& tc = cold(t);
                             if (nlong > lleft) {  // a fresh range (rare): close the old one, one atomic, drain
-                                list_close(t, lbase, lleft, lane);
+                                list_close(tc, lbase, lleft, lane);
                                 const uint32_t want = kLongReserve;
                                 unsigned long long b0 = 0;
-                                if (lane == 0) b0 = atomicAdd(&t.ctr->nlist, (unsigned long long)want);
+                                if (lane == 0) b0 = atomicAdd(&tc.ctr->nlist, (unsigned long long)want);
                                 lbase = __builtin_amdgcn_readfirstlane((uint32_t)b0) |
                                         ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b0 >> 32)) << 32);
                                 lleft = want;
-                                if (lbase + want > t.list_cap && lane == 0) set_status(t.ctr, kStListFull);
+                                if (lbase + want > tc.list_cap && lane == 0) set_status(tc.ctr, kStListFull);
                                 wait_vmem_all();
                             }
+                            uint64_t* lptr;
+                            uint64_t lcap;
+                            cold_list(t, lptr, lcap);
                             const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
-                                (void*)t.list, (short)0,
-                                (int)(t.list_cap * 8u < 0xFFFFFF00ull ? t.list_cap * 8u : 0xFFFFFF00ull), 0x00020000);
+                                (void*)lptr, (short)0, (int)(lcap * 8u < 0xFFFFFF00ull ? lcap * 8u : 0xFFFFFF00ull), 0x00020000);
                             const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
                             const uint64_t at = lbase + lane;
                             __builtin_amdgcn_raw_buffer_store_b64(
                                 (u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
-                                lane < nlong && at < t.list_cap && at < (1ull << 29) ? (uint32_t)(at * 8u) : kOutOfRange,
+                                lane < nlong && at < lcap && at < (1ull << 29) ? (uint32_t)(at * 8u) : kOutOfRange,
                                 0, 0);
                             lbase += nlong;
                             lleft -= nlong;
                         } else {  // several passes (> 192 words): the list slot is still needed
         #pragma unroll
                             for (int u = 0; u < kBatch; u++)
-                                if (__builtin_amdgcn_inverse_ballot_w64(mLng[u])) list_append(t, cs - kBack + (e[u] & 0x3FFu));
+                                if (__builtin_amdgcn_inverse_ballot_w64(mLng[u])) list_append(cold(t), cs - kBack + (e[u] & 0x3FFu));
                             wait_vmem_all();
                         }
                     }
@@ -588,8 +677,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint64_t mOver = __ballot(valid) & ((mBigS & ~mF16) | (~mBigS & ~mF8));
                         if (mOver) {  // a stream is full: count in the HBM table; the bucket then merges through it
                             if (__builtin_amdgcn_inverse_ballot_w64(mOver)) {
-                                short_insert(t, ((uint64_t)r.y << 32) | r.x, ((uint64_t)r.w << 32) | r.z, 1);
-                                t.bflag[b] = 1u;
+                                const Tables& tc = cold(t);
+                                short_insert(tc, ((uint64_t)r.y << 32) | r.x, ((uint64_t)r.w << 32) | r.z, 1);
+                                tc.bflag[b] = 1u;
                                 ovf++;
                             }
                             wait_vmem_all();
@@ -624,8 +714,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint64_t mOver = mMiss[u] & ((mBig[u] & ~mFit16) | (~mBig[u] & ~mFit8));
                         if (mOver) {  // rare: HBM-table inserts, then drain (the counted wait assumes stores only)
                             if (__builtin_amdgcn_inverse_ballot_w64(mOver)) {
-                                short_insert(t, k0[u], k1[u], 1);
-                                t.bflag[b] = 1u;
+                                const Tables& tc = cold(t);
+                                short_insert(tc, k0[u], k1[u], 1);
+                                tc.bflag[b] = 1u;
                                 ovf++;
                             }
                             wait_vmem_all();
@@ -644,7 +735,14 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         }
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
-        dma_for_chunk<dma_policy(mode)>(in, n, cs + 2 * cstep, lane, ring0 + kf * kSlotStride);
+        ds.issue<dma_policy(mode)>(lane, ring0 + kf * kSlotStride);
+        ds.voff += cstep32;
+        if (ds.voff >= (3u << 30)) {  // rare: the window moved 2 GiB past the base
+            const uint8_t* cin;
+            uint64_t cn;
+            cold_input(cin, cn);
+            ds.set(cin, cn, cs + 3 * cstep);
+        }
     }
     list_close(t, lbase, lleft, lane);
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
@@ -1740,6 +1838,10 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     const uint64_t n4 = n & ~3ull, reach = kSlotBytes + kSlotTail - kBack;
     const uint32_t ctail = (n & 3) == 0 ? 0xFFFFFFFFu : n4 < reach ? 0u : (uint32_t)((n4 - reach) / kOwn + 1);
     const uint64_t g = wc_map_grid(n, grid);
+#ifdef MRG_ISA_MAIN_ONLY  // (ISA inspection builds: the default map kernel only)
+    wc_map_kernel<0, kWavesPerWG, kSpillBucketsLo><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
+    return true;
+#endif
     if (t.sp.nb == kSpillBucketsHi) {  // high-cardinality layout (ablation modes apply to the default one only)
         wc_map_kernel<0, 12, kSpillBucketsHi><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
         return true;
