@@ -218,6 +218,7 @@ struct mrg_ctx {
     int spill_alt = 0;
     DevBuf bflag, dict, dict_cnt, sample, recbuf, recarena, sortbuf, dbg;
     DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
+    bool seg_sync = true;               // size the miss segments from this split's totals (host read)
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     DevBuf ghits, glines, gdefer;        // grep: sorted hits, resolved (start, end) lines, deferred hits
     int agg_rounds = 8;                 // bucket aggregation rounds at most (the last sends leftovers to HBM)
@@ -364,6 +365,7 @@ static Tables make_tables(mrg_ctx* c) {
     t.sp.seg8_out = nullptr;
     t.sp.seg16_in = nullptr;
     t.sp.seg16_out = nullptr;
+    t.sp.seg8_cap = t.sp.seg16_cap = 0;
     t.sp.round = 0;
     t.sp.last = 1;
     t.sp.carry_min = c->agg_carry_min;
@@ -520,6 +522,7 @@ static int grow_on_overflow(mrg_ctx* c, uint32_t st) {
     if (st & kStLongFull) { c->lo_log2_cur += 2; again = 1; }
     if (st & kStListFull) { c->list_cap = std::max<uint64_t>(c->list_cap * 4, c->h_ctr->nlist + 1024); again = 1; }
     if (st & kStRecFull) { c->rec_cap = std::max<uint64_t>(c->rec_cap * 2, c->h_ctr->nrec + 4096); again = 1; }
+    if (st & kStSegFull) { c->seg_sync = true; again = 1; }
     return again;
 }
 
@@ -704,14 +707,24 @@ static int aggregate_rounds(mrg_ctx* c, Tables& t) {
     uint64_t* off16 = off8 + E + 1;
     uint32_t* cnt[2] = {(uint32_t*)(off16 + E + 1), (uint32_t*)(off16 + E + 1) + 2 * E};
     launch_seg_layout(t, tmp, off8, off16, c->s);
-    uint64_t* tot = c->h_scr;  // pinned
-    HCHK(c, hipMemcpyAsync(&tot[0], off8 + E, 8, hipMemcpyDeviceToHost, c->s));
-    HCHK(c, hipMemcpyAsync(&tot[1], off16 + E, 8, hipMemcpyDeviceToHost, c->s));
-    HCHK(c, hipStreamSynchronize(c->s));
-    for (int i = 0; i < 2; i++) {
-        HCHK(c, c->seg8[i].ensure_grow(tot[0] * 8 + 64));
-        HCHK(c, c->seg16[i].ensure_grow(tot[1] * 16 + 64));
+    // The segment buffers hold every record a round may carry (the records round
+    // 0 reads).  Sized from this split's totals with a host read the first time
+    // (or after a miss overflowed them: kStSegFull, the run repeats); later splits
+    // reuse them unread (a worker's map tasks are alike) and the aggregator
+    // checks each miss against the capacity.
+    if (c->seg_sync || !c->seg8[0].p || !c->seg16[0].p) {
+        uint64_t* tot = c->h_scr;  // pinned
+        HCHK(c, hipMemcpyAsync(&tot[0], off8 + E, 8, hipMemcpyDeviceToHost, c->s));
+        HCHK(c, hipMemcpyAsync(&tot[1], off16 + E, 8, hipMemcpyDeviceToHost, c->s));
+        HCHK(c, hipStreamSynchronize(c->s));
+        for (int i = 0; i < 2; i++) {
+            HCHK(c, c->seg8[i].ensure_grow(tot[0] * 8 + 64));
+            HCHK(c, c->seg16[i].ensure_grow(tot[1] * 16 + 64));
+        }
+        c->seg_sync = false;
     }
+    t.sp.seg8_cap = std::min(c->seg8[0].cap, c->seg8[1].cap) / 8;
+    t.sp.seg16_cap = std::min(c->seg16[0].cap, c->seg16[1].cap) / 16;
     t.sp.seg_off8 = off8;
     t.sp.seg_off16 = off16;
     const int rounds = std::max(1, c->agg_rounds);
@@ -903,7 +916,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             if (agg_keys > c->spill_hi_keys) c->next_nb = kSpillBucketsHi;
             else if (agg_keys < c->spill_hi_keys / 3 * 2) c->next_nb = kSpillBucketsLo;
         }
-        if (grow_on_overflow(c, h.status & (kStShortFull | kStLongFull | kStRecFull))) continue;
+        if (grow_on_overflow(c, h.status & (kStShortFull | kStLongFull | kStRecFull | kStSegFull))) continue;
         if (h.long_bytes + 16 > c->recarena.cap) {  // the arena is written by collect below
             HCHK(c, c->recarena.ensure_cached(h.long_bytes + 16, c->device));
             t.out = rec_view(c);
@@ -1168,6 +1181,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set(c->rws, 0, v >= 0 ? 1 : 0, -1);
     } else if (!strcmp(name, "sort_compact_ties")) {  // tied runs merge-sorted on key copies (-1: on the records)
         reduce_ws_set_compact_ties(c->rws, v >= 0);
+    } else if (!strcmp(name, "sort_prefix32")) {  // wc reduce: single pass on the top 32 key bits (1, default) or all (0)
+        reduce_ws_set_prefix32(c->rws, v != 0);
     } else if (!strcmp(name, "sort_bins")) {  // wc reduce: hand-written sample sort (1) or rocPRIM (0, -1: default)
         reduce_ws_set_bin_sort(c->rws, v > 0);
     } else if (!strcmp(name, "grep_sort_k1")) {  // grep radix over 16 key bytes (default) or 8 (-1)

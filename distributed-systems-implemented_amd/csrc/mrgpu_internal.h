@@ -28,6 +28,7 @@ enum : uint32_t {
     kStListFull = 1u << 2,
     kStSpin = 1u << 3,
     kStRecFull = 1u << 4,   // the record output buffer was too small
+    kStSegFull = 1u << 5,   // an aggregation miss segment buffer was too small (sized without a host read)
 };
 
 struct ShortSlot {
@@ -102,6 +103,7 @@ struct Spill {
     uint64_t* seg8_out;
     const uint4* seg16_in;
     uint4* seg16_out;
+    uint64_t seg8_cap, seg16_cap;    // records the seg*_out buffers hold (a miss past them sets kStSegFull)
     uint32_t round;                  // 0: the input is the map's spill streams; > 0: seg*_in
     uint32_t last;                   // nonzero: unsettled misses go to the HBM table (final round)
     uint32_t carry_min;              // a bucket with fewer misses than this settles them in the HBM table
@@ -226,6 +228,8 @@ void reduce_ws_set(ReduceWs*, int digit_bits, int fold_part, int grep_k1);
 void reduce_ws_set_compact_ties(ReduceWs*, bool on);
 // The single-key wc sort pass by the hand-written bucketed sort (default) or rocPRIM onesweep.
 void reduce_ws_set_bin_sort(ReduceWs*, bool on);
+// The wc single-key pass on the key's top 32 bits (default) or the whole 60/64-bit key.
+void reduce_ws_set_prefix32(ReduceWs*, bool on);
 // Sort recs (optionally only partition `only_part`), format "key value\n" lines.
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
 // ascii_keys: every key byte is < 0x80 (the sort key then packs 7 bits per byte).

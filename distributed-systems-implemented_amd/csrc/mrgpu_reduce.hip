@@ -57,6 +57,10 @@ struct ReduceWs {
     // onesweep: exact, but measured slower (C2 reduce 0.70 vs 0.42 ms, C5 4.4 vs
     // 2.5 ms: its LDS bitonic bin sorts and scattered writes), so off by default
     bool bin_sort = false;
+    // the wc single-key pass sorts only the key's top 32 bits ((partition, first
+    // key bits): four 8-bit onesweep passes over u32 keys instead of six 10-bit
+    // passes over u64 ones); keys tied on them are ordered by fix_ties
+    bool prefix32 = true;
 };
 
 void reduce_ws_set(ReduceWs* w, int digit_bits, int fold_part, int grep_k1) {
@@ -69,6 +73,7 @@ void reduce_ws_set_compact_ties(ReduceWs* w, bool on) { w->compact_ties = on;
 }
 
 void reduce_ws_set_bin_sort(ReduceWs* w, bool on) { w->bin_sort = on; }
+void reduce_ws_set_prefix32(ReduceWs* w, bool on) { w->prefix32 = on; }
 
 ReduceWs* reduce_ws_new() {
     ReduceWs* w = new ReduceWs();
@@ -108,7 +113,8 @@ __device__ __forceinline__ uint64_t pack7(uint64_t k0) {
 
 // which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part, 4 = part in the top
 // `fold` bits over bswap(k0) >> fold (the first 64 - fold key bits), 5 = part
-// over pack7(k0) (ASCII keys: 56 + fold bits, nothing dropped).
+// over pack7(k0) (ASCII keys: 56 + fold bits, nothing dropped); 6 / 7 = the
+// top 32 bits of the 5 / 4 key (u32).
 __global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32,
                                   uint32_t fold = 0) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -119,6 +125,8 @@ __global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int 
         else if (which == 2) k64[i] = __builtin_bswap64(r.k0[j]);
         else if (which == 4) k64[i] = ((uint64_t)r.part[j] << (64 - fold)) | (__builtin_bswap64(r.k0[j]) >> fold);
         else if (which == 5) k64[i] = ((uint64_t)r.part[j] << 56) | pack7(r.k0[j]);
+        else if (which == 6) k32[i] = (uint32_t)((((uint64_t)r.part[j] << 56) | pack7(r.k0[j])) >> 28);  // 60-bit key's top 32
+        else if (which == 7) k32[i] = (uint32_t)((((uint64_t)r.part[j] << (64 - fold)) | (__builtin_bswap64(r.k0[j]) >> fold)) >> 32);
         else k32[i] = r.part[j];
     }
 }
@@ -129,6 +137,16 @@ __global__ void mark_ties_sorted_kernel(const uint64_t* keys, uint64_t n, uint8_
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint8_t t = i > 0 && keys[i] == keys[i - 1] ? 1 : 0;  // (coalesced: no record gathers)
+        tie[i] = t;
+        if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
+    }
+}
+
+// The same on sorted u32 keys (the 32-bit prefix pass).
+__global__ void mark_ties_sorted32_kernel(const uint32_t* keys, uint64_t n, uint8_t* tie, unsigned long long* flags) {
+    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint8_t t = i > 0 && keys[i] == keys[i - 1] ? 1 : 0;
         tie[i] = t;
         if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
     }
@@ -948,6 +966,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     // first 8 bytes) loses nothing and sorts 56 + pbits bits
     const bool packed = ws->fold_part && ascii_keys && pbits <= 8 && !grep;
     bool keys_sorted = false;  // key_b holds the sort keys of the single (partition, prefix) pass
+    bool keys32 = false;       // ... as u32 (the 32-bit prefix pass)
     // Stable LSD passes: (k1), k0, partition.  The k1 pass (bytes 8-15) is
     // skipped at first: keys that share their first 8 bytes form short tied runs
     // that fix_ties orders by full comparison; if a run is long (many keys with
@@ -964,6 +983,15 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     auto sort_all = [&](bool with_k1) -> int {
         int e;
         keys_sorted = !with_k1 && (packed || fold);
+        keys32 = keys_sorted && ws->prefix32 && !use_bins;
+        if (keys32) {  // top 32 bits of the (partition, prefix) key: u32 pairs, 4 passes
+            gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, nullptr, n, packed ? 6 : 7, nullptr, ws->key_a.as<uint32_t>(),
+                                                          fold);
+            iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
+            e = sort_pass<uint32_t>(ws, ws->key_a.as<uint32_t>(), ws->key_b.as<uint32_t>(), pa, pb, n, 32, s);
+            std::swap(pa, pb);
+            return e;
+        }
         if (!with_k1 && packed) return use_bins ? bin_pass(5, 0) : pass64(5, 0, true, 56 + pbits);
         if (!with_k1 && fold) return use_bins ? bin_pass(4, fold) : pass64(4, fold, true);
         if (with_k1) {
@@ -984,7 +1012,8 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         uint8_t* lng = tie + n;
         RCHK(hipMemsetAsync(lng, 0, n, s));
         RCHK(hipMemsetAsync(flags + 2, 0, 16, s));
-        if (!with_k1 && keys_sorted) mark_ties_sorted_kernel<<<grid_for(n), 256, 0, s>>>(ws->key_b.as<uint64_t>(), n, tie, flags);
+        if (!with_k1 && keys32) mark_ties_sorted32_kernel<<<grid_for(n), 256, 0, s>>>(ws->key_b.as<uint32_t>(), n, tie, flags);
+        else if (!with_k1 && keys_sorted) mark_ties_sorted_kernel<<<grid_for(n), 256, 0, s>>>(ws->key_b.as<uint64_t>(), n, tie, flags);
         else mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, with_k1, with_k1 ? 0u : fold);
         if (all_runs) {  // every tied run goes to the merge sort (no per-run insertion sort)
             mark_all_ties_kernel<<<grid_for(n), 256, 0, s>>>(tie, n, lng);

@@ -952,13 +952,19 @@ __device__ __forceinline__ void defer_miss(AL& A, const Tables& t, uint64_t k0, 
     if (keep_miss) {
         const uint32_t sg = wv % kAggSegs;  // the wave's segment (kParts waves share one)
         const uint64_t seg = (uint64_t)blockIdx.x * kAggSegs + sg;
+        // (the buffers are sized from an earlier split's layout unless the host
+        // read this one's: a miss past them flags the run, which is repeated)
         if (k1 == 0) {
             const uint32_t pos = atomicAdd(&A.ncur8[sg], 1u);
-            t.sp.seg8_out[t.sp.seg_off8[seg] + pos] = k0;
+            const uint64_t at = t.sp.seg_off8[seg] + pos;
+            if (at < t.sp.seg8_cap) t.sp.seg8_out[at] = k0;
+            else set_status(t.ctr, kStSegFull);
         } else {
             const uint32_t pos = atomicAdd(&A.ncur16[sg], 1u);
-            t.sp.seg16_out[t.sp.seg_off16[seg] + pos] =
-                make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+            const uint64_t at = t.sp.seg_off16[seg] + pos;
+            if (at < t.sp.seg16_cap)
+                t.sp.seg16_out[at] = make_uint4((uint32_t)k0, (uint32_t)(k0 >> 32), (uint32_t)k1, (uint32_t)(k1 >> 32));
+            else set_status(t.ctr, kStSegFull);
         }
     }
     miss++;

@@ -186,7 +186,9 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        process prints the phase and exits with status 124
  *   sort_digit_bits (8, 10), sort_fold_part (-1: off), grep_sort_k1 (-1: 8-byte
  *                                        prefix passes only), sort_compact_ties (-1:
- *                                        off)   reduce sort variants */
+ *                                        off), sort_bins (1: sample sort), sort_prefix32
+ *                                        (0: the wc key pass over all 60/64 bits instead
+ *                                        of the top 32)   reduce sort variants */
 int mrg_set_option(mrg_ctx* ctx, const char* name, int64_t value);
 
 uint32_t mrg_ihash(const uint8_t* key, size_t n);

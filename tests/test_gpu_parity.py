@@ -223,10 +223,12 @@ def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact):
         ctx.set_option("sort_compact_ties", 0)
 
 
-@pytest.mark.parametrize("bins", [1, 0])
-def test_reduce_bucketed_sort(ctx, bins):
-    """The wc reduce's hand-written sample sort (option sort_bins=1) against
-    rocPRIM (the default): splitters from a sorted sample, a skewed input
+@pytest.mark.parametrize("bins,prefix32", [(1, 1), (0, 1), (0, 0)])
+def test_reduce_bucketed_sort(ctx, bins, prefix32):
+    """The wc reduce's key pass variants: the hand-written sample sort (option
+    sort_bins=1), rocPRIM on the key's top 32 bits (the default: ties of the
+    first ~4 characters ordered by full comparison) and rocPRIM on the whole
+    60/64-bit key (sort_prefix32=0): splitters from a sorted sample, a skewed input
     (20 000 distinct words starting with 'q'), > 8192 keys tied on their first 8
     bytes (an overflowing bin: the rocPRIM fallback), ties of the packed / folded key,
     UTF-8 keys (the folded key), 1e5+ distinct keys."""
@@ -239,11 +241,13 @@ def test_reduce_bucketed_sort(ctx, bins):
     files = [skew] + cases.synthetic(C.KIND_ASCII, 300000, [3_000_000], 43) + \
         cases.synthetic(C.KIND_UTF8, 100000, [2_000_000], 44, 0.001)
     ctx.set_option("sort_bins", bins)
+    ctx.set_option("sort_prefix32", prefix32)
     try:
         check(ctx, "wc", files, nreduces=(1, 10, 64))
         check(ctx, "wc", [skew], nreduces=(1, 2))
     finally:
         ctx.set_option("sort_bins", 0)
+        ctx.set_option("sort_prefix32", 1)
 
 
 def test_wc_large_vs_oracle(wctx):
