@@ -214,6 +214,7 @@ struct mrg_ctx {
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
+    DevBuf shl;  // the ShortTable's claim list
     DevBuf spool_alt;     // diagnostic option spill_alt_pools: a second spill pool, the two alternate per split
     int spill_alt = 0;
     DevBuf bflag, dict, dict_cnt, sample, recbuf, recarena, sortbuf, dbg;
@@ -346,6 +347,7 @@ static Tables make_tables(mrg_ctx* c) {
     t.hits = (const uint64_t*)c->ghits.p;
     t.lines = (uint64_t*)c->glines.p;
     t.defer = (uint64_t*)c->gdefer.p;
+    t.sh_list = (uint32_t*)c->shl.p;
     t.list = (uint64_t*)c->list.p;
     t.list_cap = c->list_cap;
     t.ctr = (Counters*)c->ctr.p;
@@ -426,6 +428,7 @@ static int ensure_spill(mrg_ctx* c, uint64_t n) {
 static int ensure_tables(mrg_ctx* c) {
     const void* old = c->sh.p;
     HCHK(c, c->sh.ensure(sizeof(ShortSlot) << c->sh_log2));
+    HCHK(c, c->shl.ensure(sizeof(uint32_t) << c->sh_log2));
     if (c->sh.p != old) c->sh_clean = false;  // fresh memory is not zeroed
     HCHK(c, c->bflag.ensure(kSpillBucketsHi * sizeof(uint32_t)));
     const size_t lo_bytes = sizeof(LongSlot) << c->lo_log2_cur;
@@ -500,7 +503,8 @@ static int collect_parts(mrg_ctx* c, int app, uint32_t nreduce, mrg_parts** out)
     t.nreduce = nreduce;
     const bool sh_used = h.short_used != 0, lo_used = h.long_used != 0;
     HCHK(c, hipMemsetAsync(&t.ctr->nrec, 0, 3 * sizeof(unsigned long long), c->s));
-    if (launch_collect(t, c->rws, 0, sh_used ? h.short_used : 0, lo_used, c->s))
+    (void)sh_used;
+    if (launch_collect(t, lo_used, c->s))
         return fail(c, MRG_EDEVICE, "collect failed");
     rc = read_counters(c);
     if (rc) { mrg_parts_free(p); return rc; }
@@ -896,17 +900,23 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         if (have_dict) launch_dict_emit(t, nwg, c->s);
         HCHK(c, hipEventRecord(c->ev[8], c->s));
         HCHK(c, hipGetLastError());
-        if ((rc = read_counters(c))) return rc;
-        if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
-        const uint64_t nlist = c->h_ctr->nlist;
-        if (nlist) {  // words > 16 bytes
-            launch_wc_long(in, len, t, lt, nlist, c->s);
-            HCHK(c, hipGetLastError());
-        }
+        // Words > 16 bytes, then the HBM tables' keys (aggregator leftovers, long
+        // words) appended to the records, every count read on the device; one host
+        // read of the counters afterwards checks every capacity (an overflow grows
+        // what filled up and repeats the attempt).
+        launch_wc_long(in, len, t, lt, ~0ull, c->s);
+        HCHK(c, hipGetLastError());
         HCHK(c, hipEventRecord(c->ev[2], c->s));
-        if (nlist && (rc = read_counters(c))) return rc;
+        if (launch_collect(t, c->lo_log2_cur > 0, c->s)) return fail(c, MRG_EDEVICE, "collect failed");
+        if ((rc = read_counters(c))) return rc;
         Counters h = *c->h_ctr;
         if (h.status & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", h.status);
+        if ((h.status & kStRecFull) && h.long_bytes + 16 > c->recarena.cap) {  // the arena first (collect_long)
+            HCHK(c, c->recarena.ensure_cached(h.long_bytes + 16, c->device));
+            if (h.nrec <= c->rec_cap) continue;  // only the arena was short
+        }
+        if (grow_on_overflow(c, h.status & (kStListFull | kStShortFull | kStLongFull | kStRecFull | kStSegFull)))
+            continue;
         {
             // Bucket count for the next split (a worker's map tasks are alike):
             // the aggregated keys (records minus the dictionary's) against what
@@ -916,16 +926,6 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             if (agg_keys > c->spill_hi_keys) c->next_nb = kSpillBucketsHi;
             else if (agg_keys < c->spill_hi_keys / 3 * 2) c->next_nb = kSpillBucketsLo;
         }
-        if (grow_on_overflow(c, h.status & (kStShortFull | kStLongFull | kStRecFull | kStSegFull))) continue;
-        if (h.long_bytes + 16 > c->recarena.cap) {  // the arena is written by collect below
-            HCHK(c, c->recarena.ensure_cached(h.long_bytes + 16, c->device));
-            t.out = rec_view(c);
-        }
-        if ((h.short_used || h.long_used) && launch_collect(t, c->rws, h.nrec, h.short_used, h.long_used != 0, c->s))
-            return fail(c, MRG_EDEVICE, "collect failed");
-        if ((h.short_used || h.long_used) && (rc = read_counters(c))) return rc;
-        h = *c->h_ctr;
-        if (grow_on_overflow(c, h.status & kStRecFull)) continue;
         // the parts object takes over the record buffer and arena (no copy); the
         // next map task gets cached blocks
         mrg_parts* p = new mrg_parts();
@@ -1132,7 +1132,7 @@ void mrg_close(mrg_ctx* c) {
     hipSetDevice(c->device);
     if (c->s) hipStreamSynchronize(c->s);
     if (c->comm) ncclCommDestroy(c->comm);
-    DevBuf* bs[] = {&c->sh, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spool_alt, &c->spmeta,
+    DevBuf* bs[] = {&c->sh, &c->shl, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spool_alt, &c->spmeta,
                     &c->bflag, &c->dict, &c->dict_cnt, &c->sample, &c->recbuf, &c->recarena, &c->sortbuf,
                     &c->segmeta, &c->seg8[0], &c->seg8[1], &c->seg16[0], &c->seg16[1]};
     for (DevBuf* b : bs) b->release();

@@ -418,7 +418,7 @@ __device__ inline bool bytes_equal(const uint8_t* a, const uint8_t* b, uint64_t 
 enum : int { kDone = 0, kRetry = 1, kFull = 2, kClaimed = 3 };
 constexpr uint32_t kMaxRetries = 1u << 20;
 
-__device__ inline int short_try(const Tables& t, uint64_t k0, uint64_t k1, uint64_t cnt) {
+__device__ inline int short_try(const Tables& t, uint64_t k0, uint64_t k1, uint64_t cnt, uint64_t& slot) {
     uint64_t i = short_hash64(k0, k1) & t.sh_mask;
     for (uint32_t probes = 0; probes <= (uint32_t)kGlobalProbes; probes++) {
         ShortSlot* s = &t.sh[i];
@@ -428,6 +428,7 @@ __device__ inline int short_try(const Tables& t, uint64_t k0, uint64_t k1, uint6
             if (prev == 0) {
                 st_agent(&s->k1, k1);
                 atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                slot = i;
                 return kClaimed;
             }
             cur = prev;
@@ -458,19 +459,33 @@ __device__ __forceinline__ void count_claims(unsigned long long* used_ctr, uint6
     }
 }
 
+// A claim also records its slot in the claim list (the collect reads the list
+// instead of scanning the whole table).
 __device__ inline void short_insert(const Tables& t, uint64_t k0, uint64_t k1, uint64_t cnt) {
     bool pending = true;
     uint32_t tries = 0;
     while (__ballot(pending)) {  // wave-uniform: reconverges between attempts
         bool claimed = false;
+        uint64_t slot = 0;
         if (pending) {
-            const int r = short_try(t, k0, k1, cnt);
+            const int r = short_try(t, k0, k1, cnt, slot);
             if (r == kFull) set_status(t.ctr, kStShortFull);
             claimed = r == kClaimed;
             pending = r == kRetry;
             if (pending && ++tries > kMaxRetries) { set_status(t.ctr, kStSpin); pending = false; }
         }
-        count_claims(&t.ctr->short_used, t.sh_mask + 1, claimed, t.ctr, kStShortFull);
+        const uint64_t m = __ballot(claimed);
+        if (m == 0) continue;
+        const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+        unsigned long long base = 0;
+        if (lane_id() == leader) {  // one atomic per wave; the fill check on the wave's post-increment total
+            const unsigned long long k = (unsigned long long)__popcll(m);
+            base = atomicAdd(&t.ctr->short_used, k);
+            if ((base + k) * 10 > (t.sh_mask + 1) * 7) set_status(t.ctr, kStShortFull);
+        }
+        base = __shfl(base, (int)leader);
+        const uint64_t at = base + mbcnt64(m);
+        if (claimed && at <= t.sh_mask) t.sh_list[at] = (uint32_t)slot;
     }
 }
 

@@ -135,6 +135,7 @@ struct Recs {
 struct Tables {
     ShortSlot* sh;
     uint64_t sh_mask;
+    uint32_t* sh_list;   // [sh_mask + 1] indices of the claimed ShortTable slots, in claim order (ctr->short_used)
     LongSlot* lo;
     uint64_t lo_mask;
     uint64_t* list;      // u64 offsets (long-word starts / grep match positions)
@@ -193,6 +194,7 @@ void launch_sample_gather(const uint8_t* in, uint64_t n, uint64_t win, uint64_t 
 void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s);
 // Sort keys for the dictionary build: ~count (u32) of each record.
 void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t s);
+// nlist = ~0: the list length is read on the device (ctr->nlist; nothing to do if 0)
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s);
 void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t, int grid,
                      hipStream_t s, uint64_t cbeg = 0, uint64_t cend = ~0ull);
@@ -212,7 +214,11 @@ struct ReduceWs;
 // Append the HBM tables' keys to t.out: the ShortTable's `short_used` keys at
 // records [base, base + short_used) (ctr->nrec must equal base), then the
 // LongTable's at ctr->nrec (arena offsets from ctr->arena).  Returns 0 or a hipError_t.
-int launch_collect(const Tables& t, ReduceWs* ws, uint64_t base, uint64_t short_used, bool long_table, hipStream_t s);
+// Append the HBM tables' keys to t.out at ctr->nrec, every count read on the
+// device (no host round trip): the ShortTable's claimed slots from its claim
+// list, then (long_table) the LongTable's keys with their arena bytes.
+// Capacity overflows set kStRecFull.  Returns 0 or a hipError_t.
+int launch_collect(const Tables& t, bool long_table, hipStream_t s);
 void launch_insert_recs(const Recs& src, const Tables& t, hipStream_t s);
 int map_grid_size(int device);
 

@@ -52,6 +52,11 @@ __device__ __forceinline__ uint4 ld16_bounded(const uint8_t* in, uint64_t n, uin
 __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restrict__ in, uint64_t n, Tables t,
                                                           LetterTables lt, uint64_t nlist) {
     __shared__ LongLds A;
+    if (nlist == ~0ull) {  // the map's list length, read here (workgroup-uniform)
+        const uint64_t m = t.ctr->nlist;
+        nlist = m < t.list_cap ? m : t.list_cap;
+        if (nlist == 0) return;
+    }
     for (uint32_t i = threadIdx.x; i < (uint32_t)kLongSlots; i += kLongWG) {
         A.h[i] = 0;
         A.rep[i] = kRepUnpub;
@@ -604,13 +609,17 @@ __global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __r
 // ------------------------------------------------------------ collect
 // ShortTable: the occupied slots are compacted by rocprim select first
 // (select_used_short), so record i is written at base + i with no shared cursor.
-__global__ void collect_short_kernel(Tables t, const uint32_t* idx, const uint32_t* d_count, uint64_t base) {
-    const uint64_t n = *d_count;
+// The ShortTable's claimed slots (its claim list, ctr->short_used entries) as
+// records at ctr->nrec; nrec_add_kernel then advances ctr->nrec past them.
+__global__ void collect_short_kernel(Tables t) {
+    const uint64_t used = t.ctr->short_used;
+    const uint64_t n = used < t.sh_mask + 1 ? used : t.sh_mask + 1;
+    const uint64_t base = t.ctr->nrec;  // (nothing moves it during this kernel)
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t o = base + i;
         if (o >= t.out_cap) { set_status(t.ctr, kStRecFull); continue; }
-        const ShortSlot s = t.sh[idx[i]];
+        const ShortSlot s = t.sh[t.sh_list[i]];
         const uint32_t len = key_len_short(s.k0, s.k1);
         t.out.k0[o] = s.k0;
         t.out.k1[o] = s.k1;
@@ -621,7 +630,10 @@ __global__ void collect_short_kernel(Tables t, const uint32_t* idx, const uint32
     }
 }
 
-__global__ void nrec_add_kernel(Counters* ctr, const uint32_t* d_count) { ctr->nrec += *d_count; }
+__global__ void nrec_add_kernel(Tables t) {
+    const uint64_t used = t.ctr->short_used;
+    t.ctr->nrec += used < t.sh_mask + 1 ? used : t.sh_mask + 1;
+}
 
 // One LongTable record: key bytes copied to the arena at `off` by aligned
 // 16-byte blocks (the representative sits at a random input offset: one load
@@ -675,6 +687,7 @@ __device__ __forceinline__ bool emit_long_rec(const Tables& t, const LongSlot& s
 constexpr int kCollectSlots = 2;
 __global__ void __launch_bounds__(kLineWG) collect_long_kernel(Tables t) {
     __shared__ unsigned long long scratch[2 * kLineWaves + 2];
+    if (t.ctr->long_used == 0) return;  // (launched without a host read of the count; workgroup-uniform)
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint64_t n = t.lo_mask + 1;
     constexpr uint64_t kStep = 64 * kCollectSlots;
@@ -801,7 +814,8 @@ void clear_tables(const Tables& t, bool short_table, hipStream_t s) {
 void launch_wc_long(const uint8_t* in, uint64_t n, const Tables& t, LetterTables lt, uint64_t nlist, hipStream_t s) {
     if (nlist == 0) return;
     // one workgroup per CU (LDS-bound), each with a contiguous share of the list
-    uint64_t g = (nlist + kLongWG * 4 - 1) / (kLongWG * 4);
+    // (nlist = ~0, read on the device: every CU)
+    uint64_t g = nlist == ~0ull ? ~0ull : (nlist + kLongWG * 4 - 1) / (kLongWG * 4);
     const uint64_t ncu = (uint64_t)map_grid_size(0);
     if (g > ncu) g = ncu;
     wc_long_kernel<<<(unsigned)g, kLongWG, 0, s>>>(in, n, t, lt, nlist);
@@ -840,16 +854,9 @@ void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, hip
     grep_insert_kernel<<<(unsigned)((nlines + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, t, nlines);
 }
 
-int launch_collect(const Tables& t, ReduceWs* ws, uint64_t base, uint64_t short_used, bool long_table, hipStream_t s) {
-    if (short_used) {
-        uint32_t *idx = nullptr, *cnt = nullptr;
-        const int e = select_used_short(ws, t.sh, t.sh_mask + 1, short_used, &idx, &cnt, s);
-        if (e) return e;
-        uint64_t g = (short_used + 255) / 256;
-        if (g > 2048) g = 2048;
-        collect_short_kernel<<<(unsigned)g, 256, 0, s>>>(t, idx, cnt, base);
-        nrec_add_kernel<<<1, 1, 0, s>>>(t.ctr, cnt);
-    }
+int launch_collect(const Tables& t, bool long_table, hipStream_t s) {
+    collect_short_kernel<<<512, 256, 0, s>>>(t);
+    nrec_add_kernel<<<1, 1, 0, s>>>(t);
     if (long_table) {
         const uint64_t steps = (t.lo_mask + 1 + 64 * kCollectSlots - 1) / (64 * kCollectSlots);  // wave steps
         const uint64_t g = (steps + kLineWaves - 1) / kLineWaves < 512 ? (steps + kLineWaves - 1) / kLineWaves : 512;

@@ -114,7 +114,7 @@ __device__ __forceinline__ uint64_t pack7(uint64_t k0) {
 // which: 0 = len, 1 = bswap(k1), 2 = bswap(k0), 3 = part, 4 = part in the top
 // `fold` bits over bswap(k0) >> fold (the first 64 - fold key bits), 5 = part
 // over pack7(k0) (ASCII keys: 56 + fold bits, nothing dropped); 6 / 7 = the
-// top 32 bits of the 5 / 4 key (u32).
+// top 32 bits of the 5 / 4 key (u32; for 6, fold = the partition bits).
 __global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int which, uint64_t* k64, uint32_t* k32,
                                   uint32_t fold = 0) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -125,7 +125,8 @@ __global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int 
         else if (which == 2) k64[i] = __builtin_bswap64(r.k0[j]);
         else if (which == 4) k64[i] = ((uint64_t)r.part[j] << (64 - fold)) | (__builtin_bswap64(r.k0[j]) >> fold);
         else if (which == 5) k64[i] = ((uint64_t)r.part[j] << 56) | pack7(r.k0[j]);
-        else if (which == 6) k32[i] = (uint32_t)((((uint64_t)r.part[j] << 56) | pack7(r.k0[j])) >> 28);  // 60-bit key's top 32
+        else if (which == 6)  // top 32 bits of the (56 + fold)-bit packed key (fold = the partition bits here)
+            k32[i] = (uint32_t)((((uint64_t)r.part[j] << 56) | pack7(r.k0[j])) >> (24 + fold));
         else if (which == 7) k32[i] = (uint32_t)((((uint64_t)r.part[j] << (64 - fold)) | (__builtin_bswap64(r.k0[j]) >> fold)) >> 32);
         else k32[i] = r.part[j];
     }
@@ -986,7 +987,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         keys32 = keys_sorted && ws->prefix32 && !use_bins;
         if (keys32) {  // top 32 bits of the (partition, prefix) key: u32 pairs, 4 passes
             gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, nullptr, n, packed ? 6 : 7, nullptr, ws->key_a.as<uint32_t>(),
-                                                          fold);
+                                                          packed ? pbits : fold);
             iota_kernel<<<grid_for(n), 256, 0, s>>>(pa, n);
             e = sort_pass<uint32_t>(ws, ws->key_a.as<uint32_t>(), ws->key_b.as<uint32_t>(), pa, pb, n, 32, s);
             std::swap(pa, pb);

@@ -1513,7 +1513,15 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
     const uint32_t sg = wv % kAggSegs, i0 = lane + kWave * (wv / kAggSegs);
     constexpr uint32_t kStep = kWave * AL::kParts;
     const uint64_t seg = b * kAggSegs + sg;
-    const uint32_t n8 = keep_miss ? A.ncur8[sg] : 0u, n16 = keep_miss ? A.ncur16[sg] : 0u;
+    // (misses past the segment buffers' capacity were dropped and flagged: only
+    // the stored ones are read; the flagged run is repeated)
+    uint32_t n8 = keep_miss ? A.ncur8[sg] : 0u, n16 = keep_miss ? A.ncur16[sg] : 0u;
+    if (keep_miss) {
+        const uint64_t o8 = t.sp.seg_off8[seg], o16 = t.sp.seg_off16[seg];
+        const uint64_t room8 = o8 < t.sp.seg8_cap ? t.sp.seg8_cap - o8 : 0, room16 = o16 < t.sp.seg16_cap ? t.sp.seg16_cap - o16 : 0;
+        if (n8 > room8) n8 = (uint32_t)room8;
+        if (n16 > room16) n16 = (uint32_t)room16;
+    }
     uint64_t* s8 = keep_miss ? t.sp.seg8_out + t.sp.seg_off8[seg] : nullptr;
     uint4* s16 = keep_miss ? t.sp.seg16_out + t.sp.seg_off16[seg] : nullptr;
     // merge: a key of this bucket went to the HBM table from the map kernel
