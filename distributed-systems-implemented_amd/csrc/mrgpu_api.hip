@@ -220,6 +220,7 @@ struct mrg_ctx {
     DevBuf bflag, dict, dict_cnt, sample, recbuf, recarena, sortbuf, dbg;
     DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
     bool seg_sync = true;               // size the miss segments from this split's totals (host read)
+    bool out_direct = true;             // mrg_run_job: output lines written straight into pinned host memory
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     DevBuf ghits, glines, gdefer;        // grep: sorted hits, resolved (start, end) lines, deferred hits
     int agg_rounds = 8;                 // bucket aggregation rounds at most (the last sends leftovers to HBM)
@@ -1181,6 +1182,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set(c->rws, 0, v >= 0 ? 1 : 0, -1);
     } else if (!strcmp(name, "sort_compact_ties")) {  // tied runs merge-sorted on key copies (-1: on the records)
         reduce_ws_set_compact_ties(c->rws, v >= 0);
+    } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default) or via a copy (-1)
+        c->out_direct = v >= 0;
     } else if (!strcmp(name, "sort_prefix32")) {  // wc reduce: single pass on the top 32 key bits (1, default) or all (0)
         reduce_ws_set_prefix32(c->rws, v != 0);
     } else if (!strcmp(name, "sort_bins")) {  // wc reduce: hand-written sample sort (1) or rocPRIM (0, -1: default)
@@ -1667,12 +1670,13 @@ int mrg_parts_import(mrg_ctx* c, const void* bytes, size_t nb, mrg_parts** out) 
     return MRG_OK;
 }
 
-static int reduce_common(mrg_ctx* c, const mrg_parts* p, uint32_t only, uint8_t** d_out, uint64_t* n_out, uint64_t* offsets) {
+static int reduce_common(mrg_ctx* c, const mrg_parts* p, uint32_t only, uint8_t** d_out, uint64_t* n_out, uint64_t* offsets,
+                         uint8_t* hout = nullptr, uint64_t hout_cap = 0) {
     int rc;
     if ((rc = bind(c))) return rc;
     HCHK(c, hipEventRecord(c->ev[4], c->s));
     if (only == 0xFFFFFFFFu) {
-        rc = reduce_format(c->rws, p->r, p->app, p->nreduce, only, d_out, n_out, offsets, c->s, p->ascii);
+        rc = reduce_format(c->rws, p->r, p->app, p->nreduce, only, d_out, n_out, offsets, c->s, p->ascii, hout, hout_cap);
         if (rc) return fail(c, MRG_EDEVICE, "reduce_format: %s", hipGetErrorString((hipError_t)rc));
     } else {
         mrg_parts* sel = nullptr;
@@ -2082,11 +2086,33 @@ int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, cons
         if (rc) return rc;
         use = o;
     }
+    // wc: the output lines are written straight into the context's pinned host
+    // buffer by the formatting kernel (sized for the output's bound up front), so
+    // the transfer overlaps the formatting and the copy's host round trip goes
+    // (C2: 0.56 -> 0.50 ms for reduce + transfer).  grep keeps the device buffer
+    // + copy: its ~160-byte lines overflow the kernel's LDS staging in some
+    // blocks, whose byte-wise stores to host memory made the direct write slower
+    // than the copy (C3 2.66 vs 2.63 ms).  Option out_direct = -1: always the copy.
+    const bool direct_ok = c->out_direct && use->app == MRG_APP_WC;
+    const uint64_t bound = reduce_out_bound(use->r, use->app) + 1;
+    const uint64_t need = direct_ok ? bound : 0;
+    if (need > c->h_out_cap) {
+        if (c->h_out) hipHostFree(c->h_out);
+        c->h_out = nullptr;
+        c->h_out_cap = 0;
+        size_t cap = need + need / 4 + 4096;
+        if (hipHostMalloc((void**)&c->h_out, cap, hipHostMallocDefault) != hipSuccess) {
+            mrg_parts_free(use);
+            return fail(c, MRG_ENOMEM, "pinned output alloc");
+        }
+        c->h_out_cap = cap;
+    }
     uint8_t* d = nullptr;
     uint64_t n = 0;
-    rc = reduce_common(c, use, 0xFFFFFFFFu, &d, &n, offsets);
+    rc = reduce_common(c, use, 0xFFFFFFFFu, &d, &n, offsets, direct_ok ? c->h_out : nullptr, c->h_out_cap);
     if (rc) { mrg_parts_free(use); return rc; }
-    if (n + 1 > c->h_out_cap) {
+    const bool direct = d == c->h_out;
+    if (!direct && n + 1 > c->h_out_cap) {
         if (c->h_out) hipHostFree(c->h_out);
         c->h_out = nullptr;
         c->h_out_cap = 0;
@@ -2098,7 +2124,7 @@ int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, cons
         c->h_out_cap = cap;
     }
     HCHK(c, hipEventRecord(c->ev[6], c->s));
-    if (n) HCHK(c, hipMemcpyAsync(c->h_out, d, n, hipMemcpyDeviceToHost, c->s));
+    if (n && !direct) HCHK(c, hipMemcpyAsync(c->h_out, d, n, hipMemcpyDeviceToHost, c->s));
     HCHK(c, hipEventRecord(c->ev[7], c->s));
     HCHK(c, hipEventSynchronize(c->ev[7]));
     keep.reduce_ms = ev_ms(c->ev[4], c->ev[5]);

@@ -240,7 +240,11 @@ void reduce_ws_set_prefix32(ReduceWs*, bool on);
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
 // ascii_keys: every key byte is < 0x80 (the sort key then packs 7 bits per byte).
 int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,
-                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s, bool ascii_keys);
+                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s, bool ascii_keys, uint8_t* hout = nullptr,
+                  uint64_t hout_cap = 0);
+// Bytes reduce_format's output can take at most (its buffer, or a host buffer
+// given as hout: the lines are then written straight into pinned host memory).
+uint64_t reduce_out_bound(const Recs& r, int app);
 // Indices of occupied ShortTable slots; *d_count (device) = how many.
 int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64_t max_used, uint32_t** d_idx,
                       uint32_t** d_count, hipStream_t s);

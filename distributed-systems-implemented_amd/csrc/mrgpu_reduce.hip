@@ -891,8 +891,19 @@ int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs
     return 0;
 }
 
+uint64_t reduce_out_bound(const Recs& r, int app) {
+    // a wc line is key + ' ' + <= 20 digits + '\n', a grep line key + ' ' + key + '\n';
+    // key bytes past 16 live in the arena
+    const uint64_t key_bound = 16 * r.n + r.arena_n;
+    return app == 1 ? key_bound + 22 * r.n + 16 : 2 * key_bound + 2 * r.n + 16;
+}
+
+// hout (pinned host memory of hout_cap bytes, or null): the output lines are
+// written there directly by the formatting kernel (its stores cross PCIe at the
+// copy engine's rate, measured 54.8 GB/s, so the write and the transfer overlap
+// and the separate device-to-host copy and its host round trip disappear).
 int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,
-                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s, bool ascii_keys) {
+                  uint64_t* out_n, uint64_t* h_offsets, hipStream_t s, bool ascii_keys, uint8_t* hout, uint64_t hout_cap) {
     const uint64_t n = r.n;
     const bool all = only_part == 0xFFFFFFFFu;
     const uint32_t nparts = all ? nreduce : 1;
@@ -910,11 +921,10 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     RCHK(ws->key_a.ensure(n * 8));
     RCHK(ws->key_b.ensure(n * 8));
     RCHK(ws->lineoff.ensure(n * 8 + 8));
-    // Output bytes, bounded up front so nothing waits for the exact total: a wc
-    // line is key + ' ' + <= 20 digits + '\n', a grep line key + ' ' + key + '\n';
-    // key bytes past 16 live in the arena.
-    const uint64_t key_bound = 16 * n + r.arena_n;
-    RCHK(ws->out.ensure(app == 1 ? key_bound + 22 * n + 16 : 2 * key_bound + 2 * n + 16));
+    // Output bytes, bounded up front so nothing waits for the exact total
+    const uint64_t bound = reduce_out_bound(r, app);
+    const bool to_host = hout != nullptr && bound <= hout_cap;
+    if (!to_host) RCHK(ws->out.ensure(bound));
     RCHK(ws->offs.ensure((size_t)(nparts + 1) * 8));
     RCHK(hipMemsetAsync(flags, 0, 32, s));
 
@@ -1062,7 +1072,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     RCHK(rocprim::exclusive_scan(nullptr, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
     RCHK(ws->tmp.ensure(tb));
     RCHK(rocprim::exclusive_scan(ws->tmp.p, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
-    uint8_t* out = ws->out.as<uint8_t>();
+    uint8_t* out = to_host ? hout : ws->out.as<uint8_t>();
     const unsigned wl_grid = (unsigned)std::min<uint64_t>((n + kWlLines - 1) / kWlLines, 8192);
     if (app != 1) write_lines_staged_kernel<2><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
     else write_lines_staged_kernel<1><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);

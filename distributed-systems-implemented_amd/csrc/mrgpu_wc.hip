@@ -102,8 +102,10 @@ __device__ __forceinline__ void dict_set_addrs(uint32_t h, bool mid, uint32_t& a
     const uint32_t off = mid ? (uint32_t)kDictShortSets * 16u : 0u;
     const uint32_t A = h >> 16;           // a << 4 in bits 4..15
     const uint32_t X = (h & ~15u) | 16u;  // x << 4 in bits 4..15 (bit 4 forced: a2 != a1)
-    a1 = (A & m) | off;
-    a2 = ((A ^ X) & m) | off;
+    // (a & b) | c as v_bitop3_b32 (truth table 0xEA): a plain VALU op on gfx950,
+    // where v_and_or_b32 issues at the 4-cycle rate (tools/ubench/valu_probe.hip)
+    a1 = __builtin_amdgcn_bitop3_b32(A, m, off, 0xEA);
+    a2 = __builtin_amdgcn_bitop3_b32(A ^ X, m, off, 0xEA);
 }
 __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, uint32_t& s2) {
     uint32_t a1, a2;

@@ -188,7 +188,10 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        prefix passes only), sort_compact_ties (-1:
  *                                        off), sort_bins (1: sample sort), sort_prefix32
  *                                        (0: the wc key pass over all 60/64 bits instead
- *                                        of the top 32)   reduce sort variants */
+ *                                        of the top 32)   reduce sort variants
+ *   out_direct (-1: off)                 mrg_run_job (wc) writes the output lines straight into
+ *                                        its pinned host buffer (default) instead of a
+ *                                        device buffer + copy */
 int mrg_set_option(mrg_ctx* ctx, const char* name, int64_t value);
 
 uint32_t mrg_ihash(const uint8_t* key, size_t n);

@@ -663,3 +663,23 @@ def test_host_input_streamed_in_pieces(ctx, app):
         ctx.set_option("ingest_piece", 0)
         ctx.set_option("ingest_min", 0)
         ctx.set_option("dict_min_bytes", 0)
+
+
+@pytest.mark.parametrize("direct", [0, -1])
+def test_run_job_output_to_host(ctx, direct):
+    """mrg_run_job's wc output lines written straight into pinned host memory by
+    the formatting kernel (option out_direct, default) or through a device buffer
+    and a copy (-1): the same bytes as the oracle on wc edge cases (long words,
+    an empty output); grep (which always takes the copy) alongside."""
+    ctx.set_option("out_direct", direct)
+    try:
+        edge = cases.edge_cases()
+        for name in ("empty", "big_word", "utf8_mix", "mixed_lengths", "long_shared_prefix"):
+            for f in edge.get(name, []):
+                assert ctx.run_job(MRG_APP_WC, f, nreduce=10) == O.c_partitioned("wc", [f], 10), name
+        for name, (gf, pat) in sorted(cases.grep_edge_cases().items()):
+            for f in gf:
+                want = O.c_partitioned("grep:" + pat.decode("utf-8", "surrogateescape"), [f], 4)
+                assert ctx.run_job(MRG_APP_GREP, f, pattern=pat, nreduce=4) == want, name
+    finally:
+        ctx.set_option("out_direct", 0)
