@@ -283,6 +283,13 @@ struct DmaStream {
 // unused rest of a range is closed with kListHole entries (skipped by
 // wc_long_kernel).
 constexpr uint32_t kLongReserve = 256;
+// the 2048-bucket layout drains its spill stores after each chunk (measured
+// faster for the slot-wise appends: its 4096 streams per workgroup then leave L2
+// less fragmented); whether the staged >64-miss appends do the same
+#ifndef MRG_STAGE2_DRAIN
+#define MRG_STAGE2_DRAIN 1
+#endif
+constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
 __device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint32_t lleft, uint32_t lane) {
     for (uint32_t g = 0; g < lleft; g += kWave)
         if (g + lane < lleft && lbase + g + lane < t.list_cap) t.list[lbase + g + lane] = kListHole;
@@ -688,6 +695,80 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         }
                         continue;  // passes == 1
                     }
+#ifndef MRG_NO_STAGE2
+                    // More than 64 misses (high-cardinality text: most chunks of C5),
+                    // one pass: the short misses staged as 8-byte keys in the chunk's
+                    // slot (up to 128) and the 9-16-byte ones as 16-byte records in the
+                    // list slot (free once the list entries are in registers; up to
+                    // 64), then appended by type: two 8-byte and one 16-byte store
+                    // instruction, every lane a record (the slot-wise appends below
+                    // issue six stores, two thirds of their lanes out of range).
+                    // Three stores after the DMA: the next counted wait, vmcnt(3),
+                    // still leaves only them in flight.
+                    uint32_t n8u[kBatch + 1], n16u[kBatch + 1];
+                    n8u[0] = n16u[0] = 0;
+        #pragma unroll
+                    for (int u = 0; u < kBatch; u++) {
+                        n8u[u + 1] = n8u[u] + (uint32_t)__popcll(mMiss[u] & ~mBig[u]);
+                        n16u[u + 1] = n16u[u] + (uint32_t)__popcll(mMiss[u] & mBig[u]);
+                    }
+                    // (the high-cardinality layout only: in the default kernel the extra
+                    // path's live state pushed the loop's scalars back into VGPR-lane spills)
+                    if (NB == kSpillBucketsHi && passes == 1 && n8u[kBatch] <= 2u * kWave && n16u[kBatch] <= (uint32_t)kWave) {
+                        lds_u64* st8 = (lds_u64*)buf;
+                        lds_uint4* st16 = (lds_uint4*)L.ring[wv][kf];
+        #pragma unroll
+                        for (int u = 0; u < kBatch; u++) {
+                            const uint64_t m8 = mMiss[u] & ~mBig[u], m16 = mMiss[u] & mBig[u];
+                            if (__builtin_amdgcn_inverse_ballot_w64(m8)) st8[n8u[u] + mbcnt64(m8)] = k0[u];
+                            if (__builtin_amdgcn_inverse_ballot_w64(m16))
+                                st16[n16u[u] + mbcnt64(m16)] =
+                                    (u32x4){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32), (uint32_t)k1[u], (uint32_t)(k1[u] >> 32)};
+                        }
+                        const uint32_t n8 = n8u[kBatch], n16 = n16u[kBatch];
+                        uint64_t mOverAll = 0;
+        #pragma unroll
+                        for (int h = 0; h < 3; h++) {  // 8-byte records lane, lane + 64; then 16-byte records
+                            const bool big = h == 2;
+                            const uint32_t i = lane + (h == 1 ? (uint32_t)kWave : 0u);
+                            const bool valid = i < (big ? n16 : n8);
+                            u32x4 r;
+                            if (big) {
+                                r = st16[lane];
+                            } else {
+                                const unsigned long long v = st8[i];
+                                r = (u32x4){(uint32_t)v, (uint32_t)(v >> 32), 0u, 0u};
+                            }
+                            const uint32_t b = spill_bucket<NB>(big ? fold32(r.x, r.y, r.z, r.w) : fold32(r.x, r.y, 0u, 0u));
+                            const uint32_t ci = valid ? b + (big ? (uint32_t)NB : 0u) : 2u * NB + lane;
+                            const uint32_t pos = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            if constexpr ((mode & 32) != 0) {
+                                acc += pos;
+                                continue;
+                            }
+                            const bool fit = pos < (big ? sub : sub8);
+                            if (big)
+                                __builtin_amdgcn_raw_buffer_store_b128(r, rs16, valid && fit ? (__umul24(b, sub) + pos) * 16u : kOutOfRange,
+                                                                       0, 0);
+                            else
+                                __builtin_amdgcn_raw_buffer_store_b64((u32x2){r.x, r.y}, rs8,
+                                                                      valid && fit ? (__umul24(b, sub8) + pos) * 8u : kOutOfRange, 0, 0);
+                            const uint64_t mOver = __ballot(valid) & ~__ballot(fit);
+                            if (mOver) {  // a stream is full: count in the HBM table; the bucket then merges through it
+                                if (__builtin_amdgcn_inverse_ballot_w64(mOver)) {
+                                    const Tables& tc = cold(t);
+                                    short_insert(tc, ((uint64_t)r.y << 32) | r.x, ((uint64_t)r.w << 32) | r.z, 1);
+                                    tc.bflag[b] = 1u;
+                                    ovf++;
+                                }
+                                mOverAll |= mOver;
+                            }
+                        }
+                        if (mOverAll) wait_vmem_all();
+                        if constexpr (NB == kSpillBucketsHi && kStage2Drain) wait_vmem_all();
+                        continue;  // passes == 1
+                    }
+#endif
                     uint32_t pos[kBatch];
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
