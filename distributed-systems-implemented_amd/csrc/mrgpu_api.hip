@@ -221,6 +221,7 @@ struct mrg_ctx {
     DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
     bool seg_sync = true;               // size the miss segments from this split's totals (host read)
     bool out_direct = true;             // mrg_run_job: output lines written straight into pinned host memory
+    uint64_t arena_hint = 0;            // wc: long-key bytes expected in a split (the previous one's + 25 %)
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     DevBuf ghits, glines, gdefer;        // grep: sorted hits, resolved (start, end) lines, deferred hits
     int agg_rounds = 8;                 // bucket aggregation rounds at most (the last sends leftovers to HBM)
@@ -908,14 +909,26 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         launch_wc_long(in, len, t, lt, ~0ull, c->s);
         HCHK(c, hipGetLastError());
         HCHK(c, hipEventRecord(c->ev[2], c->s));
+        // the arena (long keys' bytes) sized from the previous split's long keys
+        // (parts adopt the context's arena, so each split starts with a fresh one)
+        if (c->arena_hint + 16 > c->recarena.cap) {
+            HCHK(c, c->recarena.ensure_cached(c->arena_hint + 16, c->device));
+            t.out = rec_view(c);
+        }
         if (launch_collect(t, c->lo_log2_cur > 0, c->s)) return fail(c, MRG_EDEVICE, "collect failed");
         if ((rc = read_counters(c))) return rc;
         Counters h = *c->h_ctr;
         if (h.status & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", h.status);
-        if ((h.status & kStRecFull) && h.long_bytes + 16 > c->recarena.cap) {  // the arena first (collect_long)
+        if ((h.status & kStRecFull) && h.long_bytes + 16 > c->recarena.cap && h.nrec <= c->rec_cap) {
+            // only the arena was short: grow it and run the collect again (not the map)
             HCHK(c, c->recarena.ensure_cached(h.long_bytes + 16, c->device));
-            if (h.nrec <= c->rec_cap) continue;  // only the arena was short
+            t.out = rec_view(c);
+            launch_collect_undo(t, c->s);
+            if (launch_collect(t, c->lo_log2_cur > 0, c->s)) return fail(c, MRG_EDEVICE, "collect failed");
+            if ((rc = read_counters(c))) return rc;
+            h = *c->h_ctr;
         }
+        c->arena_hint = h.long_bytes + h.long_bytes / 4;
         if (grow_on_overflow(c, h.status & (kStListFull | kStShortFull | kStLongFull | kStRecFull | kStSegFull)))
             continue;
         {

@@ -53,6 +53,20 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// A 64-bit value of lane j (uniform j).  The readlane builtins return int: each
+// half goes through uint32_t, or a low word with bit 31 set sign-extends over the
+// high one.
+__device__ __forceinline__ uint64_t readlane64(uint64_t v, uint32_t j) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, (int)j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), (int)j);
+    return ((uint64_t)hi << 32) | lo;
+}
+__device__ __forceinline__ uint64_t readfirstlane64(uint64_t v) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32));
+    return ((uint64_t)hi << 32) | lo;
+}
+
 __device__ __forceinline__ uint32_t lane_id() { return __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)); }
 
 __device__ __forceinline__ uint32_t mbcnt64(uint64_t m) {

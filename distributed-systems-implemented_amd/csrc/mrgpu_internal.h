@@ -62,6 +62,7 @@ struct Counters {
     unsigned long long round_mask; // bit r: aggregation round r had input
     unsigned long long nlines;     // grep: matching line occurrences resolved (one per line, not per hit)
     unsigned long long ndefer;     // grep: hits whose line bounds lie beyond a lane's scan window
+    unsigned long long nrec_base;  // ctr->nrec before the collect (a collect-only retry restores it)
     unsigned long long pad[1];
 };
 
@@ -219,6 +220,9 @@ struct ReduceWs;
 // list, then (long_table) the LongTable's keys with their arena bytes.
 // Capacity overflows set kStRecFull.  Returns 0 or a hipError_t.
 int launch_collect(const Tables& t, bool long_table, hipStream_t s);
+// Undo a collect whose arena was too small (records and arena bytes from
+// ctr->nrec_base, kStRecFull cleared), so it can run again with a bigger arena.
+void launch_collect_undo(const Tables& t, hipStream_t s);
 void launch_insert_recs(const Recs& src, const Tables& t, hipStream_t s);
 int map_grid_size(int device);
 

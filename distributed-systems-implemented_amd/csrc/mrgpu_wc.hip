@@ -549,8 +549,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                 const uint32_t want = kLongReserve;
                                 unsigned long long b0 = 0;
                                 if (lane == 0) b0 = atomicAdd(&tc.ctr->nlist, (unsigned long long)want);
-                                lbase = __builtin_amdgcn_readfirstlane((uint32_t)b0) |
-                                        ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(b0 >> 32)) << 32);
+                                lbase = readfirstlane64(b0);
                                 lleft = want;
                                 if (lbase + want > tc.list_cap && lane == 0) set_status(tc.ctr, kStListFull);
                                 wait_vmem_all();
