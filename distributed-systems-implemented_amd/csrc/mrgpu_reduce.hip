@@ -133,23 +133,28 @@ __global__ void gather_key_kernel(Recs r, const uint32_t* perm, uint64_t n, int 
 }
 
 // tie[i] = 1 when sorted position i has the same sort key as i - 1 (the single
-// folded / packed key pass: equal keys are equal (partition, prefix)).
+// folded / packed key pass: equal keys are equal (partition, prefix)).  The
+// "any tie" flag (read by grep's all-runs path) takes one atomic per workgroup:
+// a per-wave check and atomic on one address made this 30 us instead of 5 at
+// C2's 1e6 keys.  The u32 variant (ASCII wc keys only) sets no flag.
 __global__ void mark_ties_sorted_kernel(const uint64_t* keys, uint64_t n, uint8_t* tie, unsigned long long* flags) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    int any = 0;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint8_t t = i > 0 && keys[i] == keys[i - 1] ? 1 : 0;  // (coalesced: no record gathers)
         tie[i] = t;
-        if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
+        any |= t;
     }
+    // flags[2] = "some run is tied" (grep's folded single pass reads it): one
+    // atomic per workgroup (block-uniform: every thread reaches the barrier)
+    if (__syncthreads_or(any) && threadIdx.x == 0) atomicOr(&flags[2], 1ull);
 }
 
 // The same on sorted u32 keys (the 32-bit prefix pass).
 __global__ void mark_ties_sorted32_kernel(const uint32_t* keys, uint64_t n, uint8_t* tie, unsigned long long* flags) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint8_t t = i > 0 && keys[i] == keys[i - 1] ? 1 : 0;
-        tie[i] = t;
-        if (__ballot(t) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
+        tie[i] = i > 0 && keys[i] == keys[i - 1] ? 1 : 0;
     }
 }
 
@@ -1048,40 +1053,64 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     if (grep) {  // every tied run (equal first 16, or with !grep_k1 first 8 - pbits / 8, bytes) merge-sorted
         bool any_long = false;
         if ((e = fix_ties(k1_first, true, &any_long, true))) return e;
-    } else {
-        // keys of 9-16 bytes sharing an 8-byte prefix in a long run: sort again with
-        // the k1 pass (cheaper than a comparison sort); any other long run (keys
-        // > 16 bytes; 8-byte keys differing in the folded-away bits): comparison
-        // merge sort of the run members
-        // (a run over 64 needs 65 distinct keys sharing the sort key's prefix:
-        // 9-16-byte keys, or longer ones; <= 8-byte keys differ within 2^fold)
-        bool any_long = false;
-        if ((e = fix_ties(false, false, &any_long))) return e;
-        if (use_bins && keys_sorted && ws->h_pinned[1]) {  // a bin overflowed: the whole pass again with rocPRIM
-            use_bins = false;
-            RCHK(hipMemsetAsync(flags + 1, 0, 8, s));
-            if ((e = sort_all(false))) return e;
-            if ((e = fix_ties(false, false, &any_long))) return e;
-        }
-        if (any_long) {
-            if ((e = sort_all(true))) return e;
-            if ((e = fix_ties(true, true, &any_long))) return e;
-        }
     }
-    uint64_t* ll = ws->key_b.as<uint64_t>();
-    uint64_t* off = ws->lineoff.as<uint64_t>();
-    line_len_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, app, ll);
-    size_t tb = 0;
-    RCHK(rocprim::exclusive_scan(nullptr, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
-    RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::exclusive_scan(ws->tmp.p, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
     uint8_t* out = to_host ? hout : ws->out.as<uint8_t>();
-    const unsigned wl_grid = (unsigned)std::min<uint64_t>((n + kWlLines - 1) / kWlLines, 8192);
-    if (app != 1) write_lines_staged_kernel<2><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
-    else write_lines_staged_kernel<1><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
-    part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, ll, nparts, !all,
-                                                                 ws->offs.as<uint64_t>());
-    RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
+    // line lengths, their scan, the lines, the partition offsets (copied to the host)
+    auto emit_output = [&]() -> int {
+        uint64_t* ll = ws->key_b.as<uint64_t>();
+        uint64_t* off = ws->lineoff.as<uint64_t>();
+        line_len_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, app, ll);
+        size_t tb = 0;
+        RCHK(rocprim::exclusive_scan(nullptr, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+        RCHK(ws->tmp.ensure(tb));
+        RCHK(rocprim::exclusive_scan(ws->tmp.p, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+        const unsigned wl_grid = (unsigned)std::min<uint64_t>((n + kWlLines - 1) / kWlLines, 8192);
+        if (app != 1) write_lines_staged_kernel<2><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
+        else write_lines_staged_kernel<1><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
+        part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, ll, nparts, !all,
+                                                                     ws->offs.as<uint64_t>());
+        RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
+        return 0;
+    };
+    if (!grep) {
+        // Speculative: the single key pass's tied runs are fixed and the output is
+        // written without a host check in between; the fix-up's flags come back
+        // with the partition offsets (one host round trip for the whole reduce).
+        // Only if a run was long (or a bin overflowed) is the output redone.
+        // (lng is not cleared here: it is read only by the long-run path below,
+        // which clears and recomputes it.)
+        uint8_t* tie = ws->key_a.as<uint8_t>();
+        if (keys32) mark_ties_sorted32_kernel<<<grid_for(n), 256, 0, s>>>(ws->key_b.as<uint32_t>(), n, tie, flags);
+        else if (keys_sorted) mark_ties_sorted_kernel<<<grid_for(n), 256, 0, s>>>(ws->key_b.as<uint64_t>(), n, tie, flags);
+        else mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, false, fold);
+        fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, kMaxRun, flags, tie + n);
+        if ((e = emit_output())) return e;
+        RCHK(hipMemcpyAsync(ws->h_pinned + 1, flags + 1, 24, hipMemcpyDeviceToHost, s));  // flags 1-3
+        RCHK(hipStreamSynchronize(s));
+        const bool bins_over = use_bins && keys_sorted && ws->h_pinned[1];
+        bool any_long = ws->h_pinned[3] != 0;
+        if (bins_over || any_long) {
+            // keys of 9-16 bytes sharing an 8-byte prefix in a long run: sort again with
+            // the k1 pass (cheaper than a comparison sort); any other long run (keys
+            // > 16 bytes; 8-byte keys differing in the folded-away bits): comparison
+            // merge sort of the run members
+            // (a run over 64 needs 65 distinct keys sharing the sort key's prefix:
+            // 9-16-byte keys, or longer ones; <= 8-byte keys differ within 2^fold)
+            if (bins_over) {  // a bin overflowed: the whole pass again with rocPRIM
+                use_bins = false;
+                RCHK(hipMemsetAsync(flags + 1, 0, 8, s));
+                if ((e = sort_all(false))) return e;
+                if ((e = fix_ties(false, false, &any_long))) return e;
+            }
+            if (any_long) {
+                if ((e = sort_all(true))) return e;
+                if ((e = fix_ties(true, true, &any_long))) return e;
+            }
+            if ((e = emit_output())) return e;
+        }
+    } else if ((e = emit_output())) {
+        return e;
+    }
     RCHK(hipStreamSynchronize(s));
     *d_out = out;
     *out_n = h_offsets[nparts];
