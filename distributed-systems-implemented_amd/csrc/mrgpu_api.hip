@@ -1199,6 +1199,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set_compact_ties(c->rws, v >= 0);
     } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default) or via a copy (-1)
         c->out_direct = v >= 0;
+    } else if (!strcmp(name, "own_sort")) {  // reduce radix passes: hand-written LSD sort (1, default) or rocPRIM (0)
+        reduce_ws_set_own_sort(c->rws, v != 0);
     } else if (!strcmp(name, "sort_prefix32")) {  // wc reduce: single pass on the top 32 key bits (1, default) or all (0)
         reduce_ws_set_prefix32(c->rws, v != 0);
     } else if (!strcmp(name, "sort_bins")) {  // wc reduce: hand-written sample sort (1) or rocPRIM (0, -1: default)
@@ -1260,6 +1262,14 @@ int mrg_memcpy_h2d(mrg_ctx* c, void* dst, const void* src, size_t n) {
     HCHK(c, hipMemcpy(dst, src, n, hipMemcpyHostToDevice));
     return MRG_OK;
 }
+int mrg_sort_pairs(mrg_ctx* c, void* keys, void* vals, size_t n, int key_bytes, unsigned bits) {
+    if (!c || (n && !keys)) return MRG_EINVAL;
+    const int e = sort_in_place(c->rws, key_bytes, keys, (uint32_t*)vals, n, bits, c->s);
+    if (e == (int)hipErrorInvalidValue) return fail(c, MRG_EINVAL, "mrg_sort_pairs: key_bytes 4 or 8; 4-byte keys need values");
+    if (e) return fail(c, MRG_EDEVICE, "mrg_sort_pairs: %s", hipGetErrorString((hipError_t)e));
+    return MRG_OK;
+}
+
 int mrg_memcpy_d2h(mrg_ctx* c, void* dst, const void* src, size_t n) {
     int rc;
     if ((rc = bind(c))) return rc;

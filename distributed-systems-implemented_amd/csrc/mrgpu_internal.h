@@ -226,6 +226,18 @@ void launch_collect_undo(const Tables& t, hipStream_t s);
 void launch_insert_recs(const Recs& src, const Tables& t, hipStream_t s);
 int map_grid_size(int device);
 
+// ---- stable LSD radix sort (mrgpu_sort.hip) ----
+struct RadixWs;
+RadixWs* radix_ws_new();
+void radix_ws_free(RadixWs*);
+// Stable sort by the low `bits` key bits (8-bit digits, one launch per pass);
+// k_in / v_in are not modified.  Returns 0 or a hipError_t.
+int radix_sort_pairs_u32(RadixWs*, const uint32_t* k_in, uint32_t* k_out, const uint32_t* v_in, uint32_t* v_out,
+                         uint64_t n, unsigned bits, hipStream_t s);
+int radix_sort_pairs_u64(RadixWs*, const uint64_t* k_in, uint64_t* k_out, const uint32_t* v_in, uint32_t* v_out,
+                         uint64_t n, unsigned bits, hipStream_t s);
+int radix_sort_keys_u64(RadixWs*, const uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s);
+
 // ---- reduce (mrgpu_reduce.hip) ----
 struct ReduceWs;  // opaque workspace
 ReduceWs* reduce_ws_new();
@@ -240,6 +252,8 @@ void reduce_ws_set_compact_ties(ReduceWs*, bool on);
 void reduce_ws_set_bin_sort(ReduceWs*, bool on);
 // The wc single-key pass on the key's top 32 bits (default) or the whole 60/64-bit key.
 void reduce_ws_set_prefix32(ReduceWs*, bool on);
+// Radix passes by the hand-written sort (default) or rocPRIM onesweep.
+void reduce_ws_set_own_sort(ReduceWs*, bool on);
 // Sort recs (optionally only partition `only_part`), format "key value\n" lines.
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
 // ascii_keys: every key byte is < 0x80 (the sort key then packs 7 bits per byte).
@@ -254,6 +268,9 @@ int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64
                       uint32_t** d_count, hipStream_t s);
 // Radix sort of u64 keys (the low `bits` bits); result in k_out.
 int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s);
+// In-place stable sort of device keys (key_bytes 4 or 8, low `bits` bits) with
+// optional u32 values (nullptr: 8-byte keys only); waits for the stream.
+int sort_in_place(ReduceWs* ws, int key_bytes, void* keys, uint32_t* vals, uint64_t n, unsigned bits, hipStream_t s);
 // Stable radix sort of (u32 key, u32 value) pairs; result in k_out / v_out.
 int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, uint64_t n,
                    unsigned bits, hipStream_t s);

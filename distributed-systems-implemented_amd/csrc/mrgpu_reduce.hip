@@ -61,6 +61,10 @@ struct ReduceWs {
     // key bits): four 8-bit onesweep passes over u32 keys instead of six 10-bit
     // passes over u64 ones); keys tied on them are ordered by fix_ties
     bool prefix32 = true;
+    // radix passes by the hand-written LSD sort (mrgpu_sort.hip: one launch per
+    // pass, no memsets) instead of rocPRIM onesweep
+    bool own_sort = true;
+    RadixWs* rx = nullptr;
 };
 
 void reduce_ws_set(ReduceWs* w, int digit_bits, int fold_part, int grep_k1) {
@@ -74,9 +78,11 @@ void reduce_ws_set_compact_ties(ReduceWs* w, bool on) { w->compact_ties = on;
 
 void reduce_ws_set_bin_sort(ReduceWs* w, bool on) { w->bin_sort = on; }
 void reduce_ws_set_prefix32(ReduceWs* w, bool on) { w->prefix32 = on; }
+void reduce_ws_set_own_sort(ReduceWs* w, bool on) { w->own_sort = on; }
 
 ReduceWs* reduce_ws_new() {
     ReduceWs* w = new ReduceWs();
+    w->rx = radix_ws_new();
     if (hipHostMalloc((void**)&w->h_pinned, 4096 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) w->h_pinned = nullptr;
     return w;
 }
@@ -86,6 +92,7 @@ void reduce_ws_free(ReduceWs* w) {
     DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek, &w->bins};
     for (DBuf* b : bs) b->release();
     if (w->h_pinned) hipHostFree(w->h_pinned);
+    radix_ws_free(w->rx);
     delete w;
 }
 
@@ -778,6 +785,10 @@ using OnesweepCfg10 = rocprim::radix_sort_config<
 template <class K>
 static int sort_pass(ReduceWs* ws, K* keys_in, K* keys_out, uint32_t* v_in, uint32_t* v_out, uint64_t n, unsigned bits,
                      hipStream_t s) {
+    if (ws->own_sort) {
+        if constexpr (sizeof(K) == 8) return radix_sort_pairs_u64(ws->rx, keys_in, keys_out, v_in, v_out, n, bits, s);
+        else return radix_sort_pairs_u32(ws->rx, keys_in, keys_out, v_in, v_out, n, bits, s);
+    }
     size_t tb = 0;
     if (sizeof(K) == 8 && ws->digit_bits == 10 && bits > 32) {
         RCHK(rocprim::radix_sort_pairs<OnesweepCfg10>(nullptr, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
@@ -814,6 +825,7 @@ int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64
 }
 
 int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s) {
+    if (ws->own_sort) return radix_sort_keys_u64(ws->rx, k_in, k_out, n, bits, s);
     size_t tb = 0;
     if (ws->digit_bits != 8 && bits > 32) {  // (grep hit positions: 4 passes of 10 bits for a 34-bit split)
         RCHK(rocprim::radix_sort_keys<OnesweepCfg10>(nullptr, tb, k_in, k_out, (size_t)n, 0u, bits, s));
@@ -825,6 +837,30 @@ int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, uns
     RCHK(ws->tmp.ensure(tb));
     RCHK(rocprim::radix_sort_keys<OnesweepCfg>(ws->tmp.p, tb, k_in, k_out, (size_t)n, 0u, bits, s));
     return 0;
+}
+
+// In-place sort of device keys (4 or 8 bytes) with optional u32 values
+// (mrg_sort_pairs, a test hook): through the same dispatch as the reduce.
+int sort_in_place(ReduceWs* ws, int key_bytes, void* keys, uint32_t* vals, uint64_t n, unsigned bits, hipStream_t s) {
+    if (n == 0) return 0;
+    if ((key_bytes != 4 && key_bytes != 8) || (!vals && key_bytes != 8)) return (int)hipErrorInvalidValue;
+    void* ko = nullptr;
+    uint32_t* vo = nullptr;
+    RCHK(hipMalloc(&ko, n * key_bytes));
+    if (vals && hipMalloc((void**)&vo, n * 4) != hipSuccess) {
+        (void)hipFree(ko);
+        return (int)hipErrorOutOfMemory;
+    }
+    int e;
+    if (key_bytes == 4) e = sort_pass<uint32_t>(ws, (uint32_t*)keys, (uint32_t*)ko, vals, vo, n, bits, s);
+    else if (vals) e = sort_pass<uint64_t>(ws, (uint64_t*)keys, (uint64_t*)ko, vals, vo, n, bits, s);
+    else e = sort_u64_keys(ws, (uint64_t*)keys, (uint64_t*)ko, n, bits, s);
+    if (!e) e = (int)hipMemcpyAsync(keys, ko, n * key_bytes, hipMemcpyDeviceToDevice, s);
+    if (!e && vals) e = (int)hipMemcpyAsync(vals, vo, n * 4, hipMemcpyDeviceToDevice, s);
+    if (!e) e = (int)hipStreamSynchronize(s);
+    (void)hipFree(ko);
+    if (vo) (void)hipFree(vo);
+    return e;
 }
 
 int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in, uint32_t* v_out, uint64_t n,

@@ -40,7 +40,7 @@ EXPORTED = [
     "mrg_parts_export_json", "mrg_parts_import_json", "mrg_parts_free", "mrg_reduce",
     "mrg_reduce_all", "mrg_run_job", "mrg_comm_unique_id", "mrg_comm_init", "mrg_exchange",
     "mrg_exchange_group",
-    "mrg_device_alloc", "mrg_device_free", "mrg_memcpy_h2d", "mrg_memcpy_d2h", "mrg_sync",
+    "mrg_device_alloc", "mrg_device_free", "mrg_memcpy_h2d", "mrg_memcpy_d2h", "mrg_sort_pairs", "mrg_sync",
     "mrg_get_stats", "mrg_set_option", "mrg_ihash", "mrg_free",
 ]
 
@@ -121,6 +121,7 @@ def load_library(path: str | None = None):
     L.mrg_device_free.argtypes = [vp, vp]
     L.mrg_memcpy_h2d.argtypes = [vp, vp, vp, c_size_t]
     L.mrg_memcpy_d2h.argtypes = [vp, vp, vp, c_size_t]
+    L.mrg_sort_pairs.argtypes = [vp, vp, vp, c_size_t, c_int, ctypes.c_uint]
     L.mrg_sync.argtypes = [vp]
     L.mrg_get_stats.argtypes = [vp, POINTER(Stats)]
     L.mrg_set_option.argtypes = [vp, c_char_p, c_int64]
@@ -354,3 +355,30 @@ class Context:
 
     def sync(self):
         self._check(self.L.mrg_sync(self.h), "mrg_sync")
+
+    def sort_pairs(self, keys, vals=None, bits: int = 0):
+        """Test hook (mrg_sort_pairs): the reduce's stable radix sort of numpy
+        keys (uint32 / uint64) carrying uint32 vals (or None: uint64 keys only),
+        by their low `bits` bits; returns the sorted (keys, vals) as numpy arrays."""
+        import numpy as np
+        keys = np.ascontiguousarray(keys)
+        kb = keys.dtype.itemsize
+        n = keys.size
+        dk = self.device_alloc(max(n * kb, 16))
+        dv = self.device_alloc(max(n * 4, 16)) if vals is not None else None
+        try:
+            if n:
+                self.h2d(dk, keys.tobytes())
+                if vals is not None:
+                    self.h2d(dv, np.ascontiguousarray(vals, dtype=np.uint32).tobytes())
+            self._check(self.L.mrg_sort_pairs(self.h, c_void_p(dk), c_void_p(dv) if dv else None, n, kb, bits),
+                        "mrg_sort_pairs")
+            ko = np.frombuffer(self.d2h(dk, n * kb), dtype=keys.dtype) if n else keys[:0].copy()
+            vo = None
+            if vals is not None:
+                vo = np.frombuffer(self.d2h(dv, n * 4), dtype=np.uint32) if n else np.zeros(0, np.uint32)
+            return ko, vo
+        finally:
+            self.device_free(dk)
+            if dv:
+                self.device_free(dv)

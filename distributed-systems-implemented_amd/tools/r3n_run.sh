@@ -1,0 +1,8 @@
+set -e
+out=gpurun_out/r3n
+mkdir -p $out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread -k "radix_sort_hook or sort_variants" > $out/sort_tests.log 2>&1
+tail -1 $out/sort_tests.log
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/gpu_tests.log 2>&1
+tail -1 $out/gpu_tests.log
+bash distributed-systems-implemented_amd/tools/ab_opts.sh r3n/ab "c2 c3 c5" "--opt own_sort=1" "--opt own_sort=0"

@@ -160,6 +160,11 @@ int mrg_device_alloc(mrg_ctx* ctx, size_t n, void** dptr);
 int mrg_device_free(mrg_ctx* ctx, void* dptr);
 int mrg_memcpy_h2d(mrg_ctx* ctx, void* dst, const void* src, size_t n);
 int mrg_memcpy_d2h(mrg_ctx* ctx, void* dst, const void* src, size_t n);
+/* Test hook for the reduce's radix sort (no reference counterpart): stable
+ * in-place sort of n device keys (key_bytes 4 or 8, by their low `bits` bits;
+ * 0 = all) carrying u32 device values (NULL: 8-byte keys only), through the
+ * same dispatch as the reduce (option own_sort).  Waits for completion. */
+int mrg_sort_pairs(mrg_ctx* ctx, void* keys, void* vals, size_t n, int key_bytes, unsigned bits);
 int mrg_sync(mrg_ctx* ctx);
 int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
 
@@ -188,7 +193,9 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        prefix passes only), sort_compact_ties (-1:
  *                                        off), sort_bins (1: sample sort), sort_prefix32
  *                                        (0: the wc key pass over all 60/64 bits instead
- *                                        of the top 32)   reduce sort variants
+ *                                        of the top 32), own_sort (0: rocPRIM onesweep
+ *                                        radix passes instead of the hand-written LSD
+ *                                        sort)   reduce sort variants
  *   out_direct (-1: off)                 mrg_run_job (wc) writes the output lines straight into
  *                                        its pinned host buffer (default) instead of a
  *                                        device buffer + copy */

@@ -195,10 +195,12 @@ def test_wc_high_cardinality_buckets(ctx, rounds):
         ctx.set_option("spill_hi_keys", 0)
 
 
-@pytest.mark.parametrize("digit_bits,fold,grep_k1,compact",
-                         [(8, 0, 0, 0), (8, -1, 0, -1), (10, 0, 0, 0), (10, -1, -1, -1), (8, 0, -1, 0)])
-def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact):
-    """The reduce's sort variants give the same bytes: 8- or 10-bit radix digits,
+@pytest.mark.parametrize("digit_bits,fold,grep_k1,compact,own",
+                         [(8, 0, 0, 0, 1), (8, -1, 0, -1, 1), (10, 0, 0, 0, 0), (10, -1, -1, -1, 0), (8, 0, -1, 0, 1),
+                          (10, -1, 0, 0, 1)])
+def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact, own):
+    """The reduce's sort variants give the same bytes: the hand-written radix
+    passes (default) or rocPRIM onesweep (own_sort=0) with 8- or 10-bit digits,
     the partition folded into the first key pass (default) or sorted on its own,
     grep lines radix-sorted on 16 key bytes (default) or 8 (more tied runs), tied
     runs merge-sorted on compact key copies (default) or on the records.
@@ -212,6 +214,7 @@ def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact):
     ctx.set_option("sort_fold_part", fold)
     ctx.set_option("grep_sort_k1", grep_k1)
     ctx.set_option("sort_compact_ties", compact)
+    ctx.set_option("own_sort", own)
     try:
         check(ctx, "wc", files, nreduces=(1, 10, 64))
         check(ctx, "wc", [words, words[::-1]], nreduces=(1, 10, 300))  # ASCII only: the packed sort key
@@ -221,6 +224,47 @@ def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact):
         ctx.set_option("sort_fold_part", 0)
         ctx.set_option("grep_sort_k1", 0)
         ctx.set_option("sort_compact_ties", 0)
+        ctx.set_option("own_sort", 1)
+
+
+@pytest.mark.parametrize("own", [1, 0])
+@pytest.mark.parametrize("kind,bits", [("u32", 32), ("u32", 4), ("u32", 20), ("u64", 64), ("u64", 60), ("u64", 12),
+                                       ("u64keys", 34), ("u64keys", 64)])
+def test_radix_sort_hook(ctx, own, kind, bits):
+    """The reduce's radix sort (mrg_sort_pairs) against numpy's stable argsort:
+    sizes around the 4096-key tile (0, 1, 4095, 4096, 4097), 1e5 keys, and 3e6
+    (733 tiles: more than can be resident at once, so the look-back waits on
+    tiles started later); uniform keys, keys from 5 values (ties: stability),
+    all keys equal, high bits set past `bits` (ignored by the sort)."""
+    rng = np.random.default_rng(bits * 7 + own)
+    dt = np.uint32 if kind == "u32" else np.uint64
+    width = 32 if kind == "u32" else 64
+    mask = (1 << bits) - 1 if bits < width else (1 << width) - 1
+    ctx.set_option("own_sort", own)
+    try:
+        for n in (0, 1, 4095, 4096, 4097, 100_000, 3_000_000):
+            for dist in ("uniform", "few", "equal"):
+                if n >= 3_000_000 and dist != "uniform":
+                    continue
+                if dist == "uniform":
+                    keys = rng.integers(0, 1 << width, size=n, dtype=np.uint64 if width == 64 else np.int64).astype(dt)
+                elif dist == "few":
+                    keys = rng.choice(np.array([0, 3, mask, mask >> 1, 1 << (bits - 1)], dtype=np.uint64),
+                                      size=n).astype(dt)
+                else:
+                    keys = np.full(n, mask & 0x5A5A5A5A5A5A5A5A, dtype=dt)
+                masked = keys & dt(mask)
+                order = np.argsort(masked, kind="stable")
+                if kind == "u64keys":
+                    ko, _ = ctx.sort_pairs(keys, None, bits)
+                    assert np.array_equal(ko, keys[order]), (n, dist)
+                else:
+                    vals = np.arange(n, dtype=np.uint32)
+                    ko, vo = ctx.sort_pairs(keys, vals, bits)
+                    assert np.array_equal(vo, order.astype(np.uint32)), (n, dist)
+                    assert np.array_equal(ko, keys[order]), (n, dist)
+    finally:
+        ctx.set_option("own_sort", 1)
 
 
 @pytest.mark.parametrize("bins,prefix32", [(1, 1), (0, 1), (0, 0)])
