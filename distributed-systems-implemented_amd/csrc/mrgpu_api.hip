@@ -1199,6 +1199,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set_compact_ties(c->rws, v >= 0);
     } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default) or via a copy (-1)
         c->out_direct = v >= 0;
+    } else if (!strcmp(name, "tie_rank")) {  // grep reduce: tied runs ranked per run (1, default) or merge-sorted (0)
+        reduce_ws_set_tie_rank(c->rws, v != 0);
     } else if (!strcmp(name, "own_sort")) {  // reduce radix passes: hand-written LSD sort (1, default) or rocPRIM (0)
         reduce_ws_set_own_sort(c->rws, v != 0);
     } else if (!strcmp(name, "sort_prefix32")) {  // wc reduce: single pass on the top 32 key bits (1, default) or all (0)

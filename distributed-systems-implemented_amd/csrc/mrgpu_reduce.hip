@@ -11,6 +11,8 @@
 // key, so that order is exact whenever prefixes differ.  Runs of equal
 // prefixes (keys > 16 bytes, or grep lines containing NUL bytes) are then
 // ordered by a full bytewise comparison inside each run.
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_merge_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
@@ -47,7 +49,7 @@ struct DBuf {
 };
 
 struct ReduceWs {
-    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext, tiek, bins;
+    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext, tiek, bins, runs;
     uint64_t* h_pinned = nullptr;  // small pinned staging
     int digit_bits = 0;            // radix digit of the 64-bit key passes: 8, 10, 0 = by app (grep 10, wc 8)
     bool fold_part = true;         // wc: partition folded into the top bits of the k0 sort key
@@ -64,6 +66,9 @@ struct ReduceWs {
     // radix passes by the hand-written LSD sort (mrgpu_sort.hip: one launch per
     // pass, no memsets) instead of rocPRIM onesweep
     bool own_sort = true;
+    // grep (16-byte passes): tied runs ordered by rank per run (waves / workgroups)
+    // instead of one merge sort of every tied key
+    bool tie_rank = true;
     RadixWs* rx = nullptr;
 };
 
@@ -79,6 +84,7 @@ void reduce_ws_set_compact_ties(ReduceWs* w, bool on) { w->compact_ties = on;
 void reduce_ws_set_bin_sort(ReduceWs* w, bool on) { w->bin_sort = on; }
 void reduce_ws_set_prefix32(ReduceWs* w, bool on) { w->prefix32 = on; }
 void reduce_ws_set_own_sort(ReduceWs* w, bool on) { w->own_sort = on; }
+void reduce_ws_set_tie_rank(ReduceWs* w, bool on) { w->tie_rank = on; }
 
 ReduceWs* reduce_ws_new() {
     ReduceWs* w = new ReduceWs();
@@ -89,7 +95,7 @@ ReduceWs* reduce_ws_new() {
 
 void reduce_ws_free(ReduceWs* w) {
     if (!w) return;
-    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek, &w->bins};
+    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek, &w->bins, &w->runs};
     for (DBuf* b : bs) b->release();
     if (w->h_pinned) hipHostFree(w->h_pinned);
     radix_ws_free(w->rx);
@@ -917,6 +923,206 @@ static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
     return 0;
 }
 
+// ---- grep's tied runs (keys equal in (partition, first 16 bytes)) ----------
+// After the 16-byte radix sort, C3 has ~90 K tied keys in ~13 K runs: 12 K runs
+// of 2-8 keys, ~1.2 K of 9-64, ~120 of 65-1422 (10 GB, R = 10).  Each run is
+// ordered on its own, by rank: a key's position in its run = how many run
+// members compare less (keys are distinct, so ranks are a permutation):
+//  - runs of <= 64 keys: one wave per run, a key per lane, the other members'
+//    words broadcast by readlane (no LDS, no barriers);
+//  - runs of 65-2048 keys: one 1024-thread workgroup per run, a bitonic sort of
+//    member indices over the members' words staged in LDS;
+//  - longer runs: marked in `lng` for the merge sort (sort_long_runs).
+// Compared: key bytes 16-63 (the ext words), then bytes 64+ from the arena when
+// both keys are longer, then the length — the order rec_cmp_ext gives.
+constexpr uint32_t kSmallRun = 64, kMidRun = 2048;
+
+__device__ __forceinline__ int tied_cmp(const Recs& r, const uint64_t* ea, uint32_t la, uint32_t ra, const uint64_t* eb,
+                                        uint32_t lb, uint32_t rb) {
+#pragma unroll
+    for (int w = 0; w < kExtWords; w++)
+        if (ea[w] != eb[w]) return ea[w] < eb[w] ? -1 : 1;
+    constexpr uint32_t kCovered = 16 + 8 * kExtWords;
+    if (la > kCovered && lb > kCovered) {
+        const uint8_t* pa = r.arena + r.koff[ra];
+        const uint8_t* pb = r.arena + r.koff[rb];
+        const uint32_t mx = la > lb ? la : lb;
+        for (uint32_t pos = kCovered; pos < mx; pos += 8) {
+            const uint64_t wa = key_word_be(pa, pos, la), wb = key_word_be(pb, pos, lb);
+            if (wa != wb) return wa < wb ? -1 : 1;
+        }
+    }
+    return (la > lb) - (la < lb);
+}
+
+struct IsBoundary {  // sorted position i starts a new (partition, prefix) group
+    const uint8_t* tie;
+    __host__ __device__ bool operator()(const uint32_t& i) const { return tie[i] == 0; }
+};
+
+// One wave per 64 consecutive group boundaries (bpos: sorted positions that
+// start a (partition, prefix) group; cnt[0]'s low half = how many): the wave
+// ranks each run of 2-64 keys among them in turn — a key per lane, the other
+// members' words broadcast by readlane — and lists runs of 65-kMidRun keys in
+// `mid` (cnt[2]); longer runs are marked in lng and flag flags[3].
+__global__ void __launch_bounds__(256) rank_small_runs_kernel(Recs r, const uint64_t* ext, uint32_t* perm,
+                                                              const uint32_t* bpos, uint64_t n, uint2* mid,
+                                                              unsigned long long* cnt, uint8_t* lng,
+                                                              unsigned long long* flags) {
+    const uint64_t nb = *(const uint32_t*)cnt;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t c = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; c * 64 < nb; c += nwaves) {
+        const uint64_t j = c * 64 + lane;
+        uint32_t bs = 0, bk = 0;
+        if (j < nb) {
+            bs = bpos[j];
+            bk = (uint32_t)((j + 1 < nb ? (uint64_t)bpos[j + 1] : n) - bs);
+        }
+        if (bk > kSmallRun && bk <= kMidRun) mid[atomicAdd(cnt + 2, 1ull)] = make_uint2(bs, bk);
+        if (bk > kMidRun) {
+            for (uint32_t a = 0; a < bk; a++) lng[bs + a] = 1;
+            atomicOr(&flags[3], 1ull);
+        }
+        uint64_t todo = __ballot(bk >= 2 && bk <= kSmallRun);
+        while (todo) {
+            const uint32_t q = (uint32_t)__builtin_ctzll(todo);
+            todo &= todo - 1;
+            const uint32_t s = (uint32_t)__builtin_amdgcn_readlane((int)bs, (int)q);
+            const uint32_t k = (uint32_t)__builtin_amdgcn_readlane((int)bk, (int)q);
+            const bool have = lane < k;
+            const uint32_t rec = have ? perm[s + lane] : 0u;
+            uint64_t e[kExtWords];
+#pragma unroll
+            for (int w = 0; w < kExtWords; w++) e[w] = have ? ext[(uint64_t)kExtWords * rec + w] : 0ull;
+            const uint32_t len = have ? r.len[rec] : 0u;
+            uint32_t rank = 0;
+            for (uint32_t m = 0; m < k; m++) {
+                uint64_t em[kExtWords];
+#pragma unroll
+                for (int w = 0; w < kExtWords; w++) em[w] = readlane64(e[w], m);
+                const uint32_t lm = (uint32_t)__builtin_amdgcn_readlane((int)len, (int)m);
+                const uint32_t rm = (uint32_t)__builtin_amdgcn_readlane((int)rec, (int)m);
+                // (not against itself: equal words would walk the arena tail)
+                if (have && m != lane && tied_cmp(r, em, lm, rm, e, len, rec) < 0) rank++;
+            }
+            if (have) perm[s + rank] = rec;
+        }
+    }
+}
+
+// A run of 65-kMidRun keys per workgroup: a bitonic sort of (first ext word,
+// member) items in LDS; items with equal first words compare all words.
+struct MidItem {
+    uint64_t w;
+    uint32_t m, pad;
+};
+struct MidRunLds {
+    MidItem it[kMidRun];
+    uint64_t e[kMidRun][kExtWords];
+    uint32_t len[kMidRun];
+    uint32_t rec[kMidRun];
+};
+
+__global__ void __launch_bounds__(1024) rank_mid_runs_kernel(Recs r, const uint64_t* ext, uint32_t* perm,
+                                                             const uint2* mid, const unsigned long long* cnt) {
+    __shared__ MidRunLds L;
+    const uint64_t nruns = cnt[2];
+    const uint32_t tid = threadIdx.x;
+    for (uint64_t run = blockIdx.x; run < nruns; run += gridDim.x) {
+        const uint2 sk = mid[run];
+        const uint32_t s = sk.x, k = sk.y;
+        uint32_t P = 1;
+        while (P < k) P <<= 1;
+        for (uint32_t m = tid; m < P; m += 1024) {
+            MidItem x;
+            x.m = m;  // m >= k: padding, above every member
+            x.pad = 0;
+            x.w = ~0ull;
+            if (m < k) {
+                const uint32_t rec = perm[s + m];
+                L.rec[m] = rec;
+                L.len[m] = r.len[rec];
+#pragma unroll
+                for (int w = 0; w < kExtWords; w++) L.e[m][w] = ext[(uint64_t)kExtWords * rec + w];
+                x.w = L.e[m][0];
+            }
+            L.it[m] = x;
+        }
+        __syncthreads();
+        for (uint32_t size = 2; size <= P; size <<= 1) {
+            for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+                for (uint32_t t = tid; t < (P >> 1); t += 1024) {
+                    const uint32_t i = 2 * t - (t & (stride - 1));
+                    const uint32_t j = i + stride;
+                    const MidItem A = L.it[i], B = L.it[j];
+                    bool gt;  // item A > item B
+                    if (A.w != B.w) {
+                        gt = A.w > B.w;
+                    } else if (A.m >= k || B.m >= k) {
+                        gt = A.m >= k && (B.m < k || A.m > B.m);
+                    } else {
+                        uint64_t ea[kExtWords], eb[kExtWords];
+#pragma unroll
+                        for (int w = 0; w < kExtWords; w++) {
+                            ea[w] = L.e[A.m][w];
+                            eb[w] = L.e[B.m][w];
+                        }
+                        gt = tied_cmp(r, ea, L.len[A.m], L.rec[A.m], eb, L.len[B.m], L.rec[B.m]) > 0;
+                    }
+                    if (gt == ((i & size) == 0)) {
+                        L.it[i] = B;
+                        L.it[j] = A;
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        for (uint32_t m = tid; m < k; m += 1024) perm[s + m] = L.rec[L.it[m].m];
+        __syncthreads();  // LDS reused by the next run
+    }
+}
+
+// Orders grep's tied runs after the 16-byte sort (perm = its result, tie = the
+// tie marks).  Runs over kMidRun keys are marked in lng and flags[3] is set: the
+// caller reads the flag and merge-sorts them (sort_long_runs).
+static int rank_tied_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t n, const uint8_t* tie, uint8_t* lng,
+                          const uint64_t* ext, unsigned long long* flags, hipStream_t s) {
+    RCHK(ws->runs.ensure(64 + (n / kSmallRun + 2) * 8));
+    unsigned long long* cnt = ws->runs.as<unsigned long long>();
+    uint2* mid = (uint2*)(cnt + 8);
+    uint32_t* d_nb = (uint32_t*)cnt;  // cnt[0]'s low half
+    uint32_t* bpos = ws->key_b.as<uint32_t>();
+    RCHK(hipMemsetAsync(cnt, 0, 64, s));
+    rocprim::counting_iterator<uint32_t> first(0);
+    size_t tb = 0;
+    RCHK(rocprim::select(nullptr, tb, first, bpos, d_nb, (size_t)n, IsBoundary{tie}, s));
+    RCHK(ws->tmp.ensure(tb));
+    RCHK(rocprim::select(ws->tmp.p, tb, first, bpos, d_nb, (size_t)n, IsBoundary{tie}, s));
+    static const bool dbg = getenv("MRG_DEBUG_TIES") != nullptr;
+    hipEvent_t ev[3];
+    if (dbg) {
+        for (auto& e : ev) (void)hipEventCreate(&e);
+        (void)hipEventRecord(ev[0], s);
+    }
+    const unsigned g = (unsigned)std::min<uint64_t>((n / 64 + 4) / 4 + 1, 2048);  // 4 waves per block
+    rank_small_runs_kernel<<<g, 256, 0, s>>>(r, ext, perm, bpos, n, mid, cnt, lng, flags);
+    if (dbg) (void)hipEventRecord(ev[1], s);
+    rank_mid_runs_kernel<<<256, 1024, 0, s>>>(r, ext, perm, mid, cnt);
+    if (dbg) {
+        (void)hipEventRecord(ev[2], s);
+        (void)hipEventSynchronize(ev[2]);
+        unsigned long long h[3];
+        (void)hipMemcpy(h, cnt, 24, hipMemcpyDeviceToHost);
+        float t[2];
+        for (int i = 0; i < 2; i++) (void)hipEventElapsedTime(&t[i], ev[i], ev[i + 1]);
+        fprintf(stderr, "[ties] n %llu bounds %llu mid %llu: small %.1f us mid %.1f us\n", (unsigned long long)n,
+                h[0] & 0xFFFFFFFFull, h[2], 1e3 * t[0], 1e3 * t[1]);
+        for (auto& e : ev) (void)hipEventDestroy(e);
+    }
+    return 0;
+}
+
 int select_recs(ReduceWs* ws, const Recs& src, uint32_t mod, uint32_t want, Recs* dst, hipStream_t s) {
     // dst arrays must be preallocated by the caller with src.n capacity; arena shared with src.
     unsigned long long* cnt = nullptr;
@@ -1086,7 +1292,17 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     };
     int e;
     if ((e = sort_all(k1_first))) return e;
-    if (grep) {  // every tied run (equal first 16, or with !grep_k1 first 8 - pbits / 8, bytes) merge-sorted
+    // grep after the 16-byte passes: tied runs ranked per run, speculatively (the
+    // output is written, then the long-run flag read: only runs over kMidRun keys
+    // redo the output after a merge sort)
+    const bool rank_ties = grep && k1_first && ws->tie_rank;
+    if (rank_ties) {
+        uint8_t* tie = ws->key_a.as<uint8_t>();
+        RCHK(hipMemsetAsync(tie + n, 0, n, s));
+        RCHK(hipMemsetAsync(flags + 2, 0, 16, s));
+        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, true, 0u);
+        if ((e = rank_tied_runs(ws, r, pa, n, tie, tie + n, ext, flags, s))) return e;
+    } else if (grep) {  // every tied run (equal first 16, or with !grep_k1 first 8 - pbits / 8, bytes) merge-sorted
         bool any_long = false;
         if ((e = fix_ties(k1_first, true, &any_long, true))) return e;
     }
@@ -1142,6 +1358,15 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
                 if ((e = sort_all(true))) return e;
                 if ((e = fix_ties(true, true, &any_long))) return e;
             }
+            if ((e = emit_output())) return e;
+        }
+    } else if (rank_ties) {
+        if ((e = emit_output())) return e;
+        RCHK(hipMemcpyAsync(ws->h_pinned + 3, flags + 3, 8, hipMemcpyDeviceToHost, s));
+        RCHK(hipStreamSynchronize(s));
+        if (ws->h_pinned[3]) {  // runs over kMidRun keys: merge-sorted, the output redone
+            uint8_t* tie = ws->key_a.as<uint8_t>();
+            if ((e = sort_long_runs(ws, r, pa, n, tie + n, ext, s))) return e;
             if ((e = emit_output())) return e;
         }
     } else if ((e = emit_output())) {

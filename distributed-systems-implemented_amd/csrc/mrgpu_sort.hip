@@ -20,7 +20,8 @@
 //    keys stably (each wave owns 1024 consecutive keys, 16 rows of 64: an 8-ballot
 //    match gives a lane its peers in the row, a per-wave LDS counter per digit
 //    carries the rank across rows), publishes its per-digit counts, finds the
-//    counts of all earlier tiles by decoupled look-back, and writes its keys
+//    counts of all earlier tiles by decoupled look-back (16 tiles' words per
+//    round trip), and writes its keys
 //    grouped by digit through LDS (consecutive lanes, consecutive addresses).
 // The look-back words carry the pass's epoch in their high half, so the state
 // array is never cleared: a word from an earlier pass simply reads as "not
@@ -31,6 +32,10 @@
 
 #include "mrgpu_device.h"
 
+#ifndef MRG_SORT_ROWS
+#define MRG_SORT_ROWS 16
+#endif
+
 namespace mrg {
 
 namespace {
@@ -39,11 +44,12 @@ constexpr int kRadixBits = 8;
 constexpr uint32_t kBins = 1u << kRadixBits;
 constexpr int kSortThreads = 256;  // 4 waves
 constexpr int kSortWaves = kSortThreads / 64;
-constexpr int kRowsPerWave = 16;
+constexpr int kRowsPerWave = MRG_SORT_ROWS;
 constexpr uint32_t kWaveKeys = 64 * kRowsPerWave;           // 1024
 constexpr uint32_t kTileKeys = kWaveKeys * kSortWaves;      // 4096
 constexpr int kMaxPasses = 8;                               // 64-bit keys
 constexpr uint32_t kFlagAgg = 1, kFlagInc = 2;
+constexpr int kLookWin = 16;  // look-back words loaded per round trip
 
 // exclusive scan of one value per thread over the 256-thread block; `red`
 // = 4 u32 of LDS.  Every thread must call it.
@@ -192,19 +198,37 @@ __global__ void __launch_bounds__(kSortThreads) radix_pass_kernel(const K* __res
         __hip_atomic_store(st, hi_inc | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
         __hip_atomic_store(st, hi_agg | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        unsigned long long* q = st - kBins;
+        // kLookWin earlier tiles' words per round trip (loads in flight
+        // together): a tile deep in the grid does not walk back one L2 round
+        // trip per tile while the tiles before it still hold only aggregates
+        int64_t j = (int64_t)t - 1;
         for (;;) {
-            const uint64_t s = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t hi = s & 0xFFFFFFFF00000000ull;
-            if (hi == hi_inc) {
-                prefix += (uint32_t)s;
-                break;
+            uint64_t sv[kLookWin];
+#pragma unroll
+            for (int q = 0; q < kLookWin; q++) {
+                const int64_t jj = j - q;
+                sv[q] = jj >= 0 ? __hip_atomic_load(state + (uint64_t)jj * kBins + tid, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                : hi_inc;  // (not reached: tile 0 is inclusive)
             }
-            if (hi == hi_agg) {
-                prefix += (uint32_t)s;
-                q -= kBins;
+            bool done = false, stop = false;
+            int used = 0;
+#pragma unroll
+            for (int q = 0; q < kLookWin; q++) {
+                if (done || stop) continue;
+                const uint64_t hi = sv[q] & 0xFFFFFFFF00000000ull;
+                if (hi == hi_inc) {
+                    prefix += (uint32_t)sv[q];
+                    done = true;
+                } else if (hi == hi_agg) {
+                    prefix += (uint32_t)sv[q];
+                    used++;
+                } else {
+                    stop = true;  // not published yet (an older epoch's word): poll again from here
+                }
             }
-            // else: that tile has not published yet (an older epoch's word)
+            if (done) break;
+            j -= used;
         }
         __hip_atomic_store(st, hi_inc | (prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

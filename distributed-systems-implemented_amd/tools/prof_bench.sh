@@ -10,3 +10,4 @@ timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $out/prof -o $w -- python3
 f=$(find $out/prof -name "*.db" | head -1)
 python3 distributed-systems-implemented_amd/tools/prof_summary.py "$f" $out/${w}_kernels.csv > /dev/null
 head -16 $out/${w}_kernels.csv
+rm -rf $out/prof  # the trace database (tens of MB): gpurun copies back at most 64 MiB

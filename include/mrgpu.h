@@ -195,7 +195,9 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        (0: the wc key pass over all 60/64 bits instead
  *                                        of the top 32), own_sort (0: rocPRIM onesweep
  *                                        radix passes instead of the hand-written LSD
- *                                        sort)   reduce sort variants
+ *                                        sort), tie_rank (0: grep's tied runs merge-sorted
+ *                                        together instead of ranked per run)   reduce sort
+ *                                        variants
  *   out_direct (-1: off)                 mrg_run_job (wc) writes the output lines straight into
  *                                        its pinned host buffer (default) instead of a
  *                                        device buffer + copy */

@@ -227,6 +227,40 @@ def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact, own):
         ctx.set_option("own_sort", 1)
 
 
+@pytest.mark.parametrize("tie_rank", [1, 0])
+def test_grep_tied_runs(ctx, tie_rank):
+    """grep lines tied on their first 16 bytes, ordered per run by rank (default:
+    waves for runs <= 64 keys, a workgroup's bitonic sort for 65-2048, the merge
+    sort beyond) or all merge-sorted (tie_rank=0): one prefix shared by 3000
+    distinct lines (R=1: a run over 2048; R=10: ~300 per partition), 40 prefixes
+    x 50 lines, pairs; suffixes that differ only past byte 64, NUL bytes, UTF-8,
+    lines that are prefixes of each other."""
+    rnd = np.random.default_rng(11)
+    lines = set()
+    big = b"distributed sys "  # 16 bytes
+    while len(lines) < 3000:
+        tail = bytes(rnd.integers(32, 127, size=int(rnd.integers(0, 90))).astype(np.uint8))
+        lines.add(big + tail)
+    for k in range(40):
+        pre = b"distributed %03d " % k + b"x" * 0  # 16 bytes
+        for _ in range(50):
+            lines.add(pre + bytes(rnd.integers(40, 44, size=int(rnd.integers(0, 6))).astype(np.uint8)))
+    far = b"distributed far " + b"y" * 48  # equal through byte 63
+    for _ in range(300):
+        lines.add(far + bytes(rnd.integers(0, 3, size=int(rnd.integers(0, 40))).astype(np.uint8)).replace(b"\n", b""))
+    for k in range(500):
+        lines.add(b"distributed pair%05d" % k)
+        lines.add(b"distributed pair%05d\xc3\xa9" % k)
+    ls = sorted(lines)
+    rnd.shuffle(ls)
+    text = b"\n".join(ls) + b"\n"
+    ctx.set_option("tie_rank", tie_rank)
+    try:
+        check(ctx, "grep:distributed", [text, text[: len(text) // 2] + b"\n"], nreduces=(1, 10))
+    finally:
+        ctx.set_option("tie_rank", 1)
+
+
 @pytest.mark.parametrize("own", [1, 0])
 @pytest.mark.parametrize("kind,bits", [("u32", 32), ("u32", 4), ("u32", 20), ("u64", 64), ("u64", 60), ("u64", 12),
                                        ("u64keys", 34), ("u64keys", 64)])
