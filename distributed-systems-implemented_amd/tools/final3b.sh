@@ -11,3 +11,7 @@ bash distributed-systems-implemented_amd/tools/prof_bench.sh final3/prof c2
 bash distributed-systems-implemented_amd/tools/pmc_passes.sh $out/pmc --modes 0 --reps 1
 python3 distributed-systems-implemented_amd/tools/pmc_summary.py --each $out/pmc wc_map_kernel > $out/pmc_summary.json
 head -60 $out/pmc_summary.json
+bash distributed-systems-implemented_amd/tools/pmc_passes.sh $out/pmc_c5 --workload c5 --gb 10 --modes 0 --reps 1
+python3 distributed-systems-implemented_amd/tools/pmc_summary.py --each $out/pmc_c5 wc_map_kernel > $out/pmc_c5_summary.json
+head -60 $out/pmc_c5_summary.json
+bash distributed-systems-implemented_amd/tools/ab_opts.sh final3/abo "c2u" "--opt own_sort=1" "--opt own_sort=0"
