@@ -17,9 +17,11 @@
 //  - radix_pass_kernel, per pass: a workgroup takes the next 4096-key tile (a
 //    device counter, reset by whoever takes the last tile, so tiles start in
 //    order and the look-back cannot wait on a tile that never runs), ranks its
-//    keys stably (each wave owns 1024 consecutive keys, 16 rows of 64: an 8-ballot
-//    match gives a lane its peers in the row, a per-wave LDS counter per digit
-//    carries the rank across rows), publishes its per-digit counts, finds the
+//    keys stably (16 waves; each owns 256 consecutive keys, 4 rows of 64: an
+//    8-ballot match gives a lane its peers in the row, a per-wave LDS counter
+//    per digit carries the rank across rows; 4 waves x 16 rows measured ~50 us
+//    slower per C3 reduce, 8 x 8 and 8 x 16 in between), publishes its
+//    per-digit counts (threads 0-255, one digit each), finds the
 //    counts of all earlier tiles by decoupled look-back (16 tiles' words per
 //    round trip), and writes its keys
 //    grouped by digit through LDS (consecutive lanes, consecutive addresses).
@@ -33,7 +35,10 @@
 #include "mrgpu_device.h"
 
 #ifndef MRG_SORT_ROWS
-#define MRG_SORT_ROWS 16
+#define MRG_SORT_ROWS 4
+#endif
+#ifndef MRG_SORT_WAVES
+#define MRG_SORT_WAVES 16
 #endif
 
 namespace mrg {
@@ -42,8 +47,9 @@ namespace {
 
 constexpr int kRadixBits = 8;
 constexpr uint32_t kBins = 1u << kRadixBits;
-constexpr int kSortThreads = 256;  // 4 waves
-constexpr int kSortWaves = kSortThreads / 64;
+constexpr int kSortWaves = MRG_SORT_WAVES;  // waves per pass workgroup
+constexpr int kSortThreads = 64 * kSortWaves;
+constexpr int kHistThreads = 256;
 constexpr int kRowsPerWave = MRG_SORT_ROWS;
 constexpr uint32_t kWaveKeys = 64 * kRowsPerWave;           // 1024
 constexpr uint32_t kTileKeys = kWaveKeys * kSortWaves;      // 4096
@@ -51,8 +57,9 @@ constexpr int kMaxPasses = 8;                               // 64-bit keys
 constexpr uint32_t kFlagAgg = 1, kFlagInc = 2;
 constexpr int kLookWin = 16;  // look-back words loaded per round trip
 
-// exclusive scan of one value per thread over the 256-thread block; `red`
-// = 4 u32 of LDS.  Every thread must call it.
+// exclusive scan of one value per thread over an NW-wave block; `red` = NW
+// u32 of LDS.  Every thread must call it.
+template <int NW>
 __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red, uint32_t* total) {
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const uint32_t incl = wave_incl_scan_dpp(v);
@@ -60,7 +67,7 @@ __device__ __forceinline__ uint32_t block_excl_scan(uint32_t v, uint32_t* red, u
     __syncthreads();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
-    for (int i = 0; i < kSortWaves; i++) {
+    for (int i = 0; i < NW; i++) {
         const uint32_t r = red[i];
         pre += (uint32_t)i < w ? r : 0u;
         tot += r;
@@ -78,16 +85,16 @@ __device__ __forceinline__ uint32_t digit_of(K key, uint32_t shift, uint32_t mas
 // hist: npasses * 256 u32, zero on entry (left zero on exit); starts: the
 // passes' exclusive digit starts; ticket: zero on entry (left zero).
 template <class K>
-__global__ void __launch_bounds__(kSortThreads) radix_hist_kernel(const K* __restrict__ keys, uint64_t n, uint32_t bits,
+__global__ void __launch_bounds__(kHistThreads) radix_hist_kernel(const K* __restrict__ keys, uint64_t n, uint32_t bits,
                                                                   uint32_t npasses, uint32_t* hist, uint32_t* starts,
                                                                   uint32_t* ticket) {
     __shared__ uint32_t h[kMaxPasses * kBins];
-    __shared__ uint32_t red[kSortWaves];
+    __shared__ uint32_t red[kHistThreads / 64];
     __shared__ uint32_t last;
-    for (uint32_t i = threadIdx.x; i < npasses * kBins; i += kSortThreads) h[i] = 0;
+    for (uint32_t i = threadIdx.x; i < npasses * kBins; i += kHistThreads) h[i] = 0;
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * kSortThreads;
-    for (uint64_t i = (uint64_t)blockIdx.x * kSortThreads + threadIdx.x; i < n; i += stride) {
+    const uint64_t stride = (uint64_t)gridDim.x * kHistThreads;
+    for (uint64_t i = (uint64_t)blockIdx.x * kHistThreads + threadIdx.x; i < n; i += stride) {
         const K k = keys[i];
         for (uint32_t p = 0; p < npasses; p++) {
             const uint32_t shift = p * kRadixBits;
@@ -96,7 +103,7 @@ __global__ void __launch_bounds__(kSortThreads) radix_hist_kernel(const K* __res
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < npasses * kBins; i += kSortThreads)
+    for (uint32_t i = threadIdx.x; i < npasses * kBins; i += kHistThreads)
         if (h[i]) atomicAdd(&hist[i], h[i]);
     __threadfence();
     __syncthreads();
@@ -108,7 +115,7 @@ __global__ void __launch_bounds__(kSortThreads) radix_hist_kernel(const K* __res
         uint32_t* hp = hist + p * kBins;
         const uint32_t v = __hip_atomic_load(hp + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         uint32_t tot;
-        starts[p * kBins + threadIdx.x] = block_excl_scan(v, red, &tot);
+        starts[p * kBins + threadIdx.x] = block_excl_scan<kHistThreads / 64>(v, red, &tot);
         hp[threadIdx.x] = 0u;
     }
     if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -139,8 +146,7 @@ __global__ void __launch_bounds__(kSortThreads) radix_pass_kernel(const K* __res
         if (t == ntiles - 1) __hip_atomic_store(tile_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         L.tile = t;
     }
-#pragma unroll
-    for (int i = 0; i < kSortWaves; i++) L.wcnt[i][tid] = 0;
+    for (uint32_t i = tid; i < kSortWaves * kBins; i += kSortThreads) (&L.wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint32_t t = L.tile;
     const uint64_t tile0 = (uint64_t)t * kTileKeys;
@@ -178,16 +184,20 @@ __global__ void __launch_bounds__(kSortThreads) radix_pass_kernel(const K* __res
         if (ok && before == 0) L.wcnt[w][d] = old + (uint32_t)__popcll(peers);
     }
     __syncthreads();
-    // thread tid = digit: wave offsets, the tile's count, the tile-local start
+    // thread tid < 256 = digit: wave offsets, the tile's count, the tile-local start
+    const bool dig = tid < kBins;
     uint32_t cnt = 0;
+    if (dig) {
 #pragma unroll
-    for (int i = 0; i < kSortWaves; i++) {
-        const uint32_t c = L.wcnt[i][tid];
-        L.wcnt[i][tid] = cnt;
-        cnt += c;
+        for (int i = 0; i < kSortWaves; i++) {
+            const uint32_t c = L.wcnt[i][tid];
+            L.wcnt[i][tid] = cnt;
+            cnt += c;
+        }
     }
     uint32_t tot;
-    const uint32_t lstart = block_excl_scan(cnt, L.red, &tot);
+    const uint32_t lstart = block_excl_scan<kSortWaves>(cnt, L.red, &tot);
+    if (dig) {
     // decoupled look-back for digit tid: publish this tile's count, sum the
     // earlier tiles' counts back to the first inclusive prefix
     unsigned long long* st = state + (uint64_t)t * kBins + tid;
@@ -236,6 +246,7 @@ __global__ void __launch_bounds__(kSortThreads) radix_pass_kernel(const K* __res
     // the tile-local start of each digit, kept in the wave-offset table
 #pragma unroll
     for (int i = 0; i < kSortWaves; i++) L.wcnt[i][tid] += lstart;
+    }  // dig
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < kRowsPerWave; r++) {
@@ -324,7 +335,7 @@ static int radix_sort_impl(RadixWs* w, const K* k_in, K* k_out, const uint32_t* 
     K* k_tmp = (K*)w->buf;
     uint32_t* v_tmp = (uint32_t*)((char*)w->buf + ((n * sizeof(K) + 255) & ~(size_t)255));
     const unsigned hgrid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + 8191) / 8192, 1), 512);
-    radix_hist_kernel<K><<<hgrid, kSortThreads, 0, s>>>(k_in, n, bits, npasses, hist, starts, ticket);
+    radix_hist_kernel<K><<<hgrid, kHistThreads, 0, s>>>(k_in, n, bits, npasses, hist, starts, ticket);
     const K* src_k = k_in;
     const uint32_t* src_v = v_in;
     for (uint32_t p = 0; p < npasses; p++) {
