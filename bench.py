@@ -82,7 +82,13 @@ def file_params(w: dict, i: int, nfiles: int):
     return C.wc_params()
 
 
-def gen_corpus(w: dict, rank: int, file_mb: int, nfiles: int):
+def file_seed(w: dict, rank: int, split: int, i: int) -> int:
+    """Seed of file i of split `split` on `rank`: every (rank, split) is a distinct
+    input (split 0 keeps the seeds of earlier rounds' single-split bench lines)."""
+    return w["seed"] + 1000 * rank + 100_000 * split + i
+
+
+def gen_corpus(w: dict, rank: int, file_mb: int, nfiles: int, split: int = 0):
     """nfiles generated files back to back in one buffer.  Every file ends with '\n',
     so the concatenation is word-for-word the same input as separate splits."""
     voc = C.Vocab(w["kind"], w["s"], w["V"], w["seed"])
@@ -90,13 +96,13 @@ def gen_corpus(w: dict, rank: int, file_mb: int, nfiles: int):
     sz = file_mb * 1_000_000
     uniform = w["app"] == "grep" or w["V"] <= 10**6
     if uniform:
-        seeds = [w["seed"] + 1000 * rank + i for i in range(nfiles)]
+        seeds = [file_seed(w, rank, split, i) for i in range(nfiles)]
         voc.fill_files([sz] * nfiles, seeds, file_params(w, 0, nfiles), threads=min(16, os.cpu_count() or 1), out=buf)
     else:
         from concurrent.futures import ThreadPoolExecutor  # the C generator releases the GIL
 
         def one(i):
-            voc.fill_files([sz], [w["seed"] + 1000 * rank + i], file_params(w, i, nfiles), threads=1,
+            voc.fill_files([sz], [file_seed(w, rank, split, i)], file_params(w, i, nfiles), threads=1,
                            out=buf[i * sz:(i + 1) * sz])
         with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
             list(ex.map(one, range(nfiles)))
@@ -288,15 +294,25 @@ def upload(host: np.ndarray, local: int):
     return dev
 
 
-def timed_steps(ctx: Context, run_step, steps: int, warmup: int, world: int):
+def download(dev) -> np.ndarray:
+    """A resident split back to host memory (the oracle check reads it there; the
+    host copies are not kept while several splits are resident)."""
+    return dev.cpu().numpy()
+
+
+def timed_steps(ctx: Context, run_step, steps: int, warmup: int, world: int, nsplits: int = 1):
     """W untimed warmup steps (the first one's wall time is reported as the cold
     split: fresh dictionary, first allocations), then exactly K steps between a
-    barrier + synchronize on both sides; returns (max-over-ranks seconds, per-step stats, cold ms)."""
+    barrier + synchronize on both sides; step i maps resident split i % nsplits
+    (run_step(split)), so every timed step meets a split other than the one the
+    context's kept state (dictionary, spill layout, segment capacities) came
+    from, as a worker's next map task does.  Returns (max-over-ranks seconds,
+    per-step stats, cold ms, cold stats)."""
     cold_ms, cold_st = None, None
     for i in range(warmup):
         ctx.sync()
         t0 = time.perf_counter()
-        run_step()
+        run_step(i % nsplits)
         ctx.sync()
         if i == 0:
             cold_ms = (time.perf_counter() - t0) * 1e3
@@ -307,8 +323,8 @@ def timed_steps(ctx: Context, run_step, steps: int, warmup: int, world: int):
     torch.cuda.synchronize()
     ctx.sync()
     t_start = time.perf_counter()
-    for _ in range(steps):
-        run_step()
+    for i in range(steps):
+        run_step((warmup + i) % nsplits)
         stats.append(ctx.stats())
     ctx.sync()
     torch.cuda.synchronize()
@@ -323,15 +339,15 @@ def timed_steps(ctx: Context, run_step, steps: int, warmup: int, world: int):
     return t_max, stats, cold_ms, cold_st
 
 
-def no_shuffle_time(ctx: Context, run_step, steps: int, shared: bool) -> float:
+def no_shuffle_time(ctx: Context, run_step, steps: int, shared: bool, nsplits: int = 1) -> float:
     """T(1) of the weak-scaling efficiency: the same per-GPU splits with no
     shuffle (every partition reduced locally), in this process; max over ranks."""
     ctx.set_option("skip_exchange", 1)
     dist.barrier()
     ctx.sync()
     t1 = time.perf_counter()
-    for _ in range(steps):
-        run_step()
+    for i in range(steps):
+        run_step(i % nsplits)
     ctx.sync()
     t1 = time.perf_counter() - t1
     dist.barrier()
@@ -342,14 +358,26 @@ def no_shuffle_time(ctx: Context, run_step, steps: int, shared: bool) -> float:
 
 
 def multi_fields(stats: list[dict], t_max: float, t1: float, world: int, shared: bool, ndev: int) -> dict:
-    ex_ms = sum(st["exchange_ms"] for st in stats) / len(stats)
-    snd = sum(st["shuffle_send_bytes"] for st in stats) / len(stats)
-    v = torch.tensor([ex_ms, snd], dtype=torch.float64)
+    def mean(k):
+        return sum(st[k] for st in stats) / len(stats)
+    ex_ms, a2a_ms, unp_ms = mean("exchange_ms"), mean("exchange_a2a_ms"), mean("exchange_unpack_ms")
+    snd = mean("shuffle_send_bytes")
+    v = torch.tensor([ex_ms, a2a_ms, unp_ms, snd], dtype=torch.float64)
     dist.all_reduce(v, op=dist.ReduceOp.MAX)
-    ex_max, snd_max = float(v[0]), float(v[1])
+    ex_max, a2a_max, unp_max, snd_max = (float(x) for x in v)
+    # what RCCL itself saw, and each rank's device (gathered to every rank)
+    me = {"rank": int(os.environ.get("RANK", "0")), "rccl_nranks": int(stats[-1]["rccl_nranks"]),
+          "rccl_rank": int(stats[-1]["rccl_rank"]), "device": int(stats[-1]["device"]),
+          "local_rank": int(os.environ.get("LOCAL_RANK", "0"))}
+    ranks = [None] * world
+    dist.all_gather_object(ranks, me)
     links = min(world - 1, 7)
-    per_gpu_bw = snd / (ex_ms / 1e3) / 1e9 if ex_ms > 0 else 0.0
-    m = {"exchange_ms": round(ex_max, 3), "shuffle_bytes_per_gpu": int(snd_max),
+    # the xGMI rate is taken over the all-to-alls alone (the unpack and the
+    # owner's re-aggregation are HBM work, reported separately)
+    per_gpu_bw = snd / (a2a_ms / 1e3) / 1e9 if a2a_ms > 0 else 0.0
+    m = {"exchange_ms": round(ex_max, 3), "exchange_a2a_ms": round(a2a_max, 3),
+         "exchange_unpack_ms": round(unp_max, 3), "shuffle_bytes_per_gpu": int(snd_max),
+         "rccl_nranks": sorted({r["rccl_nranks"] for r in ranks}), "ranks": ranks,
          "xgmi_achieved_GBps": round(per_gpu_bw, 2), "xgmi_peak_GBps": links * XGMI_LINK_GBS,
          "xgmi_frac": round(per_gpu_bw / (links * XGMI_LINK_GBS), 4),
          "t1_ms_per_step": round(t1 / len(stats) * 1e3, 3), "tP_ms_per_step": round(t_max / len(stats) * 1e3, 3),
@@ -362,14 +390,18 @@ def multi_fields(stats: list[dict], t_max: float, t1: float, world: int, shared:
 def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: bool, ndev: int) -> dict:
     """SURVEY.md §8(d) defines E(P) on C5 (25 GB per GPU, 1e7 distinct keys,
     R = 64): the same timed-step / T(1) measurement on that workload, in this
-    run, after the headline workload's buffers are released."""
+    run, after the headline workload's buffers are released (args.scaling_splits
+    resident splits per rank, rotated as in the headline)."""
     w = WORKLOADS[wname]
+    nsplits = max(1, args.scaling_splits)
+    devs = []
     t0 = time.time()
-    host = gen_corpus(w, rank, w["file_mb"], w["files"])
-    nbytes = int(host.size)
-    log(f"[{wname}] generated {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
-    dev = upload(host, local)
-    del host
+    for sp in range(nsplits):
+        host = gen_corpus(w, rank, w["file_mb"], w["files"], sp)
+        devs.append(upload(host, local))
+        del host
+    nbytes = int(devs[0].numel())
+    log(f"[{wname}] generated {nsplits} x {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
     ctx = Context(local)
     for o in args.opt:
         k, v = o.split("=")
@@ -380,14 +412,14 @@ def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: 
         ctx.comm_init(obj[0], world, rank)
     else:
         ctx.set_option("skip_exchange", 1)
-    dptr = dev.data_ptr()
+    dptrs = [d.data_ptr() for d in devs]
 
-    def run_step():
-        return ctx.run_job(MRG_APP_WC, device_ptr=dptr, nbytes=nbytes, nreduce=w["nreduce"], copy_out=False)
+    def run_step(sp=0):
+        return ctx.run_job(MRG_APP_WC, device_ptr=dptrs[sp], nbytes=nbytes, nreduce=w["nreduce"], copy_out=False)
 
     steps = max(1, args.scaling_steps)
-    t_max, stats, _, _ = timed_steps(ctx, run_step, steps, 1, world)
-    p, n, offs = run_step()
+    t_max, stats, _, _ = timed_steps(ctx, run_step, steps, 1, world, nsplits)
+    p, n, offs = run_step(0)
     import ctypes
     out = ctypes.string_at(p, n) if n else b""
     parts = [out[offs[i]:offs[i + 1]] for i in range(w["nreduce"])]
@@ -395,15 +427,16 @@ def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: 
     owned_ok = all(not parts[r] for r in range(w["nreduce"]) if r % world != rank) or shared
     tw = torch.tensor([chk["total_words"]], dtype=torch.int64)
     dist.all_reduce(tw)
-    t1 = no_shuffle_time(ctx, run_step, steps, shared)
+    t1 = no_shuffle_time(ctx, run_step, steps, shared, nsplits)
     res = {"workload": f"{w['desc']}; {nbytes / 1e9:.2f} GB per GPU", "nreduce": w["nreduce"],
+           "splits_per_gpu": nsplits,
            "value": round(nbytes * world * steps / t_max / 1e9, 3), "unit": "GB/s", "steps": steps,
            "ms_per_step": round(t_max / steps * 1e3, 3),
            **multi_fields(stats, t_max, t1, world, shared, ndev),
            "checks": {"sorted_unique": chk["sorted_unique"], "partition_ok": chk["partition_ok"],
                       "non_owned_empty": owned_ok, "total_words": int(tw.item())}}
     ctx.close()
-    del dev
+    del devs
     torch.cuda.empty_cache()
     return res
 
@@ -425,6 +458,9 @@ def main():
     ap.add_argument("--no-oracle", action="store_true", help="skip the full-size exact check against the C oracle")
     ap.add_argument("--scaling-workload", default="c5", help="N > 1: workload of the E(P) sub-run ('none' to skip)")
     ap.add_argument("--scaling-steps", type=int, default=2)
+    ap.add_argument("--splits", type=int, default=0,
+                    help="distinct splits resident per rank, rotated over the timed steps (0: 3 at N=1, 2 at N>1)")
+    ap.add_argument("--scaling-splits", type=int, default=2, help="resident splits per rank in the E(P) sub-run")
     ap.add_argument("--rehearsal", action="store_true",
                     help="allow more ranks than visible GPUs (ranks share devices, no RCCL exchange: not a measurement)")
     ap.add_argument("--opt", action="append", default=[], help="library option name=value (experiments; repeatable)")
@@ -459,10 +495,19 @@ def main():
     torch.zeros(1, device=f"cuda:{local}").add_(1)
     torch.cuda.synchronize()
 
+    # S distinct splits resident in HBM (seeds per rank and split); the timed
+    # steps rotate over them, so the context's kept state never meets the split
+    # it was derived from.  The host copies are dropped after the upload (read
+    # back for the oracle check) to keep host memory at one split per rank.
+    nsplits = args.splits if args.splits > 0 else (3 if world == 1 else 2)
     t0 = time.time()
-    host = gen_corpus(w, rank, args.file_mb, args.files)
-    nbytes = int(host.size)
-    log(f"generated {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
+    devs = []
+    for sp in range(nsplits):
+        host = gen_corpus(w, rank, args.file_mb, args.files, sp)
+        devs.append(upload(host, local))
+        del host
+    nbytes = int(devs[0].numel())
+    log(f"generated {nsplits} x {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
 
     ctx = Context(local)
     for o in args.opt:
@@ -475,57 +520,81 @@ def main():
     if shared:
         log(f"{world} ranks on {ndev} device(s): rehearsal without the RCCL exchange")
         ctx.set_option("skip_exchange", 1)
-    dev = upload(host, local)
-    dptr = dev.data_ptr()
+    dptrs = [d.data_ptr() for d in devs]
     ctx.sync()
 
-    def run_step():
+    def run_step(sp=0):
         if grep:
-            return ctx.run_job(MRG_APP_GREP, pattern=PATTERN, device_ptr=dptr, nbytes=nbytes, nreduce=args.nreduce,
-                               copy_out=False)
-        return ctx.run_job(MRG_APP_WC, device_ptr=dptr, nbytes=nbytes, nreduce=args.nreduce, copy_out=False)
+            return ctx.run_job(MRG_APP_GREP, pattern=PATTERN, device_ptr=dptrs[sp], nbytes=nbytes,
+                               nreduce=args.nreduce, copy_out=False)
+        return ctx.run_job(MRG_APP_WC, device_ptr=dptrs[sp], nbytes=nbytes, nreduce=args.nreduce, copy_out=False)
 
-    t_max, stats, cold_ms, cold_st = timed_steps(ctx, run_step, args.steps, args.warmup, world)
+    t_max, stats, cold_ms, cold_st = timed_steps(ctx, run_step, args.steps, args.warmup, world, nsplits)
     kern_ms = [st["map_kernel_ms"] for st in stats]
     log("map kernel ms per timed step: " + " ".join(f"{k:.2f}" for k in kern_ms))
     log("aggregation ms per timed step: " + " ".join(f"{st['agg_ms']:.2f}" for st in stats))
+    # the same K steps re-mapping ONE split (the rounds-1-3 measurement), for comparison
+    same = None
+    if nsplits > 1:
+        t_same, st_same, _, _ = timed_steps(ctx, lambda sp: run_step(0), args.steps, 1, world, 1)
+        same = {"value": round(nbytes * world * args.steps / t_same / 1e9, 3),
+                "ms_per_step": round(t_same / args.steps * 1e3, 3),
+                "map_kernel_ms": round(sum(x["map_kernel_ms"] for x in st_same) / len(st_same), 3),
+                "agg_ms": round(sum(x["agg_ms"] for x in st_same) / len(st_same), 3),
+                "dict_ms": round(sum(x["dict_ms"] for x in st_same) / len(st_same), 3)}
 
-    # output of one more step (context-owned buffer) -> checks at full size, outside the timed region
+    # output of one more step per split (context-owned buffer) -> checks at full
+    # size, outside the timed region: every resident split against the oracle
     import ctypes
-    p, n, offs = run_step()
-    out = ctypes.string_at(p, n) if n else b""
-    parts = [out[offs[i]:offs[i + 1]] for i in range(args.nreduce)]
-    checks = check_output(parts, args.nreduce, w["app"])
-    checks["deterministic"] = hashlib.sha256(out).hexdigest() == hashlib.sha256(
-        ctypes.string_at(*run_step()[:2])).hexdigest()
-    if not grep:
-        # Σ counts of the output must equal an independent count of the input's words
-        indep = ascii_word_count(dev)
-        checks["total_words_independent"] = indep
-        checks["total_words_match"] = None if indep is None else indep == checks["total_words"]
-    if world > 1:
-        key = "matching_lines" if grep else "total_words"
-        tw = torch.tensor([checks[key]], dtype=torch.int64)
-        dist.all_reduce(tw)
-        checks[key] = int(tw.item())
-        if not grep and checks.get("total_words_independent") is not None:
-            ti = torch.tensor([checks["total_words_independent"]], dtype=torch.int64)
-            dist.all_reduce(ti)
-            checks["total_words_independent"] = int(ti.item())
-            checks["total_words_match"] = checks["total_words_independent"] == checks[key]
-    if not args.no_oracle and not shared:
-        checks.update(oracle_exact_check(w, host, parts, args.nreduce, rank, world))
-    del out, parts
+    checks = {}
+    per_split = []
+    for sp in range(nsplits):
+        p, n, offs = run_step(sp)
+        out = ctypes.string_at(p, n) if n else b""
+        parts = [out[offs[i]:offs[i + 1]] for i in range(args.nreduce)]
+        ck = check_output(parts, args.nreduce, w["app"])
+        if sp == 0:
+            ck["deterministic"] = hashlib.sha256(out).hexdigest() == hashlib.sha256(
+                ctypes.string_at(*run_step(0)[:2])).hexdigest()
+        if not grep:
+            # Σ counts of the output must equal an independent count of the input's words
+            indep = ascii_word_count(devs[sp])
+            ck["total_words_independent"] = indep
+            ck["total_words_match"] = None if indep is None else indep == ck["total_words"]
+        if world > 1:
+            key = "matching_lines" if grep else "total_words"
+            tw = torch.tensor([ck[key]], dtype=torch.int64)
+            dist.all_reduce(tw)
+            ck[key] = int(tw.item())
+            if not grep and ck.get("total_words_independent") is not None:
+                ti = torch.tensor([ck["total_words_independent"]], dtype=torch.int64)
+                dist.all_reduce(ti)
+                ck["total_words_independent"] = int(ti.item())
+                ck["total_words_match"] = ck["total_words_independent"] == ck[key]
+        if not args.no_oracle and not shared:
+            host = download(devs[sp])
+            ck.update(oracle_exact_check(w, host, parts, args.nreduce, rank, world))
+            del host
+        del out, parts
+        per_split.append(ck)
+    checks.update(per_split[0])
+    for k in ("sorted_unique", "partition_ok", "total_words_match", "exact_vs_oracle", "lines_format_ok"):
+        vals = [c.get(k) for c in per_split if c.get(k) is not None]
+        if vals:
+            checks[k] = all(vals)
+    if nsplits > 1:
+        checks["per_split"] = per_split
 
     # N > 1: the shuffle's share and the weak-scaling efficiency against the
     # same ranks running their splits with no shuffle (T(1) of the same per-GPU
     # work, measured in this process, every partition reduced locally)
     multi = None
     if world > 1:
-        t1 = no_shuffle_time(ctx, run_step, args.steps, shared)
+        t1 = no_shuffle_time(ctx, run_step, args.steps, shared, nsplits)
         multi = multi_fields(stats, t_max, t1, world, shared, ndev)
         multi["note"] = ("shuffle bytes = wire bytes a rank sends to the other ranks (max over ranks of the mean over "
-                         "timed steps; 24-byte wire records + long-key bytes); xgmi_frac = those bytes / exchange time / "
+                         "timed steps; 24-byte wire records + long-key bytes); xgmi_frac = those bytes / all-to-all time "
+                         "(exchange_a2a_ms; exchange_ms adds the owner's unpack + exact re-aggregation) / "
                          "(min(P-1,7) x 153 GB/s); E(P) = T(1) / T(P), T(1) = the same per-GPU splits run with no "
                          "shuffle in this process")
 
@@ -552,6 +621,8 @@ def main():
     pcie = None
     step = 1 << 30
     if world == 1 and not args.no_pcie:
+        dev = devs[0]
+        host = download(dev)
         ctx.sync()
         t0 = time.perf_counter()  # the copy alone (pageable host -> HBM), for comparison
         for off in range(0, nbytes, step):
@@ -577,7 +648,8 @@ def main():
         cpu = cpu_baseline(w, args.cpu_sample_files, args.cpu_sample_mb, args.cpu_seq_files, args.nreduce, ctx)
 
     ctx.close()
-    del dev, host
+    dev = host = None
+    del devs, dev, host
     torch.cuda.empty_cache()
     scaling = None
     if world > 1 and args.scaling_workload not in ("", "none") and args.scaling_workload != args.workload:
@@ -598,7 +670,9 @@ def main():
             "dtype": "u8",
             "data": "synthetic (deterministic Zipf corpus from csrc/corpus.c; reference pg-*.txt not bundled)",
             "config": {"workload": f"{w['desc']}; {nbytes / 1e9:.2f} GB per GPU ({args.files} files x "
-                                   f"{args.file_mb} MB), device-resident input",
+                                   f"{args.file_mb} MB), device-resident input; {nsplits} distinct splits per GPU "
+                                   f"resident, timed steps rotate over them",
+                       "splits_per_gpu": nsplits,
                        "nreduce": args.nreduce, "input_bytes_per_gpu": nbytes, "parallelism": f"dp{world}", **({"options": args.opt} if args.opt else {}),
                        "shuffle": "RCCL all-to-all" if world > 1 else "none (single GPU)"},
             **({"rehearsal": True} if shared else {}),
@@ -615,12 +689,14 @@ def main():
                           "dict": round(last["dict_ms"], 3), "agg": round(last["agg_ms"], 3),
                           "exchange": round(last["exchange_ms"], 3), "reduce": round(last["reduce_ms"], 3),
                           "d2h": round(last["d2h_ms"], 3)},
+            "same_split_value": same,
             "cold_split": {"ms": round(cold_ms, 3) if cold_ms is not None else None,
                            "dict_ms": round(cold_st["dict_ms"], 3) if cold_st else None,
                            "map_kernel_ms": round(cold_st["map_kernel_ms"], 3) if cold_st else None,
                            "note": "the first warmup step: a fresh context (dictionary built from the split's "
-                                   "sample, first allocations); the timed steps re-map the same split with the "
-                                   "context's dictionary and buffers kept, as a worker's later map tasks do"},
+                                   "sample, first allocations); the timed steps then rotate over the resident "
+                                   "splits with the context's buffers kept, as a worker's later map tasks do; "
+                                   "same_split_value = the same steps re-mapping split 0 only"},
             "staged_input_bytes": int(last["staged_bytes"]),
             "distinct_keys": int(last["distinct_keys"]),
             "dict_hit_words": int(last["dict_hits"]),

@@ -209,7 +209,7 @@ struct mrg_ctx {
     ExchSide* exch = nullptr;  // RCCL shuffle buffers, kept across calls (no hipMalloc / hipFree per step)
     int device = 0;
     hipStream_t s = nullptr;
-    hipEvent_t ev[12] = {};  // 0-3, 8-10: map phases; 4-5 reduce; 6-7 exchange / d2h
+    hipEvent_t ev[13] = {};  // 0-3, 8-10: map phases; 4-5 reduce; 6-7 exchange / d2h; 12 exchange end
     std::string err;
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
@@ -221,6 +221,7 @@ struct mrg_ctx {
     DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
     bool seg_sync = true;               // size the miss segments from this split's totals (host read)
     bool out_direct = true;             // mrg_run_job: output lines written straight into pinned host memory
+    bool grep_literal = false;          // grep: regexp metacharacters taken literally (QuoteMeta) instead of refused
     uint64_t arena_hint = 0;            // wc: long-key bytes expected in a split (the previous one's + 25 %)
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     DevBuf ghits, glines, gdefer;        // grep: sorted hits, resolved (start, end) lines, deferred hits
@@ -1199,6 +1200,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set_compact_ties(c->rws, v >= 0);
     } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default) or via a copy (-1)
         c->out_direct = v >= 0;
+    } else if (!strcmp(name, "grep_literal")) {  // grep: metacharacters quoted (1) instead of refused (0)
+        c->grep_literal = v > 0;
     } else if (!strcmp(name, "tie_rank")) {  // grep reduce: tied runs ranked per run (1, default) or merge-sorted (0)
         reduce_ws_set_tie_rank(c->rws, v != 0);
     } else if (!strcmp(name, "own_sort")) {  // reduce radix passes: hand-written LSD sort (1, default) or rocPRIM (0)
@@ -1266,6 +1269,9 @@ int mrg_memcpy_h2d(mrg_ctx* c, void* dst, const void* src, size_t n) {
 }
 int mrg_sort_pairs(mrg_ctx* c, void* keys, void* vals, size_t n, int key_bytes, unsigned bits) {
     if (!c || (n && !keys)) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    if (n > 0xFFFFFFFFull) return fail(c, MRG_EINVAL, "mrg_sort_pairs: at most 2^32 - 1 keys");
     const int e = sort_in_place(c->rws, key_bytes, keys, (uint32_t*)vals, n, bits, c->s);
     if (e == (int)hipErrorInvalidValue) return fail(c, MRG_EINVAL, "mrg_sort_pairs: key_bytes 4 or 8; 4-byte keys need values");
     if (e) return fail(c, MRG_EDEVICE, "mrg_sort_pairs: %s", hipGetErrorString((hipError_t)e));
@@ -1296,6 +1302,19 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
     if (!c || !out || (len && !buf) || nreduce == 0 || (app != MRG_APP_WC && app != MRG_APP_GREP))
         return c ? fail(c, MRG_EINVAL, "mrg_map: bad arguments") : MRG_EINVAL;
     if (app == MRG_APP_GREP && plen && !pat) return fail(c, MRG_EINVAL, "mrg_map: null pattern");
+    // dgrep.go:20 compiles the pattern as a regexp; this path matches literals
+    // only.  A valid-UTF-8 pattern holding a metacharacter would silently match
+    // differently, so it is refused unless the caller asks for QuoteMeta
+    // semantics (option grep_literal).  Invalid UTF-8 keeps dgrep.go:20-23's
+    // behaviour (regexp.Compile fails: no lines).
+    if (app == MRG_APP_GREP && !c->grep_literal && go_valid_utf8(pat, plen)) {
+        for (size_t i = 0; i < plen; i++)
+            if (pat[i] < 0x80 && strchr("\\.+*?()|[]{}^$", (char)pat[i]) && pat[i] != 0)
+                return fail(c, MRG_EINVAL,
+                            "mrg_map: grep pattern holds the regexp metacharacter '%c' (dgrep.go:20 compiles a "
+                            "regexp; this path matches literals: set option grep_literal=1 for QuoteMeta semantics)",
+                            (char)pat[i]);
+    }
     *out = nullptr;
     int rc;
     if ((rc = bind(c))) return rc;
@@ -1925,7 +1944,8 @@ static int exch_pack(mrg_ctx* c, const Recs& r, int P, ExchSide& x) {
 }
 
 // Step 4: unpack the received records into a Recs view and re-aggregate exactly.
-static int exch_finish(mrg_ctx* c, const mrg_parts* local, int P, ExchSide& x, mrg_parts** owned) {
+static int exch_finish(mrg_ctx* c, const mrg_parts* local, int P, ExchSide& x, mrg_parts** owned,
+                       hipEvent_t done = nullptr) {
     int rc;
     const ExchPlan& pl = x.plan;
     std::vector<uint64_t> hsrc(2 * P);
@@ -1943,6 +1963,7 @@ static int exch_finish(mrg_ctx* c, const mrg_parts* local, int P, ExchSide& x, m
                                               (const uint64_t*)x.rmeta.p + P, (uint32_t)P, tmp->r);
     if (hipGetLastError() != hipSuccess) { mrg_parts_free(tmp); return fail(c, MRG_EDEVICE, "unpack launch"); }
     rc = aggregate(c, {tmp->r}, local->app, local->nreduce, owned);
+    if (done) hipEventRecord(done, c->s);
     hipError_t e = hipStreamSynchronize(c->s);
     mrg_parts_free(tmp);
     if (rc) return rc;
@@ -1965,6 +1986,20 @@ static void exch_bytes(const ExchPlan& pl, int P, int me, mrg_stats* st) {
 }
 
 static int exchange_rccl(mrg_ctx* c, const mrg_parts* local, int P, mrg_parts** owned);
+
+// What RCCL itself reports for this context's communicator (not what the
+// caller passed to mrg_comm_init), and the HIP device the context drives.
+static void comm_identity(mrg_ctx* c) {
+    int n = 0, r = -1, d = -1;
+    if (c->comm) {
+        if (ncclCommCount(c->comm, &n) != ncclSuccess) n = -1;
+        if (ncclCommUserRank(c->comm, &r) != ncclSuccess) r = -1;
+        if (ncclCommCuDevice(c->comm, &d) != ncclSuccess) d = -1;
+    }
+    c->stats.rccl_nranks = n;
+    c->stats.rccl_rank = r;
+    c->stats.device = c->comm && d >= 0 ? d : c->device;
+}
 
 int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     if (!c || !local || !owned) return MRG_EINVAL;
@@ -2012,9 +2047,14 @@ static int exchange_rccl(mrg_ctx* c, const mrg_parts* local, int P, mrg_parts** 
         return fail(c, MRG_ECOMM, "payload all-to-all: %s", ncclGetErrorString(e1 != ncclSuccess ? e1 : e2 != ncclSuccess ? e2 : e3));
     HCHK(c, hipEventRecord(c->ev[7], c->s));
     c->wd.set("unpack + aggregate");
-    rc = exch_finish(c, local, P, x, owned);
-    c->stats.exchange_ms = ev_ms(c->ev[6], c->ev[7]);
+    rc = exch_finish(c, local, P, x, owned, c->ev[12]);
+    // exchange_ms: counts + payload all-to-alls + the owner's unpack and exact
+    // re-aggregation; the first two alone are exchange_a2a_ms (the xGMI part)
+    c->stats.exchange_a2a_ms = ev_ms(c->ev[6], c->ev[7]);
+    c->stats.exchange_unpack_ms = ev_ms(c->ev[7], c->ev[12]);
+    c->stats.exchange_ms = ev_ms(c->ev[6], c->ev[12]);
     exch_bytes(pl, P, c->rank, &c->stats);
+    comm_identity(c);
     return rc;
 }
 
@@ -2088,8 +2128,13 @@ int mrg_exchange_group(mrg_ctx* const* ctxs, int P, const mrg_parts* const* loca
     }
     for (int j = 0; j < P; j++) {
         if ((rc = bind(ctxs[j]))) return undo(rc);
-        if ((rc = exch_finish(ctxs[j], local[j], P, xs[j], &owned[j]))) return undo(rc);
-        ctxs[j]->stats.exchange_ms = ev_ms(ctxs[j]->ev[6], ctxs[j]->ev[7]);
+        if ((rc = exch_finish(ctxs[j], local[j], P, xs[j], &owned[j], ctxs[j]->ev[12]))) return undo(rc);
+        ctxs[j]->stats.exchange_a2a_ms = ev_ms(ctxs[j]->ev[6], ctxs[j]->ev[7]);
+        ctxs[j]->stats.exchange_unpack_ms = ev_ms(ctxs[j]->ev[7], ctxs[j]->ev[12]);
+        ctxs[j]->stats.exchange_ms = ev_ms(ctxs[j]->ev[6], ctxs[j]->ev[12]);
+        ctxs[j]->stats.rccl_nranks = 0;  // peer copies, no communicator
+        ctxs[j]->stats.rccl_rank = -1;
+        ctxs[j]->stats.device = ctxs[j]->device;
         exch_bytes(xs[j].plan, P, j, &ctxs[j]->stats);
     }
     return MRG_OK;
@@ -2107,6 +2152,10 @@ int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, cons
         mrg_parts* o = nullptr;
         rc = mrg_exchange(c, p, &o);
         keep.exchange_ms = c->stats.exchange_ms;
+        keep.exchange_a2a_ms = c->stats.exchange_a2a_ms;
+        keep.exchange_unpack_ms = c->stats.exchange_unpack_ms;
+        keep.rccl_nranks = c->stats.rccl_nranks;
+        keep.rccl_rank = c->stats.rccl_rank;
         keep.shuffle_send_bytes = c->stats.shuffle_send_bytes;
         keep.shuffle_recv_bytes = c->stats.shuffle_recv_bytes;
         mrg_parts_free(p);

@@ -557,14 +557,18 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             uint64_t* lptr;
                             uint64_t lcap;
                             cold_list(t, lptr, lcap);
+                            // the descriptor starts at this range's next entry, so its 32-bit
+                            // offsets never limit the list's size (a base at the list start
+                            // dropped entries past 2^29 without a status bit: ADVICE r03); its
+                            // range check stops at the list's capacity (kStListFull is set
+                            // when a range is reserved past it, and the run is repeated)
+                            const uint64_t room = lbase < lcap ? lcap - lbase : 0;
                             const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
-                                (void*)lptr, (short)0, (int)(lcap * 8u < 0xFFFFFF00ull ? lcap * 8u : 0xFFFFFF00ull), 0x00020000);
+                                (void*)(lptr + lbase), (short)0, (int)(room < (0xFFFFFF00ull >> 3) ? room * 8u : 0xFFFFFF00ull),
+                                0x00020000);
                             const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
-                            const uint64_t at = lbase + lane;
-                            __builtin_amdgcn_raw_buffer_store_b64(
-                                (u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
-                                lane < nlong && at < lcap && at < (1ull << 29) ? (uint32_t)(at * 8u) : kOutOfRange,
-                                0, 0);
+                            __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
+                                                                  lane < nlong ? lane * 8u : kOutOfRange, 0, 0);
                             lbase += nlong;
                             lleft -= nlong;
                         } else {  // several passes (> 192 words): the list slot is still needed

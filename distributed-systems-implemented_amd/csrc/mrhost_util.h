@@ -6,6 +6,7 @@
 #pragma once
 #include <unistd.h>
 
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -42,18 +43,23 @@ inline bool read_file_opt(const std::string& path, std::vector<uint8_t>* out) {
     return true;
 }
 
-// All of a file, or false if it cannot be opened or read to the end (a reduce
-// input that another worker removed meanwhile: the caller abandons the task).
+// All of a file, or false if it does not exist (a reduce input that an accepted
+// duplicate of the task removed meanwhile: the caller abandons the task).  Any
+// other failure (EACCES, EMFILE, EIO, a read error) is fatal: abandoning the task
+// would make the coordinator re-issue it forever instead of failing the job.
 inline bool read_file_try(const std::string& path, std::vector<uint8_t>* out) {
     FILE* f = fopen(path.c_str(), "rb");
-    if (!f) return false;
+    if (!f) {
+        if (errno == ENOENT) return false;
+        fatalf("cannot open %s: %s", path.c_str(), strerror(errno));
+    }
     out->clear();
     uint8_t tmp[1 << 16];
     size_t n;
     while ((n = fread(tmp, 1, sizeof tmp, f)) > 0) out->insert(out->end(), tmp, tmp + n);
-    const bool ok = !ferror(f);
+    if (ferror(f)) fatalf("cannot read %s", path.c_str());  // an unlinked file stays readable: a real I/O error
     fclose(f);
-    return ok;
+    return true;
 }
 
 // Temp + rename, as worker.go:83,91 (ioutil.TempFile + os.Rename): the temp file

@@ -74,6 +74,11 @@ class Stats(ctypes.Structure):
         ("shuffle_recv_bytes", c_uint64),
         ("staged_bytes", c_uint64),
         ("spill_buckets", c_uint64),
+        ("exchange_a2a_ms", ctypes.c_double),
+        ("exchange_unpack_ms", ctypes.c_double),
+        ("rccl_nranks", ctypes.c_int64),
+        ("rccl_rank", ctypes.c_int64),
+        ("device", ctypes.c_int64),
     ]
 
     def as_dict(self):

@@ -28,8 +28,14 @@
  * output, as worker.go:126-148 always writes mr-out-r.
  *
  * Errors: every int-returning call returns MRG_OK (0) or a negative MRG_E* code
- * and leaves a message in mrg_last_error(ctx).  The library never aborts the
- * process (the Go shim maps a nonzero code to log.Fatalf as worker.go:60-64 does).
+ * and leaves a message in mrg_last_error(ctx) (the Go shim maps a nonzero code to
+ * log.Fatalf as worker.go:60-64 does).  The library never aborts the process, with
+ * ONE exception: a collective phase of mrg_comm_init / mrg_exchange that does not
+ * finish within the option exchange_timeout_ms (default 120 s; 4x for
+ * mrg_comm_init) — a peer rank died or hangs — makes the context's watchdog thread
+ * print the stuck phase and end the process with _exit(124), because a rank
+ * blocked inside RCCL cannot return an error code; a launcher then sees a failed
+ * rank instead of a hang.
  *
  * Threading: a context is bound to one device and is not re-entrant; every entry
  * point re-binds its device (cgo calls may migrate OS threads).  Several contexts
@@ -92,6 +98,13 @@ typedef struct {
     uint64_t staged_bytes;    /* map: bytes copied into the context's staging buffer first (host input,
                                  or a device pointer not 16-byte aligned) */
     uint64_t spill_buckets;   /* wc: hash buckets of the map's spill (256 by default; 2048 for high-cardinality splits; 512 by option) */
+    double exchange_a2a_ms;   /* exchange: the count and payload all-to-alls alone (exchange_ms also holds the
+                                 owner's unpack + exact re-aggregation) */
+    double exchange_unpack_ms;/* exchange: unpack of the received records + re-aggregation on the owner */
+    int64_t rccl_nranks;      /* exchange: ranks of the communicator as RCCL reports them (ncclCommCount);
+                                 0 for mrg_exchange_group (peer copies) or no exchange */
+    int64_t rccl_rank;        /* exchange: this context's rank per ncclCommUserRank (-1: none) */
+    int64_t device;           /* the HIP device this context drives (ncclCommCuDevice when attached) */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);
@@ -102,10 +115,13 @@ int mrg_device_count(int* n);
 /* Map one input split (one file = one map task).  app = MRG_APP_WC or MRG_APP_GREP
  * (pat/plen = the literal; ignored for wc).  Output: device-resident partial
  * aggregates (distinct key, count, partition) for all nreduce partitions.
- * grep: the pattern is a literal (regexp.QuoteMeta semantics).  dgrep.go:20-23
- * returns no lines when regexp.Compile fails, which for a literal happens
- * exactly when it is not valid UTF-8: such a pattern maps to no lines, as does
- * one holding '\n' (no line of strings.Split(contents, "\n") contains it). */
+ * grep: the pattern is matched as a literal.  dgrep.go:20 compiles it as a regexp,
+ * so a valid-UTF-8 pattern holding any of the metacharacters \ . + * ? ( ) | [ ] { } ^ $
+ * is refused with MRG_EINVAL unless option grep_literal = 1 asks for
+ * regexp.QuoteMeta semantics (the caller quoted it).  dgrep.go:20-23 returns no
+ * lines when regexp.Compile fails, which for a literal happens exactly when it
+ * is not valid UTF-8: such a pattern maps to no lines, as does one holding '\n'
+ * (no line of strings.Split(contents, "\n") contains it). */
 int mrg_map(mrg_ctx* ctx, int app, const void* buf, size_t len, int input_kind, const uint8_t* pat,
             size_t plen, uint32_t nreduce, mrg_parts** out);
 /* Combine `from` into `into` (both on ctx's device, same app and nreduce). */
@@ -198,6 +214,8 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        sort), tie_rank (0: grep's tied runs merge-sorted
  *                                        together instead of ranked per run)   reduce sort
  *                                        variants
+ *   grep_literal (1: on)                 grep patterns with regexp metacharacters matched as
+ *                                        literals (QuoteMeta) instead of refused with MRG_EINVAL
  *   out_direct (-1: off)                 mrg_run_job (wc) writes the output lines straight into
  *                                        its pinned host buffer (default) instead of a
  *                                        device buffer + copy */

@@ -174,3 +174,36 @@ def test_coordinator_forked_worker_crash_still_succeeds(tmp_path):
     assert info["done"] and info["workers_failed"] == 1 and info["reissued"] >= 1
     assert [(tmp_path / f"mr-out-{k}").read_bytes() for k in range(4)] == O.c_partitioned("wc", files, 4)
     assert not list(tmp_path.glob("mr-*.tmp-*"))  # unique temp files, all renamed
+
+
+@pytest.mark.gpu
+def test_worker_fails_on_unreadable_reduce_input(tmp_path):
+    """A reduce input that exists but cannot be read (here a directory: EISDIR
+    even for root) is a fatal worker error (log.Fatalf, worker.go:60-64), not a
+    task abandoned as 'removed by a duplicate' — abandoning it made the
+    coordinator re-issue the task forever.  Only a missing input
+    (ENOENT) abandons the task."""
+    files = cases.synthetic(C.KIND_ASCII, 5000, [200_000], 65)
+    paths = _write(tmp_path, files)
+    sock = str(tmp_path / "s")
+    coord = subprocess.Popen([COORD, "-n", "2", "-w", "0", "--sock", sock, "--task-timeout", "2", "wc"] + paths,
+                             cwd=tmp_path, stdout=subprocess.PIPE, stderr=subprocess.PIPE)
+    try:
+        for _ in range(300):
+            if os.path.exists(sock):
+                break
+            time.sleep(0.01)
+        wk = os.path.join(BUILD_DIR, "mrworker_gpu")
+        env = dict(os.environ, MRG_WORKER_CRASH_AFTER="1")
+        first = subprocess.run([wk, "--sock", sock, "wc"], cwd=tmp_path, env=env, capture_output=True, timeout=120)
+        assert first.returncode == 3  # did the map task, died holding a reduce task
+        inter = tmp_path / "mr-0-0"
+        assert inter.exists()
+        inter.unlink()
+        inter.mkdir()  # opens, but every read fails
+        bad = subprocess.run([wk, "--sock", sock, "wc"], cwd=tmp_path, capture_output=True, timeout=120)
+        assert bad.returncode != 0
+        assert b"cannot read" in bad.stderr and b"mr-0-0" in bad.stderr
+    finally:
+        coord.kill()
+        coord.communicate(timeout=30)

@@ -65,6 +65,28 @@ def test_grep_edge_cases(ctx, name):
     check(ctx, "grep:" + pat.decode("utf-8", "surrogateescape"), files, nreduces=(1, 10))
 
 
+@pytest.mark.parametrize("pat", [b"a.b", b"x+y", b"(q)", b"[z]", b"^s", b"e$", b"w*", b"u?", b"{2}", b"p|q", "ά\\d".encode()])
+def test_grep_regexp_metachars(ctx, pat):
+    """dgrep.go:20 compiles the pattern as a regexp and this path matches literals:
+    a valid-UTF-8 pattern holding a metacharacter is refused (MRG_EINVAL) instead
+    of silently matching differently; with option grep_literal = 1 (the caller
+    asked for regexp.QuoteMeta semantics) it is matched as a literal, exactly as
+    the oracle's literal grep.  Invalid UTF-8 keeps dgrep.go:20-23's no lines."""
+    from mrgpu.lib import MrgError
+    files = [b"a.b ab axb\nx+y xy\n(q) q\n[z] z\n^s s\ne$ e\nw* w\nu? u\n{2} 2\np|q pq\n" + "ά\\d ά5\n".encode()]
+    with pytest.raises(MrgError, match="metacharacter"):
+        ctx.map(MRG_APP_GREP, files[0], pattern=pat, nreduce=10)
+    ctx.set_option("grep_literal", 1)
+    try:
+        check(ctx, "grep:" + pat.decode(), files, nreduces=(1, 10))
+        got = gpu_partitioned(ctx, "grep:" + pat.decode(), files, 1)
+        assert got[0].count(b"\n") == 1  # exactly the line holding the literal
+    finally:
+        ctx.set_option("grep_literal", 0)
+    # invalid UTF-8 with a metacharacter: regexp.Compile fails -> no lines, no error
+    assert gpu_partitioned(ctx, "grep:" + (b"\xff" + pat).decode("utf-8", "surrogateescape"), files, 10) == [b""] * 10
+
+
 @pytest.mark.parametrize("kind,V,seed,inv", [(C.KIND_ASCII, 5000, 1, 0.0), (C.KIND_ASCII, 200000, 2, 0.0),
                                              (C.KIND_UTF8, 20000, 3, 0.0), (C.KIND_UTF8, 20000, 4, 0.001)])
 def test_wc_synthetic(wctx, kind, V, seed, inv):
