@@ -265,9 +265,6 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
 // Bytes reduce_format's output can take at most (its buffer, or a host buffer
 // given as hout: the lines are then written straight into pinned host memory).
 uint64_t reduce_out_bound(const Recs& r, int app);
-// Indices of occupied ShortTable slots; *d_count (device) = how many.
-int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64_t max_used, uint32_t** d_idx,
-                      uint32_t** d_count, hipStream_t s);
 // Radix sort of u64 keys (the low `bits` bits); result in k_out.
 int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s);
 // In-place stable sort of device keys (key_bytes 4 or 8, low `bits` bits) with

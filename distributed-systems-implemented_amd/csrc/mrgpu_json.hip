@@ -24,7 +24,7 @@
 
 #include <cstring>
 
-#include <rocprim/rocprim.hpp>
+#include "mrgpu_scan.h"
 
 namespace mrg {
 
@@ -174,19 +174,51 @@ __global__ void json_fill_kernel(const uint64_t* L, const uint64_t* loff, const 
     }
 }
 
+// Exclusive scan of n u64 values with the tiles chained by decoupled look-back
+// (mrgpu_scan.h); the look-back state lives in `scratch` (cleared per scan: the
+// JSON export is not a hot path).
+__global__ void __launch_bounds__(kScanThreads) scan_u64_kernel(const uint64_t* __restrict__ in,
+                                                                uint64_t* __restrict__ out, uint64_t n, ScanState st) {
+    __shared__ unsigned long long red[kScanThreads / 64];
+    __shared__ unsigned long long pre;
+    __shared__ uint32_t tile_w;
+    const uint32_t t = scan_take_tile(st, &tile_w);
+    const uint64_t i0 = (uint64_t)t * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+    uint64_t v[kScanPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; k++) {
+        v[k] = i0 + k < n ? in[i0 + k] : 0ull;
+        sum += v[k];
+    }
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan_u64(sum, red, &tot);
+    if (threadIdx.x < 64) {
+        const uint64_t p = scan_lookback(st, t, tot);
+        if (threadIdx.x == 0) pre = p;
+    }
+    __syncthreads();
+    uint64_t o = pre + ex;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; k++) {
+        if (i0 + k < n) out[i0 + k] = o;
+        o += v[k];
+    }
+}
+
 static int excl_scan(void*& tmp, size_t& tmp_bytes, const uint64_t* in, uint64_t* out, uint64_t n, hipStream_t s,
                      void* (*grow)(void* ctx, size_t), void* gctx) {
-    size_t tb = 0;
-    if (rocprim::exclusive_scan(nullptr, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s) != hipSuccess)
-        return -1;
-    if (tb > tmp_bytes) {
-        tmp = grow(gctx, tb);
+    const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+    const size_t need = ntiles * 8 + 64;
+    if (need > tmp_bytes) {
+        tmp = grow(gctx, need);
         if (!tmp) return -1;
-        tmp_bytes = tb;
+        tmp_bytes = need;
     }
-    return rocprim::exclusive_scan(tmp, tb, in, out, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s) == hipSuccess
-               ? 0
-               : -1;
+    if (hipMemsetAsync(tmp, 0, need, s) != hipSuccess) return -1;
+    ScanState st{(unsigned long long*)((char*)tmp + 64), (uint32_t*)tmp, 1u, (uint32_t)ntiles};
+    scan_u64_kernel<<<(unsigned)ntiles, kScanThreads, 0, s>>>(in, out, n, st);
+    return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 int json_lengths(const Recs& r, int app, uint64_t* L, uint64_t* T, uint64_t* P, uint64_t* loff, uint64_t* toff,

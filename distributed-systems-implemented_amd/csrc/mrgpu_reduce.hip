@@ -16,13 +16,11 @@
 #include <cstring>
 #include <rocprim/device/device_merge_sort.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/device/device_scan.hpp>
-#include <rocprim/device/device_select.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 
 #include <algorithm>
 
 #include "mrgpu_device.h"
+#include "mrgpu_scan.h"
 
 namespace mrg {
 
@@ -70,6 +68,7 @@ struct ReduceWs {
     // instead of one merge sort of every tied key
     bool tie_rank = true;
     RadixWs* rx = nullptr;
+    ScanWs scan;                   // look-back state of the hand-written scans (mrgpu_scan.h)
 };
 
 void reduce_ws_set(ReduceWs* w, int digit_bits, int fold_part, int grep_k1) {
@@ -99,6 +98,7 @@ void reduce_ws_free(ReduceWs* w) {
     for (DBuf* b : bs) b->release();
     if (w->h_pinned) hipHostFree(w->h_pinned);
     radix_ws_free(w->rx);
+    w->scan.release();
     delete w;
 }
 
@@ -287,6 +287,90 @@ __global__ void mark_ties_kernel(Recs r, const uint32_t* perm, uint64_t n, uint8
     }
 }
 
+// grep after the 16-byte passes: tie[i] = 1 when sorted position i has the
+// same (partition, first 16 key bytes) as i - 1 (mark_ties_kernel with k1), and
+// in the same pass the positions that start a group (tie[i] == 0) compacted in
+// order into bpos, their count in *nb: a thread takes 16 consecutive positions,
+// the tiles chain by decoupled look-back (mrgpu_scan.h).  One launch in place of
+// the tie marks + rocPRIM's select over a counting iterator.
+__global__ void __launch_bounds__(kScanThreads) mark_ties_bounds_kernel(Recs r, const uint32_t* __restrict__ perm,
+                                                                        uint64_t n, uint8_t* __restrict__ tie,
+                                                                        unsigned long long* flags, uint32_t* bpos,
+                                                                        uint32_t* nb, ScanState st) {
+    __shared__ unsigned long long red[kScanThreads / 64];
+    __shared__ unsigned long long pre;
+    __shared__ uint32_t tile_w;
+    const uint32_t t = scan_take_tile(st, &tile_w);
+    const uint64_t i0 = (uint64_t)t * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+    uint32_t prev = i0 > 0 && i0 <= n ? perm[i0 - 1] : 0u;
+    uint32_t tb = 0, bb = 0;  // tie / boundary bits of the 16 positions
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; k++) {
+        const uint64_t i = i0 + k;
+        if (i < n) {
+            const uint32_t cur = perm[i];
+            const bool tk = i > 0 && same_prefix(r, prev, cur, true, 0u);
+            tb |= (tk ? 1u : 0u) << k;
+            bb |= (tk ? 0u : 1u) << k;
+            prev = cur;
+        }
+    }
+    if (i0 + kScanPer <= n) {
+        uint32_t w[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            w[q] = ((tb >> (4 * q)) & 1u) | (((tb >> (4 * q + 1)) & 1u) << 8) | (((tb >> (4 * q + 2)) & 1u) << 16) |
+                   (((tb >> (4 * q + 3)) & 1u) << 24);
+        *(uint4*)(tie + i0) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+        for (uint32_t k = 0; i0 + k < n; k++) tie[i0 + k] = (uint8_t)((tb >> k) & 1u);
+    }
+    if (__ballot(tb != 0) && (threadIdx.x & 63) == 0 && flags[2] == 0) atomicOr(&flags[2], 1ull);
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan_u64((uint64_t)__popc(bb), red, &tot);
+    if (threadIdx.x < 64) {
+        const uint64_t p = scan_lookback(st, t, tot);
+        if (threadIdx.x == 0) pre = p;
+    }
+    __syncthreads();
+    uint64_t o = pre + ex;
+    for (uint32_t m = bb; m; m &= m - 1) bpos[o++] = (uint32_t)(i0 + __builtin_ctz(m));
+    if (i0 < n && i0 + kScanPer >= n) *nb = (uint32_t)o;  // the thread holding the last position: the count
+}
+
+// Positions i with f[i] != 0, compacted in order into pos, their count in
+// *count (the members of long tied runs for the merge sort): one look-back
+// launch in place of rocPRIM's select.
+__global__ void __launch_bounds__(kScanThreads) flag_positions_kernel(const uint8_t* __restrict__ f, uint64_t n,
+                                                                      uint32_t* pos, uint32_t* count, ScanState st) {
+    __shared__ unsigned long long red[kScanThreads / 64];
+    __shared__ unsigned long long pre;
+    __shared__ uint32_t tile_w;
+    const uint32_t t = scan_take_tile(st, &tile_w);
+    const uint64_t i0 = (uint64_t)t * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+    uint32_t bb = 0;
+    if (i0 + kScanPer <= n) {
+        const uint4 v = *(const uint4*)(f + i0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+#pragma unroll
+            for (int b = 0; b < 4; b++) bb |= (((w[q] >> (8 * b)) & 0xFFu) != 0 ? 1u : 0u) << (4 * q + b);
+    } else {
+        for (uint32_t k = 0; i0 + k < n; k++) bb |= (f[i0 + k] != 0 ? 1u : 0u) << k;
+    }
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan_u64((uint64_t)__popc(bb), red, &tot);
+    if (threadIdx.x < 64) {
+        const uint64_t p = scan_lookback(st, t, tot);
+        if (threadIdx.x == 0) pre = p;
+    }
+    __syncthreads();
+    uint64_t o = pre + ex;
+    for (uint32_t m = bb; m; m &= m - 1) pos[o++] = (uint32_t)(i0 + __builtin_ctz(m));
+    if (i0 < n && i0 + kScanPer >= n) *count = (uint32_t)o;
+}
+
 // Insertion sort of each tied run by full bytewise comparison.  A run longer
 // than max_run is left alone, its members marked in `lng` and flags[3] set: the
 // caller then sorts with the k1 pass (16-byte prefixes), or merge-sorts the
@@ -426,13 +510,58 @@ __device__ __forceinline__ void put_digits(OutPtr o, uint64_t v, uint32_t d) {
     }
 }
 
-__global__ void line_len_kernel(Recs r, const uint32_t* perm, uint64_t n, int app, uint64_t* ll) {
-    uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        uint32_t j = perm[i];
-        uint64_t len = r.len[j];
-        ll[i] = len + 2 + (app == 1 ? ndigits(r.cnt[j]) : len);
+// Line lengths and their exclusive scan in one pass (worker.go:144 /
+// mrsequential.go:81: "key value\n" per distinct key, in sorted order):
+// off[i] = byte offset of sorted line i, off[n] = the output's total bytes.  A
+// thread takes 16 consecutive lines; the tiles chain by decoupled look-back
+// (mrgpu_scan.h), so this is one launch with no scratch memsets (it replaced a
+// line-length kernel + rocPRIM's exclusive scan).
+template <int kApp>
+__global__ void __launch_bounds__(kScanThreads) line_offsets_kernel(Recs r, const uint32_t* __restrict__ perm, uint64_t n,
+                                                                    uint64_t* __restrict__ off, ScanState st) {
+    __shared__ unsigned long long red[kScanThreads / 64];
+    __shared__ unsigned long long pre;
+    __shared__ uint32_t tile_w;
+    const uint32_t t = scan_take_tile(st, &tile_w);
+    const uint64_t i0 = (uint64_t)t * kScanTile + (uint64_t)threadIdx.x * kScanPer;
+    uint32_t j[kScanPer];
+    if (i0 + kScanPer <= n) {
+        const uint4* p4 = (const uint4*)(perm + i0);
+#pragma unroll
+        for (uint32_t q = 0; q < kScanPer / 4; q++) {
+            const uint4 v = p4[q];
+            j[4 * q] = v.x; j[4 * q + 1] = v.y; j[4 * q + 2] = v.z; j[4 * q + 3] = v.w;
+        }
+    } else {
+#pragma unroll
+        for (uint32_t k = 0; k < kScanPer; k++) j[k] = i0 + k < n ? perm[i0 + k] : 0u;
     }
+    uint64_t l[kScanPer];
+    uint64_t sum = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; k++) {
+        uint64_t v = 0;
+        if (i0 + k < n) {
+            const uint64_t len = r.len[j[k]];
+            v = kApp == 1 ? len + 2 + ndigits(r.cnt[j[k]]) : 2 * len + 2;
+        }
+        l[k] = v;
+        sum += v;
+    }
+    uint64_t tot;
+    const uint64_t ex = block_excl_scan_u64(sum, red, &tot);
+    if (threadIdx.x < 64) {
+        const uint64_t p = scan_lookback(st, t, tot);
+        if (threadIdx.x == 0) pre = p;
+    }
+    __syncthreads();
+    uint64_t o = pre + ex;
+#pragma unroll
+    for (uint32_t k = 0; k < kScanPer; k++) {
+        if (i0 + k < n) off[i0 + k] = o;
+        o += l[k];
+    }
+    if (i0 < n && i0 + kScanPer >= n) off[n] = o;  // the thread holding the last line: the total
 }
 
 // Output lines ("key count\n" for wc, "line line\n" for grep): a block's 256
@@ -443,14 +572,13 @@ __global__ void line_len_kernel(Recs r, const uint32_t* perm, uint64_t n, int ap
 constexpr uint32_t kWlLines = 256;
 template <int kApp>
 __global__ void __launch_bounds__(kWlLines) write_lines_staged_kernel(Recs r, const uint32_t* perm, uint64_t n,
-                                                                        const uint64_t* off, const uint64_t* ll,
-                                                                        uint8_t* out) {
+                                                                        const uint64_t* off, uint8_t* out) {
     constexpr uint32_t kWlBytes = kApp == 1 ? 16384 : 49152;  // C2 lines ~14 B, C3 lines ~120 B
     __shared__ __attribute__((aligned(16))) uint8_t buf[kWlBytes];
     const uint32_t tid = threadIdx.x;
     for (uint64_t i0 = (uint64_t)blockIdx.x * kWlLines; i0 < n; i0 += (uint64_t)gridDim.x * kWlLines) {
         const uint64_t iend = i0 + kWlLines < n ? i0 + kWlLines : n;
-        const uint64_t start = off[i0], end = iend < n ? off[iend] : off[n - 1] + ll[n - 1];
+        const uint64_t start = off[i0], end = off[iend];  // off[n] = the total
         const uint64_t a0 = start & ~15ull;
         const bool staged = end - a0 <= kWlBytes;  // block-uniform
         const uint64_t i = i0 + tid;
@@ -516,11 +644,11 @@ __global__ void __launch_bounds__(kWlLines) write_lines_staged_kernel(Recs r, co
 // offsets[p] = byte offset of the first line of partition p (lower bound on sorted part).
 // offsets[nparts] = the output's total bytes (last line's offset + length);
 // with one_part the output is one partition: offsets = {0, total}.
-__global__ void part_offsets_kernel(Recs r, const uint32_t* perm, uint64_t n, const uint64_t* off, const uint64_t* ll,
-                                    uint32_t nparts, bool one_part, uint64_t* offsets) {
+__global__ void part_offsets_kernel(Recs r, const uint32_t* perm, uint64_t n, const uint64_t* off, uint32_t nparts,
+                                    bool one_part, uint64_t* offsets) {
     uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p > nparts) return;
-    const uint64_t total = off[n - 1] + ll[n - 1];
+    const uint64_t total = off[n];
     if (p == nparts) { offsets[p] = total; return; }
     if (one_part) { offsets[p] = 0; return; }
     uint64_t lo = 0, hi = n;
@@ -809,27 +937,6 @@ static int sort_pass(ReduceWs* ws, K* keys_in, K* keys_out, uint32_t* v_in, uint
     return 0;
 }
 
-// Indices of the occupied ShortTable slots (rocprim select over a counting
-// iterator): a dense compaction with no same-address atomics.
-struct ShortUsed {
-    const ShortSlot* sh;
-    __host__ __device__ bool operator()(const uint32_t& i) const { return sh[i].k0 != 0; }
-};
-
-int select_used_short(ReduceWs* ws, const ShortSlot* sh, uint64_t nslots, uint64_t max_used, uint32_t** d_idx,
-                      uint32_t** d_count, hipStream_t s) {
-    RCHK(ws->sel.ensure((max_used + 1024) * 4));
-    RCHK(ws->offs.ensure(64));
-    *d_idx = ws->sel.as<uint32_t>();
-    *d_count = ws->offs.as<uint32_t>();
-    rocprim::counting_iterator<uint32_t> first(0);
-    size_t tb = 0;
-    RCHK(rocprim::select(nullptr, tb, first, *d_idx, *d_count, (size_t)nslots, ShortUsed{sh}, s));
-    RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::select(ws->tmp.p, tb, first, *d_idx, *d_count, (size_t)nslots, ShortUsed{sh}, s));
-    return 0;
-}
-
 int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s) {
     if (ws->own_sort) return radix_sort_keys_u64(ws->rx, k_in, k_out, n, bits, s);
     size_t tb = 0;
@@ -874,11 +981,6 @@ int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in
     return sort_pass<uint32_t>(ws, k_in, k_out, v_in, v_out, n, bits, s);
 }
 
-struct MarkedPos {
-    const uint8_t* lng;
-    __host__ __device__ bool operator()(const uint32_t& i) const { return lng[i] != 0; }
-};
-
 // The members of long tied runs (lng[i] != 0): compacted in order, merge-sorted
 // by full (partition, key) comparison, written back to the same positions.  The
 // runs are contiguous and already in (partition, prefix) order, which the full
@@ -890,11 +992,13 @@ static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
     RCHK(ws->offs.ensure(64));
     uint32_t* pos = ws->sel.as<uint32_t>();
     uint32_t* d_m = ws->offs.as<uint32_t>();
-    rocprim::counting_iterator<uint32_t> first(0);
+    {
+        const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+        ScanState st;
+        RCHK(ws->scan.prepare(ntiles, s, &st));
+        flag_positions_kernel<<<(unsigned)ntiles, kScanThreads, 0, s>>>(lng, n, pos, d_m, st);
+    }
     size_t tb = 0;
-    RCHK(rocprim::select(nullptr, tb, first, pos, d_m, (size_t)n, MarkedPos{lng}, s));
-    RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::select(ws->tmp.p, tb, first, pos, d_m, (size_t)n, MarkedPos{lng}, s));
     RCHK(hipMemcpyAsync(ws->h_pinned + 8, d_m, 4, hipMemcpyDeviceToHost, s));
     RCHK(hipStreamSynchronize(s));
     const uint32_t m = (uint32_t)(ws->h_pinned[8] & 0xFFFFFFFFu);
@@ -954,11 +1058,6 @@ __device__ __forceinline__ int tied_cmp(const Recs& r, const uint64_t* ea, uint3
     }
     return (la > lb) - (la < lb);
 }
-
-struct IsBoundary {  // sorted position i starts a new (partition, prefix) group
-    const uint8_t* tie;
-    __host__ __device__ bool operator()(const uint32_t& i) const { return tie[i] == 0; }
-};
 
 // One wave per 64 consecutive group boundaries (bpos: sorted positions that
 // start a (partition, prefix) group; cnt[0]'s low half = how many): the wave
@@ -1083,10 +1182,10 @@ __global__ void __launch_bounds__(1024) rank_mid_runs_kernel(Recs r, const uint6
     }
 }
 
-// Orders grep's tied runs after the 16-byte sort (perm = its result, tie = the
-// tie marks).  Runs over kMidRun keys are marked in lng and flags[3] is set: the
+// Orders grep's tied runs after the 16-byte sort (perm = its result; the tie
+// marks are written to `tie` by the boundary pass here).  Runs over kMidRun keys are marked in lng and flags[3] is set: the
 // caller reads the flag and merge-sorts them (sort_long_runs).
-static int rank_tied_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t n, const uint8_t* tie, uint8_t* lng,
+static int rank_tied_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t n, uint8_t* tie, uint8_t* lng,
                           const uint64_t* ext, unsigned long long* flags, hipStream_t s) {
     RCHK(ws->runs.ensure(64 + (n / kSmallRun + 2) * 8));
     unsigned long long* cnt = ws->runs.as<unsigned long long>();
@@ -1094,11 +1193,12 @@ static int rank_tied_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
     uint32_t* d_nb = (uint32_t*)cnt;  // cnt[0]'s low half
     uint32_t* bpos = ws->key_b.as<uint32_t>();
     RCHK(hipMemsetAsync(cnt, 0, 64, s));
-    rocprim::counting_iterator<uint32_t> first(0);
-    size_t tb = 0;
-    RCHK(rocprim::select(nullptr, tb, first, bpos, d_nb, (size_t)n, IsBoundary{tie}, s));
-    RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::select(ws->tmp.p, tb, first, bpos, d_nb, (size_t)n, IsBoundary{tie}, s));
+    {  // tie marks + the group boundaries, one look-back launch
+        const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+        ScanState st;
+        RCHK(ws->scan.prepare(ntiles, s, &st));
+        mark_ties_bounds_kernel<<<(unsigned)ntiles, kScanThreads, 0, s>>>(r, perm, n, tie, flags, bpos, d_nb, st);
+    }
     static const bool dbg = getenv("MRG_DEBUG_TIES") != nullptr;
     hipEvent_t ev[3];
     if (dbg) {
@@ -1300,7 +1400,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         uint8_t* tie = ws->key_a.as<uint8_t>();
         RCHK(hipMemsetAsync(tie + n, 0, n, s));
         RCHK(hipMemsetAsync(flags + 2, 0, 16, s));
-        mark_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, flags, true, 0u);
+        // (the tie marks are made by rank_tied_runs' boundary pass)
         if ((e = rank_tied_runs(ws, r, pa, n, tie, tie + n, ext, flags, s))) return e;
     } else if (grep) {  // every tied run (equal first 16, or with !grep_k1 first 8 - pbits / 8, bytes) merge-sorted
         bool any_long = false;
@@ -1309,18 +1409,16 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     uint8_t* out = to_host ? hout : ws->out.as<uint8_t>();
     // line lengths, their scan, the lines, the partition offsets (copied to the host)
     auto emit_output = [&]() -> int {
-        uint64_t* ll = ws->key_b.as<uint64_t>();
-        uint64_t* off = ws->lineoff.as<uint64_t>();
-        line_len_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, app, ll);
-        size_t tb = 0;
-        RCHK(rocprim::exclusive_scan(nullptr, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
-        RCHK(ws->tmp.ensure(tb));
-        RCHK(rocprim::exclusive_scan(ws->tmp.p, tb, ll, off, (uint64_t)0, (size_t)n, rocprim::plus<uint64_t>(), s));
+        uint64_t* off = ws->lineoff.as<uint64_t>();  // n + 1 offsets
+        const uint64_t ntiles = (n + kScanTile - 1) / kScanTile;
+        ScanState st;
+        RCHK(ws->scan.prepare(ntiles, s, &st));
+        if (app != 1) line_offsets_kernel<2><<<(unsigned)ntiles, kScanThreads, 0, s>>>(r, pa, n, off, st);
+        else line_offsets_kernel<1><<<(unsigned)ntiles, kScanThreads, 0, s>>>(r, pa, n, off, st);
         const unsigned wl_grid = (unsigned)std::min<uint64_t>((n + kWlLines - 1) / kWlLines, 8192);
-        if (app != 1) write_lines_staged_kernel<2><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
-        else write_lines_staged_kernel<1><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, ll, out);
-        part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, ll, nparts, !all,
-                                                                     ws->offs.as<uint64_t>());
+        if (app != 1) write_lines_staged_kernel<2><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, out);
+        else write_lines_staged_kernel<1><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, out);
+        part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, nparts, !all, ws->offs.as<uint64_t>());
         RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
         return 0;
     };

@@ -27,12 +27,12 @@ def main():
     ap.add_argument("--grids", default="0")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--opt", action="append", default=[], help="context option name=value (repeatable)")
-    ap.add_argument("--workload", default="c2", choices=["c2", "c5"])
+    ap.add_argument("--workload", default="c2", choices=["c2", "c2u", "c5"])
     a = ap.parse_args()
     nfiles = max(1, int(a.gb * 4))
-    if a.workload == "c5":
+    if a.workload in ("c5", "c2u"):
         import bench
-        buf = bench.gen_corpus(bench.WORKLOADS["c5"], 0, 250, nfiles)
+        buf = bench.gen_corpus(bench.WORKLOADS[a.workload], 0, 250, nfiles)
     else:
         voc = C.Vocab(C.KIND_ASCII, 1.07, 10**6, 2)
         sizes = [250_000_000] * nfiles

@@ -74,6 +74,57 @@ __global__ void __launch_bounds__(1024) spill(unsigned long long* out, unsigned 
     }
 }
 
+// 4 wgsync: per-workgroup streams staged in LDS, 32 bytes (4 records) per
+//   stream, with a workgroup barrier every `per` records per thread: between
+//   barriers a record takes a slot by an LDS cursor and lands in the stream's
+//   staging group if the group has room, else goes straight to memory; after
+//   the barrier every complete group leaves as one 32-byte write.
+template <int NS>
+__global__ void __launch_bounds__(1024) spill_wgsync(unsigned long long* out, unsigned cap, unsigned iters,
+                                                     const uint4* in, unsigned long long in_per_wg, int read_input,
+                                                     unsigned per) {
+    __shared__ unsigned curs[NS], fl[NS];
+    __shared__ unsigned long long stage[NS][4];
+    for (unsigned i = threadIdx.x; i < NS; i += 1024) curs[i] = fl[i] = 0;
+    __syncthreads();
+    unsigned long long* base = out + (unsigned long long)blockIdx.x * NS * cap;
+    const uint4* ip = in + (unsigned long long)blockIdx.x * in_per_wg;
+    unsigned acc = 0;
+    for (unsigned it0 = 0; it0 < iters; it0 += per) {
+        for (unsigned it = it0; it < it0 + per && it < iters; it++) {
+            if (read_input) {
+                const unsigned long long k = ((unsigned long long)it * 1024 + threadIdx.x) % in_per_wg;
+                const u4v v = __builtin_nontemporal_load((const u4v*)(ip + k));
+                acc += v.x ^ v.w;
+            }
+            const unsigned s = mix(blockIdx.x * 0x9E3779B9u + it * 1024 + threadIdx.x) & (NS - 1);
+            const unsigned pos = atomicAdd(&curs[s], 1u);
+            const unsigned long long rec = 0x0101010101010101ull * (it + 1) + acc;
+            const unsigned f = fl[s];
+            if (pos < f + 4) stage[s][pos - f] = rec;
+            else if (pos < cap) base[(unsigned long long)s * cap + pos] = rec;
+        }
+        __syncthreads();
+        for (unsigned s = threadIdx.x; s < NS; s += 1024) {
+            const unsigned c = curs[s], f = fl[s];
+            if (c >= f + 4) {
+                if (f + 4 <= cap) {
+                    uint4* dst = (uint4*)(base + (unsigned long long)s * cap + f);
+                    const uint4* src = (const uint4*)&stage[s][0];
+                    dst[0] = src[0];
+                    dst[1] = src[1];
+                }
+                fl[s] = c;  // direct writes past the group: the next group starts at c
+            }
+        }
+        __syncthreads();
+    }
+    for (unsigned s = threadIdx.x; s < NS; s += 1024) {
+        const unsigned c = curs[s], f = fl[s];
+        for (unsigned q = f; q < c && q < cap; q++) base[(unsigned long long)s * cap + q] = stage[s][q - f];
+    }
+}
+
 template <int NS, int V>
 double run(unsigned long long* out, unsigned cap, unsigned* gcur, unsigned iters, const uint4* in,
            unsigned long long in_per_wg, int read_input, int nwg, unsigned* xcc_seen, int nown) {
@@ -84,7 +135,8 @@ double run(unsigned long long* out, unsigned cap, unsigned* gcur, unsigned iters
     for (int r = 0; r < 3; r++) {
         CHK(hipMemset(gcur, 0, (size_t)nown * NS * 4));
         CHK(hipEventRecord(a));
-        spill<NS, V><<<nwg, 1024>>>(out, cap, gcur, iters, in, in_per_wg, read_input, xcc_seen);
+        if constexpr (V >= 100) spill_wgsync<NS><<<nwg, 1024>>>(out, cap, iters, in, in_per_wg, read_input, V - 100);
+        else spill<NS, V><<<nwg, 1024>>>(out, cap, gcur, iters, in, in_per_wg, read_input, xcc_seen);
         CHK(hipEventRecord(b));
         CHK(hipEventSynchronize(b));
         float ms;
@@ -125,6 +177,19 @@ int main(int argc, char** argv) {
         printf("{\"variant\": \"xcd_wg\", \"input\": %d, \"ms\": %.3f, \"rec_GBps\": %.1f}\n", read_input, ms, recs * 8 / ms / 1e6);
         ms = run<NS, 3>(out, cap_x, gcur, iters, in, in_per_wg, read_input, nwg, xs, 8);
         printf("{\"variant\": \"grp\", \"input\": %d, \"ms\": %.3f, \"rec_GBps\": %.1f}\n", read_input, ms, recs * 8 / ms / 1e6);
+    }
+    // LDS staging with workgroup barriers (2048 streams: what fits in LDS), vs direct
+    for (int read_input = 0; read_input < 2; read_input++) {
+        constexpr int NS2 = 2048;
+        const unsigned cap2 = (unsigned)(2ull * 1024 * iters / NS2 + 64);
+        double ms = run<NS2, 0>(out, cap2, gcur, iters, in, in_per_wg, read_input, nwg, xs, nwg);
+        printf("{\"variant\": \"wg2048\", \"input\": %d, \"ms\": %.3f, \"rec_GBps\": %.1f}\n", read_input, ms, recs * 8 / ms / 1e6);
+        ms = run<NS2, 101>(out, cap2, gcur, iters, in, in_per_wg, read_input, nwg, xs, nwg);
+        printf("{\"variant\": \"wgsync2048_per1\", \"input\": %d, \"ms\": %.3f, \"rec_GBps\": %.1f}\n", read_input, ms, recs * 8 / ms / 1e6);
+        ms = run<NS2, 102>(out, cap2, gcur, iters, in, in_per_wg, read_input, nwg, xs, nwg);
+        printf("{\"variant\": \"wgsync2048_per2\", \"input\": %d, \"ms\": %.3f, \"rec_GBps\": %.1f}\n", read_input, ms, recs * 8 / ms / 1e6);
+        ms = run<NS2, 104>(out, cap2, gcur, iters, in, in_per_wg, read_input, nwg, xs, nwg);
+        printf("{\"variant\": \"wgsync2048_per4\", \"input\": %d, \"ms\": %.3f, \"rec_GBps\": %.1f}\n", read_input, ms, recs * 8 / ms / 1e6);
     }
     // check: the per-XCD cursors of the last run sum to the records (nothing lost)
     unsigned h[nwg];
