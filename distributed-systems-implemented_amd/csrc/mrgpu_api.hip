@@ -213,6 +213,7 @@ struct mrg_ctx {
     std::string err;
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
+    uint32_t* d_b2 = nullptr;  // letters among code points < U+0800 (2048 bits)
     DevBuf sh, lo, list, ctr, staging, pat, spool, spmeta;
     DevBuf shl;  // the ShortTable's claim list
     DevBuf spool_alt;     // diagnostic option spill_alt_pools: a second spill pool, the two alternate per split
@@ -222,6 +223,9 @@ struct mrg_ctx {
     bool seg_sync = true;               // size the miss segments from this split's totals (host read)
     bool out_direct = true;             // mrg_run_job: output lines written straight into pinned host memory
     bool grep_literal = false;          // grep: regexp metacharacters taken literally (QuoteMeta) instead of refused
+    DevBuf lrec, lrec_cnt;              // wc: 32-byte long-word records [map workgroup][lrec_cap], their counts
+    uint32_t lrec_cap = 4096;           // records per map workgroup region (grows on kStLrecFull)
+    bool lrec_on = true;                // option long_records (-1: every long word through the offset list)
     uint64_t arena_hint = 0;            // wc: long-key bytes expected in a split (the previous one's + 25 %)
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     DevBuf ghits, glines, gdefer;        // grep: sorted hits, resolved (start, end) lines, deferred hits
@@ -294,6 +298,19 @@ struct mrg_ctx {
     uint64_t* h_scr = nullptr;     // pinned scratch for small device -> host reads (8 words)
     uint8_t* h_out = nullptr;      // pinned result buffer for mrg_run_job
     size_t h_out_cap = 0;
+    // mrg_run_job_async: up to two jobs whose output bytes are still crossing PCIe
+    // (on the output stream os, into their own pinned buffers) while the caller
+    // queues the next job; aj[aj_head] is the oldest
+    struct AsyncJob {
+        uint8_t* host = nullptr;
+        size_t cap = 0;
+        uint64_t n = 0;
+        std::vector<uint64_t> offsets;
+        hipEvent_t start = nullptr, done = nullptr;
+        mrg_stats stats{};
+    } aj[2];
+    int aj_head = 0, aj_count = 0;
+    hipStream_t os = nullptr;
     ncclComm_t comm = nullptr;
     int nranks = 1, rank = 0;
     // collective deadline (option exchange_timeout_ms; comm init gets 4x)
@@ -381,6 +398,9 @@ static Tables make_tables(mrg_ctx* c) {
     t.dict = nullptr;
     t.dict_cnt = (uint32_t*)c->dict_cnt.p;
     t.dbg = c->debug_times && c->dbg.ensure(2 * (kSpillBucketsHi + kMaxMapWGs) * 8) == hipSuccess ? (unsigned long long*)c->dbg.p : nullptr;
+    t.lrec = nullptr;  // set by wc_map for the split's map (sample maps and grep use the offset list)
+    t.lrec_cnt = nullptr;
+    t.lrec_cap = 0;
     return t;
 }
 
@@ -887,6 +907,13 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         t.nreduce = nreduce;
         t.out = rec_view(c);
         t.out_cap = c->rec_cap;
+        if (c->lrec_on) {
+            HCHK(c, c->lrec.ensure_grow((size_t)nwg * c->lrec_cap * 32));
+            HCHK(c, c->lrec_cnt.ensure((size_t)kMaxMapWGs * 4));
+            t.lrec = (uint4*)c->lrec.p;
+            t.lrec_cnt = (uint32_t*)c->lrec_cnt.p;
+            t.lrec_cap = c->lrec_cap;
+        }
         clear_for_run(c, t);
         HCHK(c, hipEventRecord(c->ev[0], c->s));
         if (ing.npieces && attempt == 0) {  // the first pass runs while the host input streams in
@@ -910,6 +937,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         // read of the counters afterwards checks every capacity (an overflow grows
         // what filled up and repeats the attempt).
         launch_wc_long(in, len, t, lt, ~0ull, c->s);
+        launch_wc_lrec(t, nwg, c->s);
         HCHK(c, hipGetLastError());
         HCHK(c, hipEventRecord(c->ev[2], c->s));
         // the arena (long keys' bytes) sized from the previous split's long keys
@@ -932,7 +960,15 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             h = *c->h_ctr;
         }
         c->arena_hint = h.long_bytes + h.long_bytes / 4;
-        if (grow_on_overflow(c, h.status & (kStListFull | kStShortFull | kStLongFull | kStRecFull | kStSegFull)))
+        if (h.status & kStLrecFull) {  // a record region filled up: size them for this split's busiest workgroup
+            std::vector<uint32_t> cnt(nwg);
+            HCHK(c, hipMemcpy(cnt.data(), c->lrec_cnt.p, (size_t)nwg * 4, hipMemcpyDeviceToHost));
+            const uint32_t mx = *std::max_element(cnt.begin(), cnt.end());
+            c->lrec_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((uint64_t)mx + mx / 4 + 1024, 2ull * c->lrec_cap),
+                                                       1u << 26);
+        }
+        if (grow_on_overflow(c, h.status & (kStListFull | kStShortFull | kStLongFull | kStRecFull | kStSegFull)) ||
+            (h.status & kStLrecFull))
             continue;
         {
             // Bucket count for the next split (a worker's map tasks are alike):
@@ -1133,6 +1169,17 @@ int mrg_open(int device, mrg_ctx** out) {
     }
     hipMemcpy(c->d_l1, mrg_letter_l1_init, sizeof(mrg_letter_l1_init), hipMemcpyHostToDevice);
     hipMemcpy(c->d_l2, mrg_letter_l2_init, sizeof(mrg_letter_l2_init), hipMemcpyHostToDevice);
+    {  // the 2-byte runes' letters as one 2048-bit table (the map kernels' one-read lookup)
+        uint32_t b2[64] = {};
+        for (uint32_t cp = 0; cp < 2048; cp++)
+            if ((mrg_letter_l2_init[mrg_letter_l1_init[cp >> 8] * 8u + ((cp >> 5) & 7u)] >> (cp & 31u)) & 1u)
+                b2[cp >> 5] |= 1u << (cp & 31u);
+        if (hipMalloc((void**)&c->d_b2, sizeof(b2)) != hipSuccess) {
+            mrg_close(c);
+            return MRG_ENOMEM;
+        }
+        hipMemcpy(c->d_b2, b2, sizeof(b2), hipMemcpyHostToDevice);
+    }
     if (hipHostMalloc((void**)&c->h_ctr, sizeof(Counters), hipHostMallocDefault) != hipSuccess ||
         hipHostMalloc((void**)&c->h_scr, 8 * sizeof(uint64_t), hipHostMallocDefault) != hipSuccess) {
         mrg_close(c);
@@ -1151,13 +1198,21 @@ void mrg_close(mrg_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     DevBuf* bs[] = {&c->sh, &c->shl, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spool_alt, &c->spmeta,
                     &c->bflag, &c->dict, &c->dict_cnt, &c->sample, &c->recbuf, &c->recarena, &c->sortbuf,
-                    &c->segmeta, &c->seg8[0], &c->seg8[1], &c->seg16[0], &c->seg16[1]};
+                    &c->segmeta, &c->seg8[0], &c->seg8[1], &c->seg16[0], &c->seg16[1], &c->lrec, &c->lrec_cnt};
     for (DevBuf* b : bs) b->release();
     if (c->d_l1) hipFree(c->d_l1);
     if (c->d_l2) hipFree(c->d_l2);
+    if (c->d_b2) hipFree(c->d_b2);
     if (c->h_ctr) hipHostFree(c->h_ctr);
     if (c->h_scr) hipHostFree(c->h_scr);
     if (c->h_out) hipHostFree(c->h_out);
+    for (auto& j : c->aj) {
+        if (j.done) hipEventSynchronize(j.done);
+        if (j.host) hipHostFree(j.host);
+        if (j.start) hipEventDestroy(j.start);
+        if (j.done) hipEventDestroy(j.done);
+    }
+    if (c->os) hipStreamDestroy(c->os);
     if (c->h_sample) hipHostFree(c->h_sample);
     for (hipEvent_t e : c->piece_ev) hipEventDestroy(e);
     if (c->cs) hipStreamDestroy(c->cs);
@@ -1200,6 +1255,10 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set_compact_ties(c->rws, v >= 0);
     } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default) or via a copy (-1)
         c->out_direct = v >= 0;
+    } else if (!strcmp(name, "long_records")) {  // wc: words of 17-32 bytes as key records (default) or offsets (-1)
+        c->lrec_on = v >= 0;
+    } else if (!strcmp(name, "lrec_cap")) {  // records per map workgroup region (tests of the overflow path)
+        c->lrec_cap = v > 0 ? (uint32_t)std::min<int64_t>(v, 1 << 26) : 4096u;
     } else if (!strcmp(name, "grep_literal")) {  // grep: metacharacters quoted (1) instead of refused (0)
         c->grep_literal = v > 0;
     } else if (!strcmp(name, "tie_rank")) {  // grep reduce: tied runs ranked per run (1, default) or merge-sorted (0)
@@ -1330,7 +1389,7 @@ int mrg_map(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const ui
         in = (const uint8_t*)c->staging.p;
         c->stats.staged_bytes = len;
     }
-    LetterTables lt{c->d_l1, c->d_l2};
+    LetterTables lt{c->d_l1, c->d_l2, c->d_b2};
     if (app == MRG_APP_WC) return wc_map(c, in, len, nreduce, lt, out, host);
     return grep_map(c, in, len, pat, plen, nreduce, out, host);
 }
@@ -1716,10 +1775,17 @@ int mrg_parts_import(mrg_ctx* c, const void* bytes, size_t nb, mrg_parts** out) 
     return MRG_OK;
 }
 
+// The output transfers of queued async jobs read the reduce's device buffer:
+// they finish before another reduce may write (or reallocate) it.
+static int drain_async(mrg_ctx* c) {
+    for (int k = 0; k < c->aj_count; k++) HCHK(c, hipEventSynchronize(c->aj[(c->aj_head + k) & 1].done));
+    return MRG_OK;
+}
+
 static int reduce_common(mrg_ctx* c, const mrg_parts* p, uint32_t only, uint8_t** d_out, uint64_t* n_out, uint64_t* offsets,
                          uint8_t* hout = nullptr, uint64_t hout_cap = 0) {
     int rc;
-    if ((rc = bind(c))) return rc;
+    if ((rc = bind(c)) || (rc = drain_async(c))) return rc;
     HCHK(c, hipEventRecord(c->ev[4], c->s));
     if (only == 0xFFFFFFFFu) {
         rc = reduce_format(c->rws, p->r, p->app, p->nreduce, only, d_out, n_out, offsets, c->s, p->ascii, hout, hout_cap);
@@ -2143,6 +2209,8 @@ int mrg_exchange_group(mrg_ctx* const* ctxs, int P, const mrg_parts* const* loca
 int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const uint8_t* pat, size_t plen,
                 uint32_t nreduce, void** bytes, size_t* nb, uint64_t* offsets) {
     if (!c || !bytes || !nb || !offsets) return MRG_EINVAL;
+    int drc;
+    if ((drc = bind(c)) || (drc = drain_async(c))) return drc;  // (its pinned output buffer is separate)
     mrg_parts* p = nullptr;
     int rc = mrg_map(c, app, buf, len, kind, pat, plen, nreduce, &p);
     if (rc) return rc;
@@ -2211,6 +2279,88 @@ int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, cons
     mrg_parts_free(use);
     *bytes = c->h_out;  // context-owned; valid until the next call on this context (do not mrg_free)
     *nb = n;
+    return MRG_OK;
+}
+
+int mrg_run_job_async(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const uint8_t* pat, size_t plen,
+                      uint32_t nreduce) {
+    if (!c) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    if (c->aj_count >= 2) return fail(c, MRG_EINVAL, "run_job_async: two jobs in flight; mrg_job_wait first");
+    if (!c->os) HCHK(c, hipStreamCreateWithFlags(&c->os, hipStreamNonBlocking));
+    mrg_ctx::AsyncJob& J = c->aj[(c->aj_head + c->aj_count) & 1];
+    if (!J.done) {
+        HCHK(c, hipEventCreate(&J.start));
+        HCHK(c, hipEventCreate(&J.done));
+    }
+    // map (+ exchange) on the context stream: it overlaps the previous job's
+    // output transfer on the output stream
+    mrg_parts* p = nullptr;
+    if ((rc = mrg_map(c, app, buf, len, kind, pat, plen, nreduce, &p))) return rc;
+    mrg_stats keep = c->stats;
+    mrg_parts* use = p;
+    if (c->comm && c->nranks > 1 && !c->skip_exchange) {
+        mrg_parts* o = nullptr;
+        rc = mrg_exchange(c, p, &o);
+        keep.exchange_ms = c->stats.exchange_ms;
+        keep.exchange_a2a_ms = c->stats.exchange_a2a_ms;
+        keep.exchange_unpack_ms = c->stats.exchange_unpack_ms;
+        keep.rccl_nranks = c->stats.rccl_nranks;
+        keep.rccl_rank = c->stats.rccl_rank;
+        keep.shuffle_send_bytes = c->stats.shuffle_send_bytes;
+        keep.shuffle_recv_bytes = c->stats.shuffle_recv_bytes;
+        mrg_parts_free(p);
+        if (rc) return rc;
+        use = o;
+    }
+    // (reduce_common first waits for the previous job's transfer: it writes the
+    // device output buffer that transfer reads)
+    J.offsets.assign((size_t)use->nreduce + 1, 0);
+    uint8_t* d = nullptr;
+    uint64_t n = 0;
+    rc = reduce_common(c, use, 0xFFFFFFFFu, &d, &n, J.offsets.data());
+    const uint64_t nkeys = use->r.n;
+    mrg_parts_free(use);
+    if (rc) return rc;
+    if (n + 1 > J.cap) {
+        if (J.host) hipHostFree(J.host);
+        J.host = nullptr;
+        J.cap = 0;
+        const size_t cap = n + n / 4 + 4096;
+        if (hipHostMalloc((void**)&J.host, cap, hipHostMallocDefault) != hipSuccess)
+            return fail(c, MRG_ENOMEM, "pinned output alloc");
+        J.cap = cap;
+    }
+    // the output crosses PCIe on the output stream after the reduce (the reduce
+    // ends with a stream synchronize, so its bytes are complete here)
+    HCHK(c, hipEventRecord(J.start, c->os));
+    if (n) HCHK(c, hipMemcpyAsync(J.host, d, n, hipMemcpyDeviceToHost, c->os));
+    HCHK(c, hipEventRecord(J.done, c->os));
+    keep.reduce_ms = ev_ms(c->ev[4], c->ev[5]);
+    keep.output_bytes = n;
+    keep.distinct_keys = nkeys;
+    J.n = n;
+    J.stats = keep;
+    c->stats = keep;
+    c->aj_count++;
+    return MRG_OK;
+}
+
+int mrg_job_wait(mrg_ctx* c, void** bytes, size_t* nb, uint64_t* offsets) {
+    if (!c || !bytes || !nb || !offsets) return MRG_EINVAL;
+    int rc;
+    if ((rc = bind(c))) return rc;
+    if (c->aj_count == 0) return fail(c, MRG_EINVAL, "job_wait: no job queued");
+    mrg_ctx::AsyncJob& J = c->aj[c->aj_head];
+    HCHK(c, hipEventSynchronize(J.done));
+    J.stats.d2h_ms = ev_ms(J.start, J.done);
+    c->stats = J.stats;
+    for (size_t i = 0; i < J.offsets.size(); i++) offsets[i] = J.offsets[i];
+    *bytes = J.host;  // context-owned; valid until the next mrg_job_wait (do not mrg_free)
+    *nb = J.n;
+    c->aj_head ^= 1;
+    c->aj_count--;
     return MRG_OK;
 }
 

@@ -274,6 +274,8 @@ typedef __attribute__((address_space(3))) uint32_t lds_u32_unaligned __attribute
 struct LdsLetters {
     const lds_u8* l1;   // [kLetterLdsPages]
     const lds_u32* l2;  // [kLetterUnique * 8]
+    const lds_u32* b2;  // letters among code points < U+0800 (every 2-byte rune): 2048 bits, one read
+                        // per rune instead of l1 + l2 (nullptr: l1 / l2 only)
 };
 __device__ __forceinline__ bool is_letter_lds(uint32_t cp, LdsLetters L) {
     if (cp >= ((uint32_t)kLetterLdsPages << 8)) return false;
@@ -306,6 +308,50 @@ __device__ __forceinline__ uint32_t flags_to_bits16(uint32_t f0, uint32_t f1, ui
 // Work is one loop turn per lead byte of the lane (LDS reads only).  first: the
 // look-back lane (q0 = 0), whose bytes before the slot read as 0 (only its bit
 // 15 is used, which depends on bytes >= 9).
+// The letter bits (relative to q0 - 3) of the rune whose lead byte is at q0 - 3
+// + i, given its 4 bytes w (Go's acceptance ranges; 0 if invalid or no letter).
+// Split in two halves so that two leads' LDS reads can be in flight together:
+// lead_decode gives the code point, its continuation count and validity;
+// lead_word the table word holding its letter bit.
+struct LeadRune {
+    uint32_t cp, need;
+    bool valid;
+};
+__device__ __forceinline__ LeadRune lead_decode(uint32_t w) {
+    const uint32_t c0 = w & 0xFFu, c1 = (w >> 8) & 0xFFu, c2 = (w >> 16) & 0xFFu, c3 = w >> 24;
+    const uint32_t need = c0 >= 0xF0u ? 3u : c0 >= 0xE0u ? 2u : 1u;  // continuation bytes
+    const uint32_t lo = c0 == 0xE0u ? 0xA0u : c0 == 0xF0u ? 0x90u : 0x80u;
+    const uint32_t hi = c0 == 0xEDu ? 0x9Fu : c0 == 0xF4u ? 0x8Fu : 0xBFu;
+    const bool valid = c0 >= 0xC2u && c0 <= 0xF4u && c1 >= lo && c1 <= hi && (need < 2u || (c2 & 0xC0u) == 0x80u) &&
+                       (need < 3u || (c3 & 0xC0u) == 0x80u);
+    const uint32_t cp = need == 1u ? ((c0 & 0x1Fu) << 6) | (c1 & 0x3Fu)
+                      : need == 2u ? ((c0 & 0x0Fu) << 12) | ((c1 & 0x3Fu) << 6) | (c2 & 0x3Fu)
+                                   : ((c0 & 0x07u) << 18) | ((c1 & 0x3Fu) << 12) | ((c2 & 0x3Fu) << 6) | (c3 & 0x3Fu);
+    return LeadRune{cp, need, valid};
+}
+// the table word of cp's letter bit (bit cp & 31): a 2-byte rune by one read of
+// the 2048-bit table, a longer one by the two-level l1 / l2 tables
+__device__ __forceinline__ uint32_t lead_word(const LeadRune& r, LdsLetters L) {
+    if (r.need == 1u && L.b2) return L.b2[r.cp >> 5];
+    if (r.cp >= ((uint32_t)kLetterLdsPages << 8)) return 0u;
+    return L.l2[L.l1[r.cp >> 8] * 8u + ((r.cp >> 5) & 7u)];
+}
+
+// Letter mask of the 16 slot bytes [q0, q0 + 16) with Go's decoding semantics
+// (strings.FieldsFunc's range loop + unicode.IsLetter, mrapps/wc.go:23,26;
+// SURVEY.md Appendix A.1), for a slot in LDS whose bytes [q0 - 4, q0 + 19) are
+// readable:
+//   - ASCII letters by SWAR;
+//   - every lead byte (>= 0xC0) in [q0 - 3, q0 + 16) starts a rune: a lead is
+//     never a continuation byte, so no valid sequence can cover it (the local
+//     rune-start rule always holds); its sequence is checked with Go's
+//     acceptance ranges and, if valid and a letter, marks all its bytes;
+//   - continuation bytes outside a valid sequence and invalid leads are
+//     U+FFFD, not letters (nothing to do).
+// Work is one loop turn per TWO lead bytes of the lane (their LDS reads in
+// flight together: the rune bytes, then the table word).  first: the look-back
+// lane (q0 = 0), whose bytes before the slot read as 0 (only its bit 15 is used,
+// which depends on bytes >= 9).
 __device__ __forceinline__ uint32_t utf8_mask16(const lds_u8* slot, uint32_t q0, bool first, LdsLetters L) {
     const lds_u32* s4 = (const lds_u32*)(slot + q0);
     const uint32_t w0 = first ? 0u : s4[-1], w1 = s4[0], w2 = s4[1], w3 = s4[2], w4 = s4[3];
@@ -314,19 +360,17 @@ __device__ __forceinline__ uint32_t utf8_mask16(const lds_u8* slot, uint32_t q0,
     uint32_t leads = (flags_to_bits16(lead_flags4(w0), lead_flags4(w1), lead_flags4(w2), lead_flags4(w3)) >> 1) |
                      (flags_to_bits16(lead_flags4(w4), 0u, 0u, 0u) << 15);
     while (leads) {
-        const uint32_t i = __builtin_ctz(leads);
+        const uint32_t i1 = __builtin_ctz(leads);
         leads &= leads - 1;
-        const uint32_t w = *(const lds_u32_unaligned*)(slot + q0 + i - 3);
-        const uint32_t c0 = w & 0xFFu, c1 = (w >> 8) & 0xFFu, c2 = (w >> 16) & 0xFFu, c3 = w >> 24;
-        const uint32_t need = c0 >= 0xF0u ? 3u : c0 >= 0xE0u ? 2u : 1u;  // continuation bytes
-        const uint32_t lo = c0 == 0xE0u ? 0xA0u : c0 == 0xF0u ? 0x90u : 0x80u;
-        const uint32_t hi = c0 == 0xEDu ? 0x9Fu : c0 == 0xF4u ? 0x8Fu : 0xBFu;
-        const bool valid = c0 >= 0xC2u && c0 <= 0xF4u && c1 >= lo && c1 <= hi && (need < 2u || (c2 & 0xC0u) == 0x80u) &&
-                           (need < 3u || (c3 & 0xC0u) == 0x80u);
-        const uint32_t cp = need == 1u ? ((c0 & 0x1Fu) << 6) | (c1 & 0x3Fu)
-                          : need == 2u ? ((c0 & 0x0Fu) << 12) | ((c1 & 0x3Fu) << 6) | (c2 & 0x3Fu)
-                                       : ((c0 & 0x07u) << 18) | ((c1 & 0x3Fu) << 12) | ((c2 & 0x3Fu) << 6) | (c3 & 0x3Fu);
-        if (valid && is_letter_lds(cp, L)) m |= ((((2u << need) - 1u) << i) >> 3) & 0xFFFFu;
+        const bool two = leads != 0;
+        const uint32_t i2 = two ? __builtin_ctz(leads) : i1;
+        leads &= leads - 1;  // (no-op when none was left)
+        const uint32_t wa = *(const lds_u32_unaligned*)(slot + q0 + i1 - 3);
+        const uint32_t wb = *(const lds_u32_unaligned*)(slot + q0 + i2 - 3);
+        const LeadRune ra = lead_decode(wa), rb = lead_decode(wb);
+        const uint32_t ta = lead_word(ra, L), tb = lead_word(rb, L);
+        if (ra.valid && ((ta >> (ra.cp & 31u)) & 1u)) m |= ((((2u << ra.need) - 1u) << i1) >> 3) & 0xFFFFu;
+        if (two && rb.valid && ((tb >> (rb.cp & 31u)) & 1u)) m |= ((((2u << rb.need) - 1u) << i2) >> 3) & 0xFFFFu;
     }
     return m;
 }

@@ -29,6 +29,7 @@ enum : uint32_t {
     kStSpin = 1u << 3,
     kStRecFull = 1u << 4,   // the record output buffer was too small
     kStSegFull = 1u << 5,   // an aggregation miss segment buffer was too small (sized without a host read)
+    kStLrecFull = 1u << 6,  // a map workgroup's region of 32-byte long-word records was too small
 };
 
 struct ShortSlot {
@@ -156,11 +157,19 @@ struct Tables {
     const uint4* dict;      // dictionary image [kDictSets] (nullptr: no dictionary)
     uint32_t* dict_cnt;     // [nwg][kDictSlots] per-map-workgroup dictionary counts
     unsigned long long* dbg;  // diagnostics (MRG_DEBUG_TIMES): per-workgroup s_memrealtime stamps, or nullptr
+    // wc words of 17-32 bytes that end inside their map window: the key bytes as
+    // 32-byte zero-padded records (two uint4), region [map workgroup][lrec_cap];
+    // lrec_cnt[g] = records workgroup g appended (past lrec_cap: kStLrecFull).
+    // nullptr: every long word goes to the start-offset list (wc_long_kernel).
+    uint4* lrec;
+    uint32_t* lrec_cnt;
+    uint32_t lrec_cap;
 };
 
 struct LetterTables {
     const uint8_t* l1;
     const uint32_t* l2;
+    const uint32_t* b2;  // letters among code points < U+0800: 2048 bits (from l1 / l2, built at mrg_open)
 };
 // The map kernels' LDS copy of the letter tables (letter_table.inc): l1 of the
 // first kLetterLdsPages 256-code-point pages (no letter lies above them in
@@ -170,6 +179,9 @@ constexpr int kLetterUnique = 111;
 
 // ---- launchers (mrgpu_map.hip) ----
 void clear_tables(const Tables& t, bool short_table, hipStream_t s);
+// Count the map's 32-byte long-word records (one workgroup per map workgroup's
+// region) into the LongTable (mrgpu_map.hip).
+void launch_wc_lrec(const Tables& t, uint32_t nwg, hipStream_t s);
 // ---- wc pipeline (mrgpu_wc.hip) ----
 uint32_t wc_map_grid(uint64_t n, int grid);
 // Chunks [cbeg, cend) of the split (kOwn = 992 input bytes each; default: all);

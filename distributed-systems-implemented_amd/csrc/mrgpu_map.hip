@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restr
     for (uint32_t i = threadIdx.x; i < (uint32_t)kLetterUnique * 8; i += kLongWG) A.l2[i] = lt.l2[i];
     for (uint32_t i = threadIdx.x; i < (uint32_t)kLetterLdsPages; i += kLongWG) A.l1[i] = lt.l1[i];
     __syncthreads();
-    const LdsLetters L{(const lds_u8*)A.l1, (const lds_u32*)A.l2};
+    const LdsLetters L{(const lds_u8*)A.l1, (const lds_u32*)A.l2, nullptr};
     // this workgroup's contiguous share of the list
     const uint64_t per = (nlist + gridDim.x - 1) / gridDim.x;
     const uint64_t b = (uint64_t)blockIdx.x * per, e = b + per < nlist ? b + per : nlist;
@@ -137,6 +137,90 @@ __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restr
         const uint32_t c = A.cnt[i];
         if (c) long_insert(t, A.h[i], in + A.rep[i], A.len[i], c);
     }
+}
+
+// Words of 17-32 bytes handed over by the map kernel as 32-byte zero-padded key
+// records (the map read them from its LDS window; no decode of the input here):
+// one workgroup per map workgroup's record region.  Each lane hashes a record
+// (FNV-1a-64 of its bytes, the same hash wc_long_kernel and the LongTable use,
+// so a word that reached the table by either path meets itself there) and counts
+// it in an LDS table confirmed by comparing the two records' 32 bytes (equal
+// zero-padded records <=> equal keys: letters are never 0x00).  The HBM
+// LongTable then sees one insert per (workgroup, distinct word), its
+// representative the record itself (the collect copies the key bytes from it).
+constexpr int kLrecSlots = 4096;
+struct alignas(16) LrecLds {
+    unsigned long long h[kLrecSlots];    // hash | 1 (0: empty)
+    unsigned long long rep[kLrecSlots];  // address of the slot's first record (kRepUnpub until published)
+    uint32_t len[kLrecSlots];
+    uint32_t cnt[kLrecSlots];
+};
+
+__global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t) {
+    __shared__ LrecLds A;
+    const uint32_t g = blockIdx.x;
+    const uint32_t cap = t.lrec_cap;
+    uint32_t n = t.lrec_cnt[g];
+    if (n > cap) n = cap;  // (overflowed regions are flagged; the map is repeated)
+    if (n == 0) return;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
+        A.h[i] = 0;
+        A.rep[i] = kRepUnpub;
+        A.cnt[i] = 0;
+    }
+    __syncthreads();
+    const uint4* recs = t.lrec + (uint64_t)g * cap * 2;
+    for (uint32_t i = threadIdx.x; i < n; i += kLongWG) {
+        const uint4 a = recs[2 * i], b = recs[2 * i + 1];
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+        uint64_t h = kFnv64Off;
+        uint32_t len = 0;
+#pragma unroll
+        for (int q = 0; q < 32; q++) {
+            const uint32_t c = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
+            if (c == 0) break;
+            h = fnv1a64_step(h, c);
+            len++;
+        }
+        const unsigned long long hk = h | 1ull;
+        const unsigned long long me = (unsigned long long)(uintptr_t)(recs + 2 * i);
+        bool done = false;
+        uint32_t slot = (uint32_t)(hk >> 20) & (kLrecSlots - 1);
+        for (int probe = 0; probe < 16 && !done; probe++, slot = (slot + 1) & (kLrecSlots - 1)) {
+            unsigned long long cur = __hip_atomic_load(&A.h[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if (cur == 0) {
+                cur = atomicCAS(&A.h[slot], 0ull, hk);
+                if (cur == 0) {  // claimed: publish the representative, then count
+                    A.len[slot] = len;
+                    __hip_atomic_store(&A.rep[slot], me, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    atomicAdd(&A.cnt[slot], 1u);
+                    done = true;
+                    break;
+                }
+            }
+            if (cur == hk) {
+                const unsigned long long r = __hip_atomic_load(&A.rep[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (r == kRepUnpub) break;  // being published: never wait here, insert directly
+                const uint4* rr = (const uint4*)(uintptr_t)r;
+                const uint4 ra = rr[0], rb = rr[1];
+                if (ra.x == a.x && ra.y == a.y && ra.z == a.z && ra.w == a.w && rb.x == b.x && rb.y == b.y &&
+                    rb.z == b.z && rb.w == b.w) {
+                    atomicAdd(&A.cnt[slot], 1u);
+                    done = true;
+                }
+            }
+        }
+        if (!done) long_insert(t, h, (const uint8_t*)(uintptr_t)me, len, 1);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
+        const uint32_t c = A.cnt[i];
+        if (c) long_insert(t, A.h[i], (const uint8_t*)(uintptr_t)A.rep[i], A.len[i], c);
+    }
+}
+
+void launch_wc_lrec(const Tables& t, uint32_t nwg, hipStream_t s) {
+    if (t.lrec && nwg) wc_lrec_kernel<<<nwg, kLongWG, 0, s>>>(t);
 }
 
 // ------------------------------------------------------------ grep kernels
@@ -804,6 +888,7 @@ __global__ void clear_tables_kernel(Tables t, bool short_table) {
         const uint64_t nc = 2ull * t.sp.nb * t.sp.nwg;
         for (uint64_t i = i0; i < nc; i += stride) t.sp.counts[i] = 0;
     }
+    if (t.lrec_cnt && i0 < (uint64_t)kMaxMapWGs) t.lrec_cnt[i0] = 0;  // (workgroups the map does not launch stay 0)
     if (short_table)
         for (uint64_t i = i0; i <= t.sh_mask; i += stride) t.sh[i] = ShortSlot{0, kUnwritten, 0, 0};
     for (uint64_t i = i0; i <= t.lo_mask; i += stride) t.lo[i] = LongSlot{0, nullptr, 0, 0};

@@ -72,6 +72,11 @@ struct alignas(16) MapLdsT {
     // spill cursors: [0, NB) 8-byte streams, [NB, 2 NB) 16-byte streams, then per-lane dummies for hits
     uint32_t curs[2 * NB + kWave];
     uint32_t lt2[kLetterUnique * 8];            // letter tables (non-ASCII chunks): l2 pages
+    uint32_t lrec_n;                            // 32-byte long-word records this workgroup appended
+    // letters among code points < U+0800 (2-byte runes: one table read), except
+    // in the default 256-bucket layout (the others have no LDS left: l1 / l2 there)
+    static constexpr bool kB2 = NB == kSpillBucketsLo;
+    uint32_t lb2[kB2 ? 64 : 1];
     uint8_t lt1[kLetterLdsPages];               // l1 of the pages that hold letters
 };
 static_assert(kSlotBytes == 1024 && kMaskLens * 16 <= 512, "kmask index fits 0x1F0");
@@ -337,9 +342,12 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         else if (resume && b < 2u * NB) v = t.sp.counts[(uint64_t)(b - NB) * t.sp.nwg + blockIdx.x];
         curs[b] = v;
     }
+    if (tid == 0) L.lrec_n = resume && t.lrec ? t.lrec_cnt[blockIdx.x] : 0u;
     for (uint32_t i = tid; i < (uint32_t)kLetterUnique * 8; i += kT) L.lt2[i] = lt.l2[i];
     for (uint32_t i = tid; i < (uint32_t)kLetterLdsPages; i += kT) L.lt1[i] = lt.l1[i];
-    const LdsLetters lds_lt{(const lds_u8*)L.lt1, (const lds_u32*)L.lt2};
+    if (MapLdsT<NW, NB>::kB2 && tid < 64) L.lb2[tid] = lt.b2[tid];
+    const LdsLetters lds_lt{(const lds_u8*)L.lt1, (const lds_u32*)L.lt2,
+                            MapLdsT<NW, NB>::kB2 ? (const lds_u32*)L.lb2 : nullptr};
     if (tid < kMaskLens * 4) {  // byte masks: dword d of kmask[len] keeps clamp(len - 4d, 0, 4) bytes
         const int nb = min(max((int)(tid >> 2) - 4 * (int)(tid & 3), 0), 4);
         ((uint32_t*)L.kmask)[tid] = nb == 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
@@ -460,11 +468,18 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
             uint32_t j = incl - nsa;
             const uint32_t pos0 = 16 * lane;
+            // two starts per loop turn: the loop runs max-over-lanes(starts) / 2
+            // turns, its control (compare, exec update, branch) paid once per pair
             while (SA) {
-                const uint32_t bit = __builtin_ctz(SA);
-                const uint32_t len = ffbl_raw(nl >> bit);  // -1 when no terminator in the window
-                list[j++] = (uint16_t)((pos0 + bit) | (len << 10));
+                const uint32_t b1 = ffbl_raw(SA);
                 SA &= SA - 1;
+                const uint32_t b2 = ffbl_raw(SA);  // -1: this lane had one start left
+                const uint32_t e1 = (pos0 + b1) | (ffbl_raw(nl >> b1) << 10);  // len -1: no terminator in the window
+                const uint32_t e2 = (pos0 + b2) | (ffbl_raw(nl >> (b2 & 31u)) << 10);
+                list[j] = (uint16_t)e1;
+                if (SA) list[j + 1] = (uint16_t)e2;
+                SA &= SA - 1;
+                j += 2;
             }
             wave_sync();
             if constexpr ((mode & 2) != 0) {
@@ -535,42 +550,95 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     // The extra store only lengthens the next counted wait.
                     if (mLng[0] | mLng[1] | mLng[2]) {
                         if (passes == 1) {
-                            lds_u64* lst = (lds_u64*)L.ring[wv][kf];
-                            uint32_t nlong = 0;
+                            // Words of 17-32 bytes that end inside the window leave as
+                            // 32-byte key records, read here from the slot (wc_lrec_kernel
+                            // counts them: no second decode of the input); longer words and
+                            // words running past the window take the start-offset list.
+                            // The length comes from the letter masks of the word's lane and
+                            // the next two (ds_bpermute; lanes past 63 are unknown bytes,
+                            // taken as letters, so a word reaching them falls back).
+                            uint64_t mFall[kBatch];
+                            const Tables& tr = cold(t);
         #pragma unroll
                             for (int u = 0; u < kBatch; u++) {
-                                if (__builtin_amdgcn_inverse_ballot_w64(mLng[u]))
-                                    lst[nlong + mbcnt64(mLng[u])] = cs - kBack + (e[u] & 0x3FFu);
-                                nlong += (uint32_t)__popcll(mLng[u]);
+                                mFall[u] = mLng[u];
+                                if (mLng[u] == 0 || tr.lrec == nullptr) continue;
+                                const uint32_t p = e[u] & 0x3FFu, lw = p >> 4;
+                                const uint32_t m0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lw << 2), (int)mA);
+                                const uint32_t m1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lw + 1) << 2), (int)mA);
+                                const uint32_t m2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lw + 2) << 2), (int)mA);
+                                const uint64_t win = (uint64_t)(m0 & 0xFFFFu) |
+                                                     ((uint64_t)(lw + 1 < 64u ? m1 & 0xFFFFu : 0xFFFFu) << 16) |
+                                                     ((uint64_t)(lw + 2 < 64u ? m2 & 0xFFFFu : 0xFFFFu) << 32) |
+                                                     (0xFFFFull << 48);
+                                const uint32_t wl = (uint32_t)__builtin_ctzll((~win >> (p & 15u)) | (1ull << 63));
+                                const uint64_t mR = mLng[u] & __ballot(wl <= 32u);
+                                if (mR == 0) continue;
+                                uint32_t rbase = 0;
+                                if (lane == 0) rbase = atomicAdd(&L.lrec_n, (uint32_t)__popcll(mR));
+                                rbase = __builtin_amdgcn_readfirstlane(rbase);
+                                const uint32_t rcap = tr.lrec_cap;
+                                const uint32_t idx = rbase + mbcnt64(mR);
+                                const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
+                                    (void*)(tr.lrec + (uint64_t)blockIdx.x * rcap * 2u), (short)0, (int)(rcap * 32u), 0x00020000);
+                                const uint32_t ro = __builtin_amdgcn_inverse_ballot_w64(mR) && idx < rcap ? idx * 32u : kOutOfRange;
+                                // the key's 32 bytes from the slot, zero past its length, 16 at a time
+        #pragma unroll
+                                for (int hf = 0; hf < 2; hf++) {
+                                    const lds_u32* q4 = (const lds_u32*)(uintptr_t)(bufa + (p & ~3u) + 16u * hf);
+                                    uint32_t d[5], k[4];
+        #pragma unroll
+                                    for (int i = 0; i < 5; i++) d[i] = q4[i];
+        #pragma unroll
+                                    for (int i = 0; i < 4; i++) {
+                                        const int nb = min(max((int)wl - 4 * (4 * hf + i), 0), 4);
+                                        k[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], p) &
+                                               (nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u);
+                                    }
+                                    __builtin_amdgcn_raw_buffer_store_b128((u32x4){k[0], k[1], k[2], k[3]}, rsr,
+                                                                           ro == kOutOfRange ? kOutOfRange : ro + 16u * hf, 0, 0);
+                                }
+                                if (rbase + (uint32_t)__popcll(mR) > rcap && lane == 0) set_status(tr.ctr, kStLrecFull);
+                                mFall[u] = mLng[u] & ~mR;
                             }
-                            const Tables& tc = cold(t);
-                            if (nlong > lleft) {  // a fresh range (rare): close the old one, one atomic, drain
-                                list_close(tc, lbase, lleft, lane);
-                                const uint32_t want = kLongReserve;
-                                unsigned long long b0 = 0;
-                                if (lane == 0) b0 = atomicAdd(&tc.ctr->nlist, (unsigned long long)want);
-                                lbase = readfirstlane64(b0);
-                                lleft = want;
-                                if (lbase + want > tc.list_cap && lane == 0) set_status(tc.ctr, kStListFull);
-                                wait_vmem_all();
+                            if (mFall[0] | mFall[1] | mFall[2]) {
+                                lds_u64* lst = (lds_u64*)L.ring[wv][kf];
+                                uint32_t nlong = 0;
+            #pragma unroll
+                                for (int u = 0; u < kBatch; u++) {
+                                    if (__builtin_amdgcn_inverse_ballot_w64(mFall[u]))
+                                        lst[nlong + mbcnt64(mFall[u])] = cs - kBack + (e[u] & 0x3FFu);
+                                    nlong += (uint32_t)__popcll(mFall[u]);
+                                }
+                                const Tables& tc = cold(t);
+                                if (nlong > lleft) {  // a fresh range (rare): close the old one, one atomic, drain
+                                    list_close(tc, lbase, lleft, lane);
+                                    const uint32_t want = kLongReserve;
+                                    unsigned long long b0 = 0;
+                                    if (lane == 0) b0 = atomicAdd(&tc.ctr->nlist, (unsigned long long)want);
+                                    lbase = readfirstlane64(b0);
+                                    lleft = want;
+                                    if (lbase + want > tc.list_cap && lane == 0) set_status(tc.ctr, kStListFull);
+                                    wait_vmem_all();
+                                }
+                                uint64_t* lptr;
+                                uint64_t lcap;
+                                cold_list(t, lptr, lcap);
+                                // the descriptor starts at this range's next entry, so its 32-bit
+                                // offsets never limit the list's size (a base at the list start
+                                // dropped entries past 2^29 without a status bit: ADVICE r03); its
+                                // range check stops at the list's capacity (kStListFull is set
+                                // when a range is reserved past it, and the run is repeated)
+                                const uint64_t room = lbase < lcap ? lcap - lbase : 0;
+                                const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+                                    (void*)(lptr + lbase), (short)0, (int)(room < (0xFFFFFF00ull >> 3) ? room * 8u : 0xFFFFFF00ull),
+                                    0x00020000);
+                                const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
+                                __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
+                                                                      lane < nlong ? lane * 8u : kOutOfRange, 0, 0);
+                                lbase += nlong;
+                                lleft -= nlong;
                             }
-                            uint64_t* lptr;
-                            uint64_t lcap;
-                            cold_list(t, lptr, lcap);
-                            // the descriptor starts at this range's next entry, so its 32-bit
-                            // offsets never limit the list's size (a base at the list start
-                            // dropped entries past 2^29 without a status bit: ADVICE r03); its
-                            // range check stops at the list's capacity (kStListFull is set
-                            // when a range is reserved past it, and the run is repeated)
-                            const uint64_t room = lbase < lcap ? lcap - lbase : 0;
-                            const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
-                                (void*)(lptr + lbase), (short)0, (int)(room < (0xFFFFFF00ull >> 3) ? room * 8u : 0xFFFFFF00ull),
-                                0x00020000);
-                            const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
-                            __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
-                                                                  lane < nlong ? lane * 8u : kOutOfRange, 0, 0);
-                            lbase += nlong;
-                            lleft -= nlong;
                         } else {  // several passes (> 192 words): the list slot is still needed
         #pragma unroll
                             for (int u = 0; u < kBatch; u++)
@@ -834,6 +902,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
 
     __syncthreads();
+    if (tid == 0 && t.lrec) t.lrec_cnt[blockIdx.x] = L.lrec_n;
     unsigned long long spilled = 0, hits = 0;
     for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {  // (this launch's share: minus the resumed values)
         const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[NB + b], sub);

@@ -38,7 +38,7 @@ EXPORTED = [
     "mrg_open", "mrg_close", "mrg_last_error", "mrg_device_count", "mrg_map", "mrg_parts_merge",
     "mrg_parts_info", "mrg_parts_export", "mrg_parts_import",
     "mrg_parts_export_json", "mrg_parts_import_json", "mrg_parts_free", "mrg_reduce",
-    "mrg_reduce_all", "mrg_run_job", "mrg_comm_unique_id", "mrg_comm_init", "mrg_exchange",
+    "mrg_reduce_all", "mrg_run_job", "mrg_run_job_async", "mrg_job_wait", "mrg_comm_unique_id", "mrg_comm_init", "mrg_exchange",
     "mrg_exchange_group",
     "mrg_device_alloc", "mrg_device_free", "mrg_memcpy_h2d", "mrg_memcpy_d2h", "mrg_sort_pairs", "mrg_sync",
     "mrg_get_stats", "mrg_set_option", "mrg_ihash", "mrg_free",
@@ -118,6 +118,8 @@ def load_library(path: str | None = None):
     L.mrg_reduce_all.argtypes = [vp, vp, POINTER(vp), POINTER(c_size_t), POINTER(c_uint64)]
     L.mrg_run_job.argtypes = [vp, c_int, vp, c_size_t, c_int, vp, c_size_t, c_uint32, POINTER(vp),
                               POINTER(c_size_t), POINTER(c_uint64)]
+    L.mrg_run_job_async.argtypes = [vp, c_int, vp, c_size_t, c_int, vp, c_size_t, c_uint32]
+    L.mrg_job_wait.argtypes = [vp, POINTER(vp), POINTER(c_size_t), POINTER(c_uint64)]
     L.mrg_comm_unique_id.argtypes = [POINTER(c_uint8)]
     L.mrg_comm_init.argtypes = [vp, POINTER(c_uint8), c_int, c_int]
     L.mrg_exchange.argtypes = [vp, vp, POINTER(vp)]
@@ -307,6 +309,33 @@ class Context:
         if not copy_out:
             return p.value, n.value, list(offs)
         data = ctypes.string_at(p, n.value) if n.value else b""  # context-owned buffer: no mrg_free
+        return [data[offs[i]:offs[i + 1]] for i in range(nreduce)]
+
+    def run_job_async(self, app: int, data=None, pattern: bytes = b"", nreduce: int = 10,
+                      device_ptr: int | None = None, nbytes: int | None = None):
+        """mrg_run_job_async: queue a whole job; its output transfer overlaps the
+        next queued job.  Collect outputs in order with job_wait()."""
+        pat_p, _kp = _buf(pattern) if pattern else (None, None)
+        if device_ptr is not None:
+            rc = self.L.mrg_run_job_async(self.h, app, c_void_p(device_ptr), nbytes, MRG_INPUT_DEVICE, pat_p,
+                                          len(pattern), nreduce)
+        else:
+            buf, _keep = _buf(data)
+            self._async_keep = _keep
+            rc = self.L.mrg_run_job_async(self.h, app, buf, len(data), MRG_INPUT_HOST, pat_p, len(pattern), nreduce)
+        self._check(rc, "mrg_run_job_async")
+        self._async_nreduce = getattr(self, "_async_nreduce", [])
+        self._async_nreduce.append(nreduce)
+
+    def job_wait(self, copy_out: bool = True):
+        """The oldest queued job's output: list of mr-out-r bytes (or (ptr, n, offsets))."""
+        nreduce = self._async_nreduce.pop(0)
+        p, n = c_void_p(), c_size_t()
+        offs = (c_uint64 * (nreduce + 1))()
+        self._check(self.L.mrg_job_wait(self.h, byref(p), byref(n), offs), "mrg_job_wait")
+        if not copy_out:
+            return p.value, n.value, list(offs)
+        data = ctypes.string_at(p, n.value) if n.value else b""
         return [data[offs[i]:offs[i + 1]] for i in range(nreduce)]
 
     # -- multi-GPU

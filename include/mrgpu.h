@@ -158,6 +158,18 @@ int mrg_reduce_all(mrg_ctx* ctx, const mrg_parts* p, void** bytes, size_t* n, ui
 int mrg_run_job(mrg_ctx* ctx, int app, const void* buf, size_t len, int input_kind, const uint8_t* pat,
                 size_t plen, uint32_t nreduce, void** bytes, size_t* n, uint64_t* offsets);
 
+/* Pipelined jobs (a worker's stream of map tasks, mr/worker.go:46-161): as
+ * mrg_run_job, but returns once the job's output transfer is queued; its bytes
+ * cross PCIe on a second stream into a context-owned pinned buffer while the
+ * caller queues the next job, whose map overlaps that transfer.  At most two
+ * jobs are queued (a third call returns MRG_EINVAL); mrg_job_wait returns the
+ * oldest queued job's output (bytes valid until the next mrg_job_wait on this
+ * context; offsets[nreduce + 1] as mrg_run_job) and its stats (d2h_ms = its
+ * transfer).  Any other reduce on the context first waits for queued transfers. */
+int mrg_run_job_async(mrg_ctx* ctx, int app, const void* buf, size_t len, int input_kind, const uint8_t* pat,
+                      size_t plen, uint32_t nreduce);
+int mrg_job_wait(mrg_ctx* ctx, void** bytes, size_t* n, uint64_t* offsets);
+
 /* Multi-GPU (one process or thread per GPU).  The 128-byte unique id is made by
  * one rank and shared out of band (the coordinator RPC stays unchanged). */
 int mrg_comm_unique_id(uint8_t id[128]);

@@ -90,3 +90,42 @@ def test_intermediate_codec_roundtrip():
     assert d["keys"] == keys and list(d["count"]) == [1, 2, 3, 4, 5] and list(d["kpart"]) == [0, 1, 2, 3, 4]
     with pytest.raises(ValueError):
         I.decode(b[:-1])
+
+
+MULTI = textwrap.dedent(r'''
+    import json, os, sys
+    sys.path.insert(0, sys.argv[1])
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    import bench
+    rank, world = dist.get_rank(), dist.get_world_size()
+    # per-step stats as mrg_get_stats reports them after an RCCL exchange
+    st = {"exchange_ms": 3.0 + rank, "exchange_a2a_ms": 2.0 + rank, "exchange_unpack_ms": 1.0,
+          "shuffle_send_bytes": 1.0e9 * (rank + 1), "rccl_nranks": world, "rccl_rank": rank, "device": rank}
+    m = bench.multi_fields([st, st], t_max=0.02, t1=0.016, world=world, shared=False, ndev=world)
+    if rank == 0:
+        print(json.dumps(m))
+    dist.destroy_process_group()
+''')
+
+
+def test_multi_gpu_fields_gloo(tmp_path):
+    """bench.py's N > 1 fields on two gloo ranks: the exchange split into its
+    all-to-all and the owner's unpack + re-aggregation (max over ranks), the rank
+    count RCCL reported and each rank's device, gathered to rank 0; the xGMI
+    rate is taken over the all-to-all time only."""
+    script = tmp_path / "multi.py"
+    script.write_text(MULTI)
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    res = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                          "--master-addr", "127.0.0.1", "--master-port", "29518", str(script), ROOT],
+                         capture_output=True, text=True, timeout=240, env=env)
+    assert res.returncode == 0, res.stderr[-3000:]
+    m = json.loads([l for l in res.stdout.splitlines() if l.startswith("{")][-1])
+    assert m["exchange_ms"] == 4.0 and m["exchange_a2a_ms"] == 3.0 and m["exchange_unpack_ms"] == 1.0
+    assert m["rccl_nranks"] == [2]
+    assert [(r["rank"], r["rccl_rank"], r["device"]) for r in m["ranks"]] == [(0, 0, 0), (1, 1, 1)]
+    assert m["shuffle_bytes_per_gpu"] == 2_000_000_000
+    # rank 0's own rate: 1e9 bytes over its 2 ms all-to-all; 1 link at P = 2
+    assert m["xgmi_achieved_GBps"] == 500.0 and m["xgmi_peak_GBps"] == 153.0
+    assert m["weak_scaling_efficiency"] == 0.8

@@ -96,19 +96,28 @@ def test_wc_synthetic(wctx, kind, V, seed, inv):
         assert wctx.stats()["dict_hits"] > 0
 
 
-@pytest.mark.parametrize("list_cap", [0, 300])
-def test_wc_long_words_many(wctx, list_cap):
+@pytest.mark.parametrize("list_cap,lrec", [(0, 0), (300, 0), (0, 8), (300, -1)])
+def test_wc_long_words_many(wctx, list_cap, lrec):
     """Mixed-script text with many words over 16 bytes, and splits made only of
-    17-70-byte words: the map waves' reserved ranges of the long-word list and
-    their closing holes, the list overflow + re-run (a 300-entry list), and the
-    long-word kernel's LDS pre-aggregation of hot long words."""
+    17-70-byte words: words of 17-32 bytes ending inside the map window leave as
+    32-byte key records (lrec 0; lrec 8: 8-record regions that overflow, are
+    regrown from the busiest workgroup's count and re-run; -1: records off), the
+    rest go to the map waves' reserved ranges of the long-word list with their
+    closing holes (list overflow + re-run: a 300-entry list), and both long-word
+    kernels' LDS pre-aggregation of hot long words."""
     files = cases.synthetic(C.KIND_UTF8, 20000, [2_000_000, 1_000_001], 21, 0.0005) + \
         [cases.long_words(3_000_000, 1), cases.long_words(70_000, 2)]
     wctx.set_option("list_cap", list_cap)
+    if lrec > 0:
+        wctx.set_option("lrec_cap", lrec)
+    if lrec < 0:
+        wctx.set_option("long_records", -1)
     try:
         check(wctx, "wc", files, nreduces=(1, 10))
     finally:
         wctx.set_option("list_cap", 0)
+        wctx.set_option("lrec_cap", 0)
+        wctx.set_option("long_records", 0)
 
 
 def test_grep_synthetic(ctx):
@@ -783,3 +792,36 @@ def test_run_job_output_to_host(ctx, direct):
                 assert ctx.run_job(MRG_APP_GREP, f, pattern=pat, nreduce=4) == want, name
     finally:
         ctx.set_option("out_direct", 0)
+
+
+@pytest.mark.parametrize("app", ["wc", "grep:distributed"])
+def test_run_job_async_pipelined(ctx, app):
+    """mrg_run_job_async / mrg_job_wait: jobs queued two deep (the second job's
+    map overlaps the first's output transfer), outputs returned in order and
+    byte-equal to the oracle; a third queued job is refused; a synchronous job
+    after async ones waits for their transfers."""
+    from mrgpu.lib import MrgError
+    a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
+    pat = b"" if app == "wc" else b"distributed"
+    if app == "wc":
+        jobs = [cases.synthetic(C.KIND_UTF8, 20000, [700_000, 300_001], 70 + k, 0.0005) for k in range(3)]
+    else:
+        jobs = [cases.synthetic_grep(20000, [800_000, 250_000], 80 + k) for k in range(3)]
+    joined = [b"\n".join(f) for f in jobs]
+    want = [O.c_partitioned(app, f, 10) for f in jobs]
+    ctx.run_job_async(a, joined[0], pattern=pat, nreduce=10)
+    ctx.run_job_async(a, joined[1], pattern=pat, nreduce=10)
+    with pytest.raises(MrgError, match="two jobs in flight"):
+        ctx.run_job_async(a, joined[2], pattern=pat, nreduce=10)
+    ctx._async_nreduce.pop()  # (the refused job was never queued)
+    assert ctx.job_wait() == want[0]
+    ctx.run_job_async(a, joined[2], pattern=pat, nreduce=10)
+    assert ctx.job_wait() == want[1]
+    # a synchronous job in between: the queued transfer finishes first, both exact
+    assert ctx.run_job(a, joined[0], pattern=pat, nreduce=10) == want[0]
+    assert ctx.job_wait() == want[2]
+    with pytest.raises(MrgError, match="no job queued"):
+        ctx.L.mrg_job_wait  # noqa: B018 (attribute exists)
+        ctx._async_nreduce.append(10)
+        ctx.job_wait()
+    ctx._async_nreduce.clear()
