@@ -458,6 +458,7 @@ def main():
     ap.add_argument("--no-oracle", action="store_true", help="skip the full-size exact check against the C oracle")
     ap.add_argument("--scaling-workload", default="c5", help="N > 1: workload of the E(P) sub-run ('none' to skip)")
     ap.add_argument("--scaling-steps", type=int, default=2)
+    ap.add_argument("--no-pipelined", action="store_true", help="N > 1: skip the pipelined-jobs measurement")
     ap.add_argument("--splits", type=int, default=0,
                     help="distinct splits resident per rank, rotated over the timed steps (0: 3 at N=1, 2 at N>1)")
     ap.add_argument("--scaling-splits", type=int, default=2, help="resident splits per rank in the E(P) sub-run")
@@ -543,14 +544,18 @@ def main():
                 "agg_ms": round(sum(x["agg_ms"] for x in st_same) / len(st_same), 3),
                 "dict_ms": round(sum(x["dict_ms"] for x in st_same) / len(st_same), 3)}
 
-    # grep's output (~78 MB for C3) crosses PCIe after the whole job: the same K
-    # jobs pipelined two deep (mrg_run_job_async: each job's output transfer
-    # overlaps the next job's map, as a worker's successive map tasks can), for
-    # comparison with the serial steps above
+    # The output (grep C3: ~78 MB, C5: ~110 MB) crosses PCIe after the whole job:
+    # the same K jobs pipelined two deep (mrg_run_job_async: each job's output
+    # transfer overlaps the next job's map, as a worker's successive map tasks
+    # can), reported beside the serial steps above (`value` stays serial)
     pipelined = None
-    if grep:
+    if world == 1 or not args.no_pipelined:
         def run_async(sp):
-            ctx.run_job_async(MRG_APP_GREP, pattern=PATTERN, device_ptr=dptrs[sp], nbytes=nbytes, nreduce=args.nreduce)
+            if grep:
+                ctx.run_job_async(MRG_APP_GREP, pattern=PATTERN, device_ptr=dptrs[sp], nbytes=nbytes,
+                                  nreduce=args.nreduce)
+            else:
+                ctx.run_job_async(MRG_APP_WC, device_ptr=dptrs[sp], nbytes=nbytes, nreduce=args.nreduce)
         if world > 1:
             dist.barrier()
         ctx.sync()

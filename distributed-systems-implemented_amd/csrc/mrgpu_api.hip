@@ -226,6 +226,9 @@ struct mrg_ctx {
     DevBuf lrec, lrec_cnt;              // wc: 32-byte long-word records [map workgroup][lrec_cap], their counts
     uint32_t lrec_cap = 4096;           // records per map workgroup region (grows on kStLrecFull)
     bool lrec_on = true;                // option long_records (-1: every long word through the offset list)
+    // 2048-bucket (high-cardinality) splits: no dictionary, the map kernel
+    // write-combines its 8-byte spill streams in that LDS (option hi_stage)
+    bool hi_stage = false;
     uint64_t arena_hint = 0;            // wc: long-key bytes expected in a split (the previous one's + 25 %)
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     DevBuf ghits, glines, gdefer;        // grep: sorted hits, resolved (start, end) lines, deferred hits
@@ -398,6 +401,7 @@ static Tables make_tables(mrg_ctx* c) {
     t.dict = nullptr;
     t.dict_cnt = (uint32_t*)c->dict_cnt.p;
     t.dbg = c->debug_times && c->dbg.ensure(2 * (kSpillBucketsHi + kMaxMapWGs) * 8) == hipSuccess ? (unsigned long long*)c->dbg.p : nullptr;
+    t.hi_staged = 0;
     t.lrec = nullptr;  // set by wc_map for the split's map (sample maps and grep use the offset list)
     t.lrec_cnt = nullptr;
     t.lrec_cap = 0;
@@ -885,7 +889,8 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
     HCHK(c, c->dict_cnt.ensure((size_t)nwg * kDictSlots * sizeof(uint32_t)));
     HCHK(c, hipEventRecord(c->ev[9], c->s));
     bool have_dict = false;
-    if (c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict, host))) {
+    const bool staged = c->spill_nb == kSpillBucketsHi && c->hi_stage;  // (its kernel has no dictionary)
+    if (!staged && c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict, host))) {
         ingest_finish(c, ing);
         return rc;
     }
@@ -904,6 +909,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         }
         Tables t = make_tables(c);
         t.dict = have_dict ? (const uint4*)c->dict.p : nullptr;
+        t.hi_staged = staged ? 1u : 0u;
         t.nreduce = nreduce;
         t.out = rec_view(c);
         t.out_cap = c->rec_cap;
@@ -1255,6 +1261,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set_compact_ties(c->rws, v >= 0);
     } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default) or via a copy (-1)
         c->out_direct = v >= 0;
+    } else if (!strcmp(name, "hi_stage")) {  // 2048-bucket splits: LDS write-combined spill, no dictionary (1) or not (-1)
+        c->hi_stage = v > 0;
     } else if (!strcmp(name, "long_records")) {  // wc: words of 17-32 bytes as key records (default) or offsets (-1)
         c->lrec_on = v >= 0;
     } else if (!strcmp(name, "lrec_cap")) {  // records per map workgroup region (tests of the overflow path)

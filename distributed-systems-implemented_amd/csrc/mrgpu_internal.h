@@ -164,6 +164,9 @@ struct Tables {
     uint4* lrec;
     uint32_t* lrec_cnt;
     uint32_t lrec_cap;
+    // 2048-bucket layout without a dictionary: the map kernel variant that
+    // write-combines its 8-byte spill streams in LDS (mrgpu_wc.hip, kS)
+    uint32_t hi_staged;
 };
 
 struct LetterTables {

@@ -63,12 +63,17 @@ static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot"
 // base); the dictionary's set offsets are then constant-displaced, which the
 // ds_read offset field absorbs.
 constexpr int kMaskLens = 32;  // kmask[len], len = 0..31 (> 16 = "more than 16 bytes", never used as a key)
-template <int NW, int NB>
+// kS (high-cardinality splits without a dictionary): the 8-byte spill records
+// are write-combined in LDS, 4 per stream (stage8), and leave as 32-byte writes
+// (see the map kernel); the dictionary's LDS holds them instead.
+template <int NW, int NB, bool kS = false>
 struct alignas(16) MapLdsT {
     uint4 kmask[kMaskLens];                     // kmask[len]: the first min(len, 16) of 16 key bytes
-    uint4 dset[kDictSets];                      // dictionary image
+    uint4 dset[kS ? 1 : kDictSets];             // dictionary image
     uint8_t ring[NW][kRing][kSlotStride];
-    uint32_t dcnt[kDictSlots + kWave];          // dictionary counts of this workgroup (+ per-lane miss dummies)
+    uint32_t dcnt[kS ? 1 : kDictSlots + kWave]; // dictionary counts of this workgroup (+ per-lane miss dummies)
+    unsigned long long stage8[kS ? NB : 0][4];  // kS: the records of each 8-byte stream not yet written
+    uint16_t fl[kS ? NB : 0];                   // kS: stream position of stage8[b][0] (low 16 bits)
     // spill cursors: [0, NB) 8-byte streams, [NB, 2 NB) 16-byte streams, then per-lane dummies for hits
     uint32_t curs[2 * NB + kWave];
     uint32_t lt2[kLetterUnique * 8];            // letter tables (non-ASCII chunks): l2 pages
@@ -83,6 +88,7 @@ static_assert(kSlotBytes == 1024 && kMaskLens * 16 <= 512, "kmask index fits 0x1
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBuckets>) <= 160 * 1024, "map LDS budget");
 static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBucketsLo>) <= 160 * 1024, "map LDS budget (256 buckets)");
 static_assert(sizeof(MapLdsT<12, kSpillBucketsHi>) <= 160 * 1024, "map LDS budget (high-cardinality)");
+static_assert(sizeof(MapLdsT<kWavesPerWG, kSpillBucketsHi, true>) <= 160 * 1024, "map LDS budget (staged)");
 
 // v_ffbl_b32 as the hardware defines it: index of the lowest set bit, 0xFFFFFFFF for 0
 // (__builtin_ctz(0) is undefined and the defined variants add a compare and select)
@@ -192,6 +198,20 @@ __device__ __forceinline__ void wait_vmem_iter_wide() {
     asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
 }
 __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// The staged (kS) loop: the flush's 4 stores and the DMA follow the awaited DMA
+__device__ __forceinline__ void wait_vmem_iter_staged() { asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); }
+
+// kS: an 8-byte record bound for stream position pos of bucket b (o8: its store
+// offset, kOutOfRange if the lane has none) joins the stream's LDS group when
+// its position lies in the group [fl[b], fl[b] + 4); otherwise it is stored
+// directly.  Returns the offset the lane still stores at.
+template <class LT>
+__device__ __forceinline__ uint32_t stage_or_store(LT& L, uint32_t b, uint32_t pos, uint64_t key, uint32_t o8) {
+    const uint32_t d = (pos - (uint32_t)L.fl[b]) & 0xFFFFu;
+    const bool st = o8 != kOutOfRange && d < 4u;
+    if (st) *(lds_u64*)&L.stage8[b][d] = key;
+    return st ? kOutOfRange : o8;
+}
 
 // Issue the DMA of chunk c (any c: chunks past the split read as zeros).
 // cs = the chunk's first owned byte (chunk index * kOwn)
@@ -305,7 +325,7 @@ __device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint
 // sc1, 0x8000 = sc0 sc1)
 constexpr int dma_policy(uint32_t mode) { return (mode & 0x100) ? 0 : (mode & 0x4000) ? 2 : (mode & 0x8000) ? 3 : 1; }
 
-template <uint32_t mode, int NW = kWavesPerWG, int NB = kSpillBuckets>
+template <uint32_t mode, int NW = kWavesPerWG, int NB = kSpillBuckets, bool kS = false>
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t cbeg,
                                                           uint32_t cend, uint32_t ctail, int resume, Tables t,
                                                           LetterTables lt) {
@@ -317,7 +337,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // sc1 / sc0 sc1 instead of nt.  (Measured and removed, DESIGN.md §6: the 4
     // hottest keys counted by ballots into SGPRs; key bytes by three aligned
     // 8-byte reads; a single-choice dictionary lookup.)
-    __shared__ MapLdsT<NW, NB> L;
+    __shared__ MapLdsT<NW, NB, kS> L;
+    static_assert(!kS || (NB == kSpillBucketsHi && NW == kWavesPerWG), "staged spill: the 2048-bucket layout, 16 waves");
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the DMA operands
@@ -327,27 +348,30 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     const lds_uint4* kmask4 = (const lds_uint4*)L.kmask;
     if (t.dbg && tid == 0) t.dbg[2 * (NB + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
 
-    const bool use_dict = t.dict != nullptr;
+    const bool use_dict = !kS && t.dict != nullptr;
     // NW (waves per workgroup) < kWavesPerWG only for the occupancy benchmark (map_mode 0x1000 / 0x2000)
     constexpr uint32_t kT = NW * kWave;
-    for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kT) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
-    // chunks [cbeg, cend) of the split; resume: an earlier launch mapped chunks
-    // before cbeg (host input streamed piece by piece), so this workgroup's spill
-    // cursors and dictionary counts continue from what it wrote
-    for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kT)
-        dcnt[i] = resume && use_dict && i < (uint32_t)kDictSlots ? t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i] : 0u;
+    if constexpr (!kS) {
+        for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kT) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
+        // chunks [cbeg, cend) of the split; resume: an earlier launch mapped chunks
+        // before cbeg (host input streamed piece by piece), so this workgroup's spill
+        // cursors and dictionary counts continue from what it wrote
+        for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kT)
+            dcnt[i] = resume && use_dict && i < (uint32_t)kDictSlots ? t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i] : 0u;
+    }
     for (uint32_t b = tid; b < 2u * NB + kWave; b += kT) {
         uint32_t v = 0;
         if (resume && b < (uint32_t)NB) v = t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
         else if (resume && b < 2u * NB) v = t.sp.counts[(uint64_t)(b - NB) * t.sp.nwg + blockIdx.x];
         curs[b] = v;
+        if (kS && b < (uint32_t)NB) L.fl[b] = (uint16_t)v;  // everything before the cursor is written
     }
     if (tid == 0) L.lrec_n = resume && t.lrec ? t.lrec_cnt[blockIdx.x] : 0u;
     for (uint32_t i = tid; i < (uint32_t)kLetterUnique * 8; i += kT) L.lt2[i] = lt.l2[i];
     for (uint32_t i = tid; i < (uint32_t)kLetterLdsPages; i += kT) L.lt1[i] = lt.l1[i];
-    if (MapLdsT<NW, NB>::kB2 && tid < 64) L.lb2[tid] = lt.b2[tid];
+    if (MapLdsT<NW, NB, kS>::kB2 && tid < 64) L.lb2[tid] = lt.b2[tid];
     const LdsLetters lds_lt{(const lds_u8*)L.lt1, (const lds_u32*)L.lt2,
-                            MapLdsT<NW, NB>::kB2 ? (const lds_u32*)L.lb2 : nullptr};
+                            MapLdsT<NW, NB, kS>::kB2 ? (const lds_u32*)L.lb2 : nullptr};
     if (tid < kMaskLens * 4) {  // byte masks: dword d of kmask[len] keeps clamp(len - 4d, 0, 4) bytes
         const int nb = min(max((int)(tid >> 2) - 4 * (int)(tid & 3), 0), 4);
         ((uint32_t*)L.kmask)[tid] = nb == 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u;
@@ -392,9 +416,16 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // spill store instructions the previous iteration issued after the DMA now
     // awaited: 2 (staged appends) or kVmemWide (appends from the word slots)
     bool wide_prev = false;
-    for (uint32_t c = c0; c < cend; c += stride, cs += cstep, kf = k, k = k == kRing - 1 ? 0 : k + 1) {
+    // kS: every wave runs the workgroup's trip count (its barriers), a chunk past
+    // cend counting as empty
+    const uint32_t cw0 = cbeg + blockIdx.x * NW;
+    const uint32_t ktrips = kS && cw0 < cend ? (cend - cw0 + stride - 1) / stride : 0u;
+    uint32_t trip = 0;
+    for (uint32_t c = c0; kS ? trip < ktrips : c < cend;
+         c += stride, cs += cstep, kf = k, k = k == kRing - 1 ? 0 : k + 1, trip++) {
         // chunk c's DMA (issued two iterations ago) has landed
-        if (wide_prev) wait_vmem_iter_wide();
+        if constexpr (kS) wait_vmem_iter_staged();
+        else if (wide_prev) wait_vmem_iter_wide();
         else wait_vmem_iter();
         wide_prev = false;
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
@@ -445,6 +476,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 }
                 mA = utf8_mask16(buf, 16 * lane, lane == 0, lds_lt);
             }
+            if (kS && c >= cend) mA = 0;  // a trip past this wave's last chunk: nothing to count
             // Word starts (a letter byte whose predecessor is not one) in the owned lanes
             // and lengths (ctz over this lane's mask and the next lane's), packed into the
             // list as slot position | len << 10 (a u16: len > 16 means a long word; no
@@ -748,8 +780,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         // VMEM count stays fixed, so its DMA waits are counted)
                         const bool fit8 = pos < sub8, fit16 = pos < sub;
                         const bool put8 = valid & !big & fit8, put16 = valid & big & fit16;
-                        __builtin_amdgcn_raw_buffer_store_b64((u32x2){r.x, r.y}, rs8,
-                                                              put8 ? (__umul24(b, sub8) + pos) * 8u : kOutOfRange, 0, 0);
+                        uint32_t o8 = put8 ? (__umul24(b, sub8) + pos) * 8u : kOutOfRange;
+                        if constexpr (kS) o8 = stage_or_store(L, b, pos, ((uint64_t)r.y << 32) | r.x, o8);
+                        __builtin_amdgcn_raw_buffer_store_b64((u32x2){r.x, r.y}, rs8, o8, 0, 0);
                         __builtin_amdgcn_raw_buffer_store_b128(r, rs16, put16 ? (__umul24(b, sub) + pos) * 16u : kOutOfRange,
                                                                0, 0);
                         // (lane masks, not a per-lane bool: no 0/1 VGPR round trip)
@@ -821,9 +854,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             if (big)
                                 __builtin_amdgcn_raw_buffer_store_b128(r, rs16, valid && fit ? (__umul24(b, sub) + pos) * 16u : kOutOfRange,
                                                                        0, 0);
-                            else
-                                __builtin_amdgcn_raw_buffer_store_b64((u32x2){r.x, r.y}, rs8,
-                                                                      valid && fit ? (__umul24(b, sub8) + pos) * 8u : kOutOfRange, 0, 0);
+                            else {
+                                uint32_t o8 = valid && fit ? (__umul24(b, sub8) + pos) * 8u : kOutOfRange;
+                                if constexpr (kS) o8 = stage_or_store(L, b, pos, ((uint64_t)r.y << 32) | r.x, o8);
+                                __builtin_amdgcn_raw_buffer_store_b64((u32x2){r.x, r.y}, rs8, o8, 0, 0);
+                            }
                             const uint64_t mOver = __ballot(valid) & ~__ballot(fit);
                             if (mOver) {  // a stream is full: count in the HBM table; the bucket then merges through it
                                 if (__builtin_amdgcn_inverse_ballot_w64(mOver)) {
@@ -859,7 +894,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const uint32_t b = spill_bucket<NB>(hh[u]);
                         const uint64_t mFit8 = __ballot(pos[u] < sub8), mFit16 = __ballot(pos[u] < sub);
                         const uint64_t mPut8 = mMiss[u] & ~mBig[u] & mFit8, mPut16 = mMiss[u] & mBig[u] & mFit16;
-                        const uint32_t o8 = __builtin_amdgcn_inverse_ballot_w64(mPut8) ? (__umul24(b, sub8) + pos[u]) * 8u : kOutOfRange;
+                        uint32_t o8 = __builtin_amdgcn_inverse_ballot_w64(mPut8) ? (__umul24(b, sub8) + pos[u]) * 8u : kOutOfRange;
+                        if constexpr (kS) o8 = stage_or_store(L, b, pos[u], k0[u], o8);
                         const uint32_t o16 = __builtin_amdgcn_inverse_ballot_w64(mPut16) ? (__umul24(b, sub) + pos[u]) * 16u : kOutOfRange;
                         __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)k0[u], (uint32_t)(k0[u] >> 32)}, rs8, o8, 0, 0);
                         __builtin_amdgcn_raw_buffer_store_b128(
@@ -887,6 +923,37 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 }
             }
         }
+        if constexpr (kS) {
+            // Write-combining round: after a barrier every stream whose LDS group
+            // holds 4 records writes them as one 32-byte store (a full sector; the
+            // 2048-bucket layout's 4096 streams per workgroup otherwise leave the
+            // XCD's L2 half-written lines: 3.3x write amplification on C5), then
+            // the group restarts at the stream's cursor (records past the group
+            // were stored directly).  2 streams per thread, 4 store instructions
+            // per wave (out-of-range offsets for the rest): a fixed VMEM count.
+            __syncthreads();
+            bool rare = false;
+#pragma unroll
+            for (uint32_t q = 0; q < (uint32_t)NB / kT; q++) {
+                const uint32_t b = tid + q * kT;
+                const uint32_t cc = curs[b];
+                const uint32_t f = cc - ((cc - (uint32_t)L.fl[b]) & 0xFFFFu);
+                const bool grp = cc - f >= 4u;
+                const bool whole = grp && f + 4u <= sub8;
+                const u32x4 lo = *(const lds_uint4*)&L.stage8[b][0], hi = *(const lds_uint4*)&L.stage8[b][2];
+                const uint32_t o = (__umul24(b, sub8) + f) * 8u;
+                __builtin_amdgcn_raw_buffer_store_b128(lo, rs8, whole ? o : kOutOfRange, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(hi, rs8, whole ? o + 16u : kOutOfRange, 0, 0);
+                if (grp && !whole) {  // the group reaches past the stream's capacity: its records below it
+                    for (uint32_t j = 0; j < 4u; j++)
+                        if (f + j < sub8) t.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
+                    rare = true;
+                }
+                if (grp) L.fl[b] = (uint16_t)cc;
+            }
+            if (__ballot(rare)) wait_vmem_all();  // (other VMEM operations: the counted wait no longer holds)
+            __syncthreads();  // the groups and fl are reused by the next round's appends
+        }
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
         ds.issue<dma_policy(mode)>(lane, ring0 + kf * kSlotStride);
@@ -902,6 +969,14 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
 
     __syncthreads();
+    if constexpr (kS) {  // the streams' last partial groups
+        for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {
+            const uint32_t cc = curs[b];
+            const uint32_t f = cc - ((cc - (uint32_t)L.fl[b]) & 0xFFFFu);
+            for (uint32_t j = 0; f + j < cc; j++)
+                if (f + j < sub8) t.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
+        }
+    }
     if (tid == 0 && t.lrec) t.lrec_cnt[blockIdx.x] = L.lrec_n;
     unsigned long long spilled = 0, hits = 0;
     for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {  // (this launch's share: minus the resumed values)
@@ -2012,7 +2087,10 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     return true;
 #endif
     if (t.sp.nb == kSpillBucketsHi) {  // high-cardinality layout (ablation modes apply to the default one only)
-        wc_map_kernel<0, 12, kSpillBucketsHi><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
+        if (t.hi_staged && !t.dict)  // no dictionary: its LDS write-combines the 8-byte spill streams
+            wc_map_kernel<0, kWavesPerWG, kSpillBucketsHi, true><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
+        else
+            wc_map_kernel<0, 12, kSpillBucketsHi><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
         return true;
     }
     if (t.sp.nb == kSpillBucketsLo) {  // the default layout (ablation modes: mapprobe.py)

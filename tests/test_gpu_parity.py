@@ -198,14 +198,16 @@ def test_wc_bucket_aggregator_overflow(ctx, rounds, big):
         ctx.set_option("agg_big_later", 0)
 
 
-@pytest.mark.parametrize("rounds", [0, 1])
-def test_wc_high_cardinality_buckets(ctx, rounds):
+@pytest.mark.parametrize("rounds,stage", [(0, -1), (1, -1), (0, 1), (1, 1)])
+def test_wc_high_cardinality_buckets(ctx, rounds, stage):
     """2048 spill buckets (high-cardinality layout: 12-wave map workgroups, 4x
-    the aggregator workgroups), forced and chosen by the feedback rule: exact
-    on a 3M-word vocabulary, in rounds or with every miss counted in HBM."""
+    the aggregator workgroups; stage 1: no dictionary, 16-wave workgroups
+    write-combining the 8-byte streams in LDS), forced and chosen by the feedback
+    rule: exact on a 3M-word vocabulary, in rounds or with every miss counted in HBM."""
     voc = C.Vocab(C.KIND_ASCII, 1.07, 3_000_000, 16)
     files = [bytes(voc.fill_files([26_000_000], [16], C.wc_params(vocab_lo=0, vocab_hi=3_000_000))[0])]
     ctx.set_option("agg_rounds", rounds)
+    ctx.set_option("hi_stage", stage)
     ctx.set_option("spill_buckets", 2048)
     try:
         check(ctx, "wc", files, nreduces=(10,))
@@ -224,6 +226,42 @@ def test_wc_high_cardinality_buckets(ctx, rounds):
         ctx.set_option("agg_rounds", 0)
         ctx.set_option("spill_buckets", 0)
         ctx.set_option("spill_hi_keys", 0)
+        ctx.set_option("hi_stage", 0)
+
+
+@pytest.mark.parametrize("case", ["tiny_streams", "host_pieces", "utf8_long"])
+def test_wc_staged_spill(ctx_dict, case):
+    """The write-combined 2048-bucket map (hi_stage): every 8-byte spill record
+    goes through a stream's 4-record LDS group or straight to memory, and the
+    groups are flushed after each workgroup round and at the end.  Tiny streams
+    (groups reaching past a stream's capacity, the rest through the HBM table),
+    host input mapped piece by piece (resumed launches: cursors and groups carry
+    over), and mixed-script text with long words; all exact, with the dictionary
+    option on (the staged kernel has none: the split is mapped without it)."""
+    c = ctx_dict
+    c.set_option("spill_buckets", 2048)
+    c.set_option("hi_stage", 1)
+    try:
+        if case == "tiny_streams":
+            files = cases.synthetic(C.KIND_ASCII, 1_000_000, [6_000_000], 15)
+            c.set_option("spill_stream_keys", 6)
+            check(c, "wc", files, nreduces=(10,))
+            assert c.stats()["spill_ovf"] > 0
+        elif case == "host_pieces":
+            files = cases.synthetic(C.KIND_ASCII, 500_000, [9_000_001, 8_000_000, 7_000_003], 73)
+            joined = b"\n".join(files)
+            c.set_option("ingest_piece", 1 << 20)
+            c.set_option("ingest_min", 1 << 20)
+            assert c.run_job(MRG_APP_WC, joined, nreduce=10) == O.c_partitioned("wc", files, 10)
+            assert c.stats()["staged_bytes"] == len(joined)
+        else:
+            files = cases.synthetic(C.KIND_UTF8, 300_000, [5_000_000, 3_000_001], 74, 0.0005) + \
+                [cases.long_words(2_000_000, 3)]
+            check(c, "wc", files, nreduces=(1, 10))
+        assert c.stats()["spill_buckets"] == 2048 and c.stats()["dict_hits"] == 0
+    finally:
+        for k in ("spill_buckets", "hi_stage", "spill_stream_keys", "ingest_piece", "ingest_min"):
+            c.set_option(k, 0)
 
 
 @pytest.mark.parametrize("digit_bits,fold,grep_k1,compact,own",
