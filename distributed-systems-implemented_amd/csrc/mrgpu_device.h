@@ -375,6 +375,57 @@ __device__ __forceinline__ uint32_t utf8_mask16(const lds_u8* slot, uint32_t q0,
     return m;
 }
 
+// Wave-compacted utf8_mask16 for the whole 1 KiB window (lane l: slot bytes
+// [16 l, 16 l + 16)).  The serial loop above runs as many turns as the lane
+// with the most leads (a lane of Greek or Cyrillic text has 8), the others
+// idle; here every lead of the window is listed once, by the lane holding it
+// (prefix scan of the lanes' counts), and the list is decoded one lead per lane
+// per pass; a letter rune ORs its bits into its lane's mask word in LDS, and
+// into the next lane's when it runs past the lane's 16 bytes.  scratch: 1 KiB
+// of LDS free during the call (leads as u16 at [0, 768), the 64 masks at
+// [768, 1024)); more than 384 leads: the serial loop.  Wave-uniform call.
+constexpr uint32_t kWaveLeads = 384;
+__device__ __forceinline__ uint32_t utf8_mask16_wave(const lds_u8* slot, uint32_t lane, lds_u8* scratch, LdsLetters L) {
+    const uint32_t q0 = 16 * lane;
+    const lds_u32* s4 = (const lds_u32*)(slot + q0);
+    const uint32_t w1 = s4[0], w2 = s4[1], w3 = s4[2], w4 = s4[3];
+    const uint32_t m = flags_to_bits16(ascii_flags4_any(w1), ascii_flags4_any(w2), ascii_flags4_any(w3), ascii_flags4_any(w4));
+    uint32_t own = flags_to_bits16(lead_flags4(w1), lead_flags4(w2), lead_flags4(w3), lead_flags4(w4));
+    const uint32_t nown = __popc(own);
+    const uint32_t incl = wave_incl_scan_dpp(nown);
+    const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
+    if (total > kWaveLeads) return utf8_mask16(slot, q0, lane == 0, L);
+    lds_u16* lst = (lds_u16*)scratch;
+    lds_u32* M = (lds_u32*)(scratch + 2 * kWaveLeads);
+    M[lane] = 0u;
+    uint32_t j = incl - nown;
+    while (own) {  // two leads per turn
+        const uint32_t b1 = __builtin_ctz(own);
+        own &= own - 1;
+        lst[j] = (uint16_t)(q0 + b1);
+        if (own) lst[j + 1] = (uint16_t)(q0 + __builtin_ctz(own));
+        own &= own - 1;
+        j += 2;
+    }
+    wave_sync();
+    for (uint32_t p = 0; p < total; p += 64) {
+        if (p + lane < total) {
+            const uint32_t e = lst[p + lane];
+            const LeadRune r = lead_decode(*(const lds_u32_unaligned*)(slot + e));
+            const uint32_t tw = lead_word(r, L);
+            if (r.valid && ((tw >> (r.cp & 31u)) & 1u)) {
+                const uint32_t bits = ((2u << r.need) - 1u) << (e & 15u);  // up to bit 18
+                const uint32_t ow = e >> 4;
+                __hip_atomic_fetch_or(&M[ow], bits & 0xFFFFu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if ((bits >> 16) != 0u && ow < 63u)
+                    __hip_atomic_fetch_or(&M[ow + 1], bits >> 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+    }
+    wave_sync();
+    return m | M[lane];
+}
+
 // 32-bit mix of a <= 16-byte key given as four little-endian words.
 __device__ __forceinline__ uint32_t fold32(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3) {
     // (three-input xor as one v_bitop3_b32, truth table 0x96; same value as the plain xors)

@@ -315,6 +315,11 @@ constexpr uint32_t kLongReserve = 256;
 #define MRG_STAGE2_DRAIN 1
 #endif
 constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
+// UTF-8 chunks: leads decoded wave-compacted (utf8_mask16_wave) or by the
+// per-lane loop (utf8_mask16)
+#ifndef MRG_UTF8_WAVE
+#define MRG_UTF8_WAVE 0
+#endif
 __device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint32_t lleft, uint32_t lane) {
     for (uint32_t g = 0; g < lleft; g += kWave)
         if (g + lane < lleft && lbase + g + lane < t.list_cap) t.list[lbase + g + lane] = kListHole;
@@ -474,7 +479,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     wait_vmem_all();
                     wave_sync();
                 }
+#if MRG_UTF8_WAVE
+                mA = utf8_mask16_wave(buf, lane, (lds_u8*)L.ring[wv][kf], lds_lt);
+#else
                 mA = utf8_mask16(buf, 16 * lane, lane == 0, lds_lt);
+#endif
             }
             if (kS && c >= cend) mA = 0;  // a trip past this wave's last chunk: nothing to count
             // Word starts (a letter byte whose predecessor is not one) in the owned lanes
