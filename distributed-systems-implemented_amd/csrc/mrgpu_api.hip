@@ -248,6 +248,7 @@ struct mrg_ctx {
     int agg_big0 = 0;
     bool agg_big_later = true;
     double spill_scale = 1.0;           // spill stream capacity factor (from the dictionary sample's miss rate)
+    double words_per_byte = 0.0;        // words per input byte of the previous wc split (no-dictionary spill sizing)
     bool debug_times = getenv("MRG_DEBUG_TIMES") != nullptr;
     uint64_t rec_cap = 1u << 21;       // record output buffer capacity (grows on overflow)
     bool sh_clean = false;             // ShortTable known to be empty (skip its clear)
@@ -894,6 +895,12 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         ingest_finish(c, ing);
         return rc;
     }
+    // without a dictionary (the staged 2048-bucket map) every word spills: the
+    // streams are sized for the previous split's words per byte, 30 % over
+    if (staged && c->words_per_byte > 0) {
+        const double need = 1.3 * c->words_per_byte / (2.0 * 0.75 / 16.0);
+        if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
+    }
     // the sample may have raised spill_scale: size the streams for this split now,
     // not only from the next call on (overflowing streams merge through HBM: slow)
     if ((rc = ensure_spill(c, len))) {
@@ -966,6 +973,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             h = *c->h_ctr;
         }
         c->arena_hint = h.long_bytes + h.long_bytes / 4;
+        if (len) c->words_per_byte = (double)(h.dict_hits + h.spilled + h.spill_ovf) / (double)len;
         if (h.status & kStLrecFull) {  // a record region filled up: size them for this split's busiest workgroup
             std::vector<uint32_t> cnt(nwg);
             HCHK(c, hipMemcpy(cnt.data(), c->lrec_cnt.p, (size_t)nwg * 4, hipMemcpyDeviceToHost));
