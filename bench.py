@@ -458,7 +458,7 @@ def main():
     ap.add_argument("--no-oracle", action="store_true", help="skip the full-size exact check against the C oracle")
     ap.add_argument("--scaling-workload", default="c5", help="N > 1: workload of the E(P) sub-run ('none' to skip)")
     ap.add_argument("--scaling-steps", type=int, default=2)
-    ap.add_argument("--no-pipelined", action="store_true", help="N > 1: skip the pipelined-jobs measurement")
+    ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined-jobs measurement")
     ap.add_argument("--splits", type=int, default=0,
                     help="distinct splits resident per rank, rotated over the timed steps (0: 3 at N=1, 2 at N>1)")
     ap.add_argument("--scaling-splits", type=int, default=2, help="resident splits per rank in the E(P) sub-run")
@@ -549,7 +549,7 @@ def main():
     # transfer overlaps the next job's map, as a worker's successive map tasks
     # can), reported beside the serial steps above (`value` stays serial)
     pipelined = None
-    if world == 1 or not args.no_pipelined:
+    if not args.no_pipelined:
         def run_async(sp):
             if grep:
                 ctx.run_job_async(MRG_APP_GREP, pattern=PATTERN, device_ptr=dptrs[sp], nbytes=nbytes,

@@ -118,8 +118,9 @@ def load_library(path: str | None = None):
     L.mrg_reduce_all.argtypes = [vp, vp, POINTER(vp), POINTER(c_size_t), POINTER(c_uint64)]
     L.mrg_run_job.argtypes = [vp, c_int, vp, c_size_t, c_int, vp, c_size_t, c_uint32, POINTER(vp),
                               POINTER(c_size_t), POINTER(c_uint64)]
-    L.mrg_run_job_async.argtypes = [vp, c_int, vp, c_size_t, c_int, vp, c_size_t, c_uint32]
-    L.mrg_job_wait.argtypes = [vp, POINTER(vp), POINTER(c_size_t), POINTER(c_uint64)]
+    if hasattr(L, "mrg_run_job_async"):  # (A/B builds of earlier commits lack it)
+        L.mrg_run_job_async.argtypes = [vp, c_int, vp, c_size_t, c_int, vp, c_size_t, c_uint32]
+        L.mrg_job_wait.argtypes = [vp, POINTER(vp), POINTER(c_size_t), POINTER(c_uint64)]
     L.mrg_comm_unique_id.argtypes = [POINTER(c_uint8)]
     L.mrg_comm_init.argtypes = [vp, POINTER(c_uint8), c_int, c_int]
     L.mrg_exchange.argtypes = [vp, vp, POINTER(vp)]
@@ -329,7 +330,8 @@ class Context:
 
     def job_wait(self, copy_out: bool = True):
         """The oldest queued job's output: list of mr-out-r bytes (or (ptr, n, offsets))."""
-        nreduce = self._async_nreduce.pop(0)
+        queued = getattr(self, "_async_nreduce", [])
+        nreduce = queued.pop(0) if queued else 1  # (none queued: the library reports the error)
         p, n = c_void_p(), c_size_t()
         offs = (c_uint64 * (nreduce + 1))()
         self._check(self.L.mrg_job_wait(self.h, byref(p), byref(n), offs), "mrg_job_wait")

@@ -11,7 +11,7 @@ for w in $wls; do
 for v in "$@"; do
   extra=""
   [ $w = c5 ] && extra="--files 40 --steps 3 --warmup 2"
-  MRGPU_LIB=$L/libmrgpu_$v.so timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --no-pcie --no-oracle --splits 2 $extra > $out/${w}_${v}_$i.json 2> $out/${w}_${v}_$i.err
+  MRGPU_LIB=$L/libmrgpu_$v.so timeout -k 10 300 python bench.py --workload $w --no-cpu-baseline --no-pcie --no-oracle --no-pipelined --splits 2 $extra > $out/${w}_${v}_$i.json 2> $out/${w}_${v}_$i.err
   python -c "import json;d=json.load(open('$out/${w}_${v}_$i.json'));print('$w $v $i',d['value'],'map',d['phases_ms']['map_kernel'],'agg',d['phases_ms']['agg'],d['checks'].get('total_words_match'))"
 done
 done
