@@ -372,9 +372,11 @@ __global__ void __launch_bounds__(kScanThreads) flag_positions_kernel(const uint
 }
 
 // Insertion sort of each tied run by full bytewise comparison.  A run longer
-// than max_run is left alone, its members marked in `lng` and flags[3] set: the
-// caller then sorts with the k1 pass (16-byte prefixes), or merge-sorts the
-// marked members by full comparison (sort_long_runs).
+// than max_run is left alone and flags[3] set; its first max_run + 1 members are
+// marked in `lng` here (bounded work per thread), the rest by
+// mark_long_tail_kernel.  The caller then sorts with the k1 pass (16-byte
+// prefixes), or merge-sorts the marked members by full comparison
+// (sort_long_runs).
 __global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_t* tie, uint64_t max_run,
                                 unsigned long long* flags, uint8_t* lng) {
     uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -384,8 +386,7 @@ __global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_
         while (e < n && tie[e] && e - i <= max_run) e++;
         if (e - i > max_run) {
             if (flags[3] == 0) atomicOr(&flags[3], 1ull);
-            lng[i] = 1;
-            for (uint64_t a = i + 1; a < n && tie[a]; a++) lng[a] = 1;
+            for (uint64_t a = i; a < e; a++) lng[a] = 1;  // e = i + max_run + 1 here
             continue;
         }
         for (uint64_t a = i + 1; a < e; a++) {
@@ -396,6 +397,50 @@ __global__ void fix_ties_kernel(Recs r, uint32_t* perm, uint64_t n, const uint8_
                 b--;
             }
             perm[b] = v;
+        }
+    }
+}
+
+// The members of fix_ties_kernel's long runs (max_run = kTailWindow) past the
+// first kTailWindow + 1: position a is one iff tie[a - 63 .. a] are all set (its
+// run then started at a - 64 or earlier, so it is longer than 64).  One thread
+// per 64 positions: the tie bytes of [b - 64, b + 64) folded into a 128-bit
+// mask, runs of 64 set bits found by shift-and doubling.
+constexpr uint32_t kTailWindow = 64;
+__device__ __forceinline__ uint64_t tie_bits8(const uint8_t* tie, int64_t p, uint64_t n) {
+    if (p < 0) return 0;
+    uint64_t w;
+    if ((uint64_t)p + 8 <= n) {
+        w = *(const uint64_t*)(tie + p);
+    } else {
+        w = 0;
+        for (uint64_t q = 0; q < 8 && (uint64_t)p + q < n; q++) w |= (uint64_t)tie[p + q] << (8 * q);
+    }
+    // byte q != 0 -> bit q
+    w = (w | (w >> 4)) & 0x0F0F0F0F0F0F0F0Full;
+    w = (w | (w >> 2)) & 0x0303030303030303ull;
+    w = (w | (w >> 1)) & 0x0101010101010101ull;
+    return (w * 0x0102040810204080ull) >> 56;
+}
+__global__ void mark_long_tail_kernel(const uint8_t* tie, uint64_t n, uint8_t* lng) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t * 64 < n; t += stride) {
+        const int64_t b = (int64_t)(t * 64);
+        uint64_t lo = 0, hi = 0;
+        for (int q = 0; q < 8; q++) {
+            lo |= tie_bits8(tie, b - 64 + 8 * q, n) << (8 * q);
+            hi |= tie_bits8(tie, b + 8 * q, n) << (8 * q);
+        }
+        // x &= x << k over the 128-bit (hi:lo), k = 1, 2, ..., 32: bit p stays set
+        // iff bits p - 63 .. p are all set
+        for (int k = 1; k < 64; k <<= 1) {
+            hi &= (hi << k) | (lo >> (64 - k));
+            lo &= lo << k;
+        }
+        for (int q = 0; q < 8 && hi; q++, hi >>= 8) {
+            const uint64_t p = (uint64_t)b + 8 * q;
+            for (int j = 0; j < 8; j++)
+                if (((hi >> j) & 1) && p + j < n) lng[p + j] = 1;
         }
     }
 }
@@ -1063,10 +1108,12 @@ __device__ __forceinline__ int tied_cmp(const Recs& r, const uint64_t* ea, uint3
 // start a (partition, prefix) group; cnt[0]'s low half = how many): the wave
 // ranks each run of 2-64 keys among them in turn — a key per lane, the other
 // members' words broadcast by readlane — and lists runs of 65-kMidRun keys in
-// `mid` (cnt[2]); longer runs are marked in lng and flag flags[3].
+// `mid` (cnt[2]); longer runs are listed as kLongChunk-key pieces in `lchunk`
+// (cnt[3], marked in lng by mark_chunks_kernel) and flag flags[3].
+constexpr uint32_t kLongChunk = 4096;
 __global__ void __launch_bounds__(256) rank_small_runs_kernel(Recs r, const uint64_t* ext, uint32_t* perm,
                                                               const uint32_t* bpos, uint64_t n, uint2* mid,
-                                                              unsigned long long* cnt, uint8_t* lng,
+                                                              uint2* lchunk, unsigned long long* cnt,
                                                               unsigned long long* flags) {
     const uint64_t nb = *(const uint32_t*)cnt;
     const uint32_t lane = threadIdx.x & 63;
@@ -1080,7 +1127,10 @@ __global__ void __launch_bounds__(256) rank_small_runs_kernel(Recs r, const uint
         }
         if (bk > kSmallRun && bk <= kMidRun) mid[atomicAdd(cnt + 2, 1ull)] = make_uint2(bs, bk);
         if (bk > kMidRun) {
-            for (uint32_t a = 0; a < bk; a++) lng[bs + a] = 1;
+            const uint32_t pieces = (bk + kLongChunk - 1) / kLongChunk;
+            const uint64_t at = atomicAdd(cnt + 3, (unsigned long long)pieces);
+            for (uint32_t q = 0; q < pieces; q++)
+                lchunk[at + q] = make_uint2(bs + q * kLongChunk, std::min(kLongChunk, bk - q * kLongChunk));
             atomicOr(&flags[3], 1ull);
         }
         uint64_t todo = __ballot(bk >= 2 && bk <= kSmallRun);
@@ -1107,6 +1157,16 @@ __global__ void __launch_bounds__(256) rank_small_runs_kernel(Recs r, const uint
             }
             if (have) perm[s + rank] = rec;
         }
+    }
+}
+
+// The long runs' members, a listed piece per workgroup iteration.
+__global__ void __launch_bounds__(256) mark_chunks_kernel(const uint2* lchunk, const unsigned long long* cnt,
+                                                          uint8_t* lng) {
+    const uint64_t np = cnt[3];
+    for (uint64_t c = blockIdx.x; c < np; c += gridDim.x) {
+        const uint2 sk = lchunk[c];
+        for (uint32_t a = threadIdx.x; a < sk.y; a += blockDim.x) lng[(uint64_t)sk.x + a] = 1;
     }
 }
 
@@ -1187,9 +1247,11 @@ __global__ void __launch_bounds__(1024) rank_mid_runs_kernel(Recs r, const uint6
 // caller reads the flag and merge-sorts them (sort_long_runs).
 static int rank_tied_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t n, uint8_t* tie, uint8_t* lng,
                           const uint64_t* ext, unsigned long long* flags, hipStream_t s) {
-    RCHK(ws->runs.ensure(64 + (n / kSmallRun + 2) * 8));
+    const uint64_t nmid = n / kSmallRun + 2, nlong = n / kLongChunk + n / (kMidRun + 1) + 2;
+    RCHK(ws->runs.ensure(64 + (nmid + nlong) * 8));
     unsigned long long* cnt = ws->runs.as<unsigned long long>();
     uint2* mid = (uint2*)(cnt + 8);
+    uint2* lchunk = mid + nmid;
     uint32_t* d_nb = (uint32_t*)cnt;  // cnt[0]'s low half
     uint32_t* bpos = ws->key_b.as<uint32_t>();
     RCHK(hipMemsetAsync(cnt, 0, 64, s));
@@ -1206,7 +1268,8 @@ static int rank_tied_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
         (void)hipEventRecord(ev[0], s);
     }
     const unsigned g = (unsigned)std::min<uint64_t>((n / 64 + 4) / 4 + 1, 2048);  // 4 waves per block
-    rank_small_runs_kernel<<<g, 256, 0, s>>>(r, ext, perm, bpos, n, mid, cnt, lng, flags);
+    rank_small_runs_kernel<<<g, 256, 0, s>>>(r, ext, perm, bpos, n, mid, lchunk, cnt, flags);
+    mark_chunks_kernel<<<1024, 256, 0, s>>>(lchunk, cnt, lng);
     if (dbg) (void)hipEventRecord(ev[1], s);
     rank_mid_runs_kernel<<<256, 1024, 0, s>>>(r, ext, perm, mid, cnt);
     if (dbg) {
@@ -1367,7 +1430,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     // Tied runs of up to kMaxRun are insertion-sorted in place (one thread per
     // run); longer ones are marked.  Returns whether any run was long; with
     // `merge`, the long runs are then merge-sorted by full comparison.
-    constexpr uint64_t kMaxRun = 64;
+    constexpr uint64_t kMaxRun = kTailWindow;  // mark_long_tail_kernel's window
     auto fix_ties = [&](bool with_k1, bool merge, bool* any_long, bool all_runs = false) -> int {
         uint8_t* tie = ws->key_a.as<uint8_t>();
         uint8_t* lng = tie + n;
@@ -1384,6 +1447,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
             return *any_long ? sort_long_runs(ws, r, pa, n, lng, ext, s) : 0;
         }
         fix_ties_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, tie, kMaxRun, flags, lng);
+        if (merge) mark_long_tail_kernel<<<grid_for((n + 63) / 64), 256, 0, s>>>(tie, n, lng);
         RCHK(hipMemcpyAsync(ws->h_pinned + 1, flags + 1, 24, hipMemcpyDeviceToHost, s));  // flags 1-3
         RCHK(hipStreamSynchronize(s));
         *any_long = ws->h_pinned[3] != 0;

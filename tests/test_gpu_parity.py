@@ -330,6 +330,33 @@ def test_grep_tied_runs(ctx, tie_rank):
         ctx.set_option("tie_rank", 1)
 
 
+@pytest.mark.parametrize("tie_rank", [1, 0])
+def test_grep_log_prefix_runs(ctx, tie_rank):
+    """Log-like grep input: 150 000 matching lines behind one 24-byte timestamp
+    prefix (one tied run of 150 000 at nReduce=1: listed as 4096-key pieces and
+    merge-sorted), plus 20 000 behind another and runs just over and under the
+    2048-key mid-run limit; and wc over 3 000 distinct 40-letter words sharing
+    their first 32 letters (a tied run far over 64 keys after the 16-byte key
+    pass: its members past the first 65 marked by the 64-wide window kernel)."""
+    rnd = np.random.default_rng(23)
+    lines = []
+    for pre, k in ((b"2026-10-17T08:00:00 INFO distributed", 150_000), (b"2026-10-17T08:00:01 WARN distributed", 20_000),
+                   (b"2026-10-17T08:00:02 INFO distributed", 2049), (b"2026-10-17T08:00:03 INFO distributed", 2048)):
+        ids = rnd.permutation(k * 4)[:k]
+        lines += [pre + b" req=%07d" % i for i in ids]
+    rnd.shuffle(lines)
+    text = b"\n".join(lines) + b"\n"
+    ctx.set_option("tie_rank", tie_rank)
+    try:
+        check(ctx, "grep:distributed", [text], nreduces=(1, 7))
+    finally:
+        ctx.set_option("tie_rank", 1)
+    base = b"q" * 32
+    words = sorted({base + bytes(rnd.integers(97, 123, size=8).astype(np.uint8)) for _ in range(3000)})
+    rnd.shuffle(words)
+    check(ctx, "wc", [b" ".join(words * 2) + b"\n"], nreduces=(1,))
+
+
 @pytest.mark.parametrize("own", [1, 0])
 @pytest.mark.parametrize("kind,bits", [("u32", 32), ("u32", 4), ("u32", 20), ("u64", 64), ("u64", 60), ("u64", 12),
                                        ("u64keys", 34), ("u64keys", 64)])
