@@ -397,7 +397,7 @@ def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: 
     devs = []
     t0 = time.time()
     for sp in range(nsplits):
-        host = gen_corpus(w, rank, w["file_mb"], w["files"], sp)
+        host = gen_corpus(w, rank, w["file_mb"], args.scaling_files or w["files"], sp)
         devs.append(upload(host, local))
         del host
     nbytes = int(devs[0].numel())
@@ -458,6 +458,8 @@ def main():
     ap.add_argument("--no-oracle", action="store_true", help="skip the full-size exact check against the C oracle")
     ap.add_argument("--scaling-workload", default="c5", help="N > 1: workload of the E(P) sub-run ('none' to skip)")
     ap.add_argument("--scaling-steps", type=int, default=2)
+    ap.add_argument("--scaling-files", type=int, default=None,
+                    help="override the E(P) workload's file count (rehearsals: ranks sharing one device's HBM)")
     ap.add_argument("--no-pipelined", action="store_true", help="skip the pipelined-jobs measurement")
     ap.add_argument("--splits", type=int, default=0,
                     help="distinct splits resident per rank, rotated over the timed steps (0: 3 at N=1, 2 at N>1)")

@@ -255,6 +255,7 @@ struct mrg_ctx {
     int dict_mode = 0;                 // <0: never build the hot-key dictionary
     bool dict_warm = true;             // level-1 dictionary = the previous map task's (see build_dict)
     bool dict_valid = false;           // c->dict holds a dictionary built by an earlier call
+    bool dict_mini = false;            // c->dict's geometry: DictMini (staged 2048-bucket map) or DictFull
     // Dictionary reuse: the previous split's dictionary is kept (no rebuild) when
     // it hits this split's sample at >= dict_keep x the fraction it hit on the
     // split it was built for (dict_frac_built, measured on that split's map).
@@ -640,6 +641,7 @@ static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win
     t.out = rec_view(c);
     t.out_cap = c->rec_cap;
     t.dict = with_dict ? (const uint4*)c->dict.p : nullptr;
+    t.hi_staged = with_dict && c->dict_mini ? 1u : 0u;  // (a mini image is built only for 2048-bucket splits)
     clear_for_run(c, t);
     // the spill layout was sized for the split's workgroup count (ensure_spill): never launch more
     const uint32_t g = wc_map_grid(sn, (int)c->spill_nwg);
@@ -658,8 +660,9 @@ static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win
     return MRG_OK;
 }
 
-// Dictionary image from the nrec records in the record buffer (descending count).
-static int dict_from_recs(mrg_ctx* c, uint64_t nrec) {
+// Dictionary image from the nrec records in the record buffer (descending count),
+// in the mini geometry (DictMini) or the full one.
+static int dict_from_recs(mrg_ctx* c, uint64_t nrec, bool mini) {
     const uint64_t cand_bytes = 4ull * kDictSlots * sizeof(uint4);
     HCHK(c, c->sortbuf.ensure(nrec * 16 + cand_bytes + 64));
     uint4* cand = (uint4*)c->sortbuf.p;
@@ -672,12 +675,16 @@ static int dict_from_recs(mrg_ctx* c, uint64_t nrec) {
     launch_dict_keys(r, keys, idx, c->s);
     if (sort_u32_pairs(c->rws, keys, keys2, idx, idx2, nrec, 16, c->s))
         return fail(c, MRG_EDEVICE, "dictionary sort failed");
-    launch_dict_build(r, idx2, nrec, cand, (uint4*)c->dict.p, c->s);
+    launch_dict_build(r, idx2, nrec, cand, (uint4*)c->dict.p, mini, c->s);
     HCHK(c, hipGetLastError());
+    c->dict_mini = mini;
     return MRG_OK;
 }
 
-static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables lt, bool* have,
+// mini: the final image in the mini geometry (the staged 2048-bucket map); the
+// sample passes map with whatever geometry c->dict has (the level-1 image is
+// always full).
+static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables lt, bool* have, bool mini,
                       const uint8_t* host = nullptr) {
     *have = false;
     uint64_t win = 256u << 10;
@@ -692,13 +699,13 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
     // task) maps the full sample with that one instead of first building a
     // level-1 dictionary from a small sample.  The final dictionary still comes
     // from this split's own sample; only speed depends on either.
-    const bool warm = c->dict_warm && c->dict_valid && target > small;
+    const bool warm = c->dict_warm && c->dict_valid && target > small && c->dict_mini == mini;
     if (!warm) {
         if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, small / win), lt, false, &nrec, nullptr,
                               host)))
             return rc;
         if (nrec == 0) return MRG_OK;
-        if ((rc = dict_from_recs(c, nrec))) return rc;
+        if ((rc = dict_from_recs(c, nrec, target > small ? false : mini))) return rc;
     }
     c->dict_fresh = true;
     if (target > small) {
@@ -710,7 +717,7 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
         // hit its own split is kept: the candidate sort and placement are skipped
         const bool keep = warm && c->dict_keep > 0 && c->dict_frac_built > 0 && frac >= c->dict_keep * c->dict_frac_built;
         c->dict_fresh = !keep;
-        if (!keep && nrec && (rc = dict_from_recs(c, nrec))) return rc;
+        if (!keep && nrec && (rc = dict_from_recs(c, nrec, mini))) return rc;
         // Spill streams hold 0.094 8-byte records per input byte at scale 1 (C2
         // spills 0.04).  A split whose sample misses its (first-level) dictionary
         // more often gets proportionally longer streams, 30 % over the estimate
@@ -890,13 +897,14 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
     HCHK(c, c->dict_cnt.ensure((size_t)nwg * kDictSlots * sizeof(uint32_t)));
     HCHK(c, hipEventRecord(c->ev[9], c->s));
     bool have_dict = false;
-    const bool staged = c->spill_nb == kSpillBucketsHi && c->hi_stage;  // (its kernel has no dictionary)
-    if (!staged && c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict, host))) {
+    const bool staged = c->spill_nb == kSpillBucketsHi && c->hi_stage;  // (its kernel has the mini dictionary)
+    if (c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict, staged, host))) {
         ingest_finish(c, ing);
         return rc;
     }
-    // without a dictionary (the staged 2048-bucket map) every word spills: the
-    // streams are sized for the previous split's words per byte, 30 % over
+    // the staged 2048-bucket map's mini dictionary takes few of the words (the
+    // sample's spill rate was measured with a full one): its streams are sized
+    // as if every word spilled, from the previous split's words per byte, 30 % over
     if (staged && c->words_per_byte > 0) {
         const double need = 1.3 * c->words_per_byte / (2.0 * 0.75 / 16.0);
         if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace mrg {
 
 constexpr uint64_t kUnwritten = ~0ull;
@@ -121,6 +123,17 @@ constexpr int kDictShortSets = 4096;
 constexpr int kDictMidSets = 256;
 constexpr int kDictSets = kDictShortSets + kDictMidSets;
 constexpr int kDictSlots = 2 * kDictSets;
+// Dictionary geometry: DictFull above; DictMini (1024 short + 64 mid keys) for
+// the write-combined 2048-bucket map, whose LDS holds the spill groups instead.
+// The mini table takes the hottest keys only: enough to lift the few hot words
+// of a high-cardinality split off their buckets' streams.
+template <int SS, int MS>
+struct DictGeo {
+    static constexpr int kShort = SS, kMid = MS, kSets = SS + MS, kSlots = 2 * (SS + MS);
+    static_assert((SS & (SS - 1)) == 0 && (MS & (MS - 1)) == 0 && SS <= 4096 && MS <= 4096, "set index = hash bits");
+};
+using DictFull = DictGeo<kDictShortSets, kDictMidSets>;
+using DictMini = DictGeo<512, 64>;
 
 struct Recs {
     uint64_t* k0;
@@ -202,12 +215,12 @@ void launch_wc_agg(const Tables& t, int mode, int emit, bool big, hipStream_t s)
 // stream counts; off8[E] / off16[E] (E = nb * kAggSegs) are the totals.
 // tmp: 2 * E u32 of scratch.
 void launch_seg_layout(const Tables& t, uint32_t* tmp, uint64_t* off8, uint64_t* off16, hipStream_t s);
-void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s);
+void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s);  // geometry: DictMini iff t.hi_staged
 // Gather `nwin` windows of `win` bytes (stride `stride`) of in[0,n) into dst, each followed by '\n'.
 void launch_sample_gather(const uint8_t* in, uint64_t n, uint64_t win, uint64_t stride, uint32_t nwin, uint8_t* dst,
                           hipStream_t s);
 // Build the dictionary image from sample records ordered by descending count.
-void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s);
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, bool mini, hipStream_t s);
 // Sort keys for the dictionary build: ~count (u32) of each record.
 void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t s);
 // nlist = ~0: the list length is read on the device (ctr->nlist; nothing to do if 0)

@@ -63,15 +63,16 @@ static_assert(kListCap * 2 <= kSlotBytes, "the word list lives in the free slot"
 // base); the dictionary's set offsets are then constant-displaced, which the
 // ds_read offset field absorbs.
 constexpr int kMaskLens = 32;  // kmask[len], len = 0..31 (> 16 = "more than 16 bytes", never used as a key)
-// kS (high-cardinality splits without a dictionary): the 8-byte spill records
-// are write-combined in LDS, 4 per stream (stage8), and leave as 32-byte writes
-// (see the map kernel); the dictionary's LDS holds them instead.
+// kS (high-cardinality splits): the 8-byte spill records are write-combined in
+// LDS, 4 per stream (stage8), and leave as 32-byte writes (see the map kernel);
+// the dictionary is then the mini geometry (DictMini), its LDS holds them.
 template <int NW, int NB, bool kS = false>
 struct alignas(16) MapLdsT {
+    using Geo = std::conditional_t<kS, DictMini, DictFull>;
     uint4 kmask[kMaskLens];                     // kmask[len]: the first min(len, 16) of 16 key bytes
-    uint4 dset[kS ? 1 : kDictSets];             // dictionary image
+    uint4 dset[Geo::kSets];                     // dictionary image
     uint8_t ring[NW][kRing][kSlotStride];
-    uint32_t dcnt[kS ? 1 : kDictSlots + kWave]; // dictionary counts of this workgroup (+ per-lane miss dummies)
+    uint32_t dcnt[Geo::kSlots + kWave];         // dictionary counts of this workgroup (+ per-lane miss dummies)
     unsigned long long stage8[kS ? NB : 0][4];  // kS: the records of each 8-byte stream not yet written
     uint16_t fl[kS ? NB : 0];                   // kS: stream position of stage8[b][0] (low 16 bits)
     // spill cursors: [0, NB) 8-byte streams, [NB, 2 NB) 16-byte streams, then per-lane dummies for hits
@@ -105,12 +106,13 @@ __device__ __forceinline__ uint32_t lds_addr(const void* p) {
 // The two candidate dictionary sets of a key (hash h; mid = key of 9-16 bytes),
 // as byte offsets of dset (16-byte sets at LDS offset 0): short keys take set
 // a = h >> 20 and a ^ x, x = ((h >> 4) & 4095) | 1; mid keys the same bits
-// masked to 8 (a = (h >> 20) & 255), in the 256 sets after the 4096 short ones.
+// masked to 8 (a = (h >> 20) & 255), in the 256 sets after the 4096 short ones
+// (DictFull; DictMini: 9 and 6 bits).
 // Computed pre-scaled by 16 with two masks, not three selects and two shifts.
+template <class G = DictFull>
 __device__ __forceinline__ void dict_set_addrs(uint32_t h, bool mid, uint32_t& a1, uint32_t& a2) {
-    static_assert(kDictShortSets == 4096 && kDictMidSets == 256, "set index = 12 / 8 hash bits");
-    const uint32_t m = mid ? 0x0FF0u : 0xFFF0u;
-    const uint32_t off = mid ? (uint32_t)kDictShortSets * 16u : 0u;
+    const uint32_t m = mid ? (uint32_t)(G::kMid - 1) << 4 : (uint32_t)(G::kShort - 1) << 4;
+    const uint32_t off = mid ? (uint32_t)G::kShort * 16u : 0u;
     const uint32_t A = h >> 16;           // a << 4 in bits 4..15
     const uint32_t X = (h & ~15u) | 16u;  // x << 4 in bits 4..15 (bit 4 forced: a2 != a1)
     // (a & b) | c as v_bitop3_b32 (truth table 0xEA): a plain VALU op on gfx950,
@@ -118,9 +120,10 @@ __device__ __forceinline__ void dict_set_addrs(uint32_t h, bool mid, uint32_t& a
     a1 = __builtin_amdgcn_bitop3_b32(A, m, off, 0xEA);
     a2 = __builtin_amdgcn_bitop3_b32(A ^ X, m, off, 0xEA);
 }
+template <class G = DictFull>
 __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, uint32_t& s2) {
     uint32_t a1, a2;
-    dict_set_addrs(h, mid, a1, a2);
+    dict_set_addrs<G>(h, mid, a1, a2);
     s1 = a1 >> 4;
     s2 = a2 >> 4;
 }
@@ -318,7 +321,11 @@ constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
 // UTF-8 chunks: leads decoded wave-compacted (utf8_mask16_wave) or by the
 // per-lane loop (utf8_mask16)
 #ifndef MRG_UTF8_WAVE
-#define MRG_UTF8_WAVE 0
+#define MRG_UTF8_WAVE 1
+#endif
+// word starts into the chunk's list one per loop turn (default) or two
+#ifndef MRG_LIST_PAIRS
+#define MRG_LIST_PAIRS 0
 #endif
 __device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint32_t lleft, uint32_t lane) {
     for (uint32_t g = 0; g < lleft; g += kWave)
@@ -353,17 +360,16 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     const lds_uint4* kmask4 = (const lds_uint4*)L.kmask;
     if (t.dbg && tid == 0) t.dbg[2 * (NB + blockIdx.x)] = __builtin_amdgcn_s_memrealtime();
 
-    const bool use_dict = !kS && t.dict != nullptr;
+    using Geo = typename MapLdsT<NW, NB, kS>::Geo;
+    const bool use_dict = t.dict != nullptr;
     // NW (waves per workgroup) < kWavesPerWG only for the occupancy benchmark (map_mode 0x1000 / 0x2000)
     constexpr uint32_t kT = NW * kWave;
-    if constexpr (!kS) {
-        for (uint32_t i = tid; i < (uint32_t)kDictSets; i += kT) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
-        // chunks [cbeg, cend) of the split; resume: an earlier launch mapped chunks
-        // before cbeg (host input streamed piece by piece), so this workgroup's spill
-        // cursors and dictionary counts continue from what it wrote
-        for (uint32_t i = tid; i < (uint32_t)kDictSlots + kWave; i += kT)
-            dcnt[i] = resume && use_dict && i < (uint32_t)kDictSlots ? t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i] : 0u;
-    }
+    for (uint32_t i = tid; i < (uint32_t)Geo::kSets; i += kT) dset[i] = use_dict ? to_v4(t.dict[i]) : (u32x4){0, 0, 0, 0};
+    // chunks [cbeg, cend) of the split; resume: an earlier launch mapped chunks
+    // before cbeg (host input streamed piece by piece), so this workgroup's spill
+    // cursors and dictionary counts continue from what it wrote
+    for (uint32_t i = tid; i < (uint32_t)Geo::kSlots + kWave; i += kT)
+        dcnt[i] = resume && use_dict && i < (uint32_t)Geo::kSlots ? t.dict_cnt[(uint64_t)blockIdx.x * Geo::kSlots + i] : 0u;
     for (uint32_t b = tid; b < 2u * NB + kWave; b += kT) {
         uint32_t v = 0;
         if (resume && b < (uint32_t)NB) v = t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
@@ -509,8 +515,10 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint32_t total = __builtin_amdgcn_readlane(incl, 63);
             uint32_t j = incl - nsa;
             const uint32_t pos0 = 16 * lane;
+#if MRG_LIST_PAIRS
             // two starts per loop turn: the loop runs max-over-lanes(starts) / 2
             // turns, its control (compare, exec update, branch) paid once per pair
+            // (A/B variant: C2's map kernel 6.95 vs 6.69 ms one per turn)
             while (SA) {
                 const uint32_t b1 = ffbl_raw(SA);
                 SA &= SA - 1;
@@ -522,6 +530,14 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 SA &= SA - 1;
                 j += 2;
             }
+#else
+            while (SA) {
+                const uint32_t bit = __builtin_ctz(SA);
+                const uint32_t len = ffbl_raw(nl >> bit);  // -1 when no terminator in the window
+                list[j++] = (uint16_t)((pos0 + bit) | (len << 10));
+                SA &= SA - 1;
+            }
+#endif
             wave_sync();
             if constexpr ((mode & 2) != 0) {
                 acc += total;
@@ -603,6 +619,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         #pragma unroll
                             for (int u = 0; u < kBatch; u++) {
                                 mFall[u] = mLng[u];
+#ifdef MRG_NO_LREC  // (A/B variant: every long word through the start-offset list)
+                                continue;
+#endif
                                 if (mLng[u] == 0 || tr.lrec == nullptr) continue;
                                 const uint32_t p = e[u] & 0x3FFu, lw = p >> 4;
                                 const uint32_t m0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lw << 2), (int)mA);
@@ -699,7 +718,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         uint32_t a1[kBatch], a2[kBatch];  // byte offsets of the two sets
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
-                            dict_set_addrs(hh[u], __builtin_amdgcn_inverse_ballot_w64(mMid[u]), a1[u], a2[u]);
+                            dict_set_addrs<Geo>(hh[u], __builtin_amdgcn_inverse_ballot_w64(mMid[u]), a1[u], a2[u]);
                             A[u] = *(const lds_uint4*)((const lds_u8*)dset + a1[u]);
                             B[u] = *(const lds_uint4*)((const lds_u8*)dset + a2[u]);
                         }
@@ -997,9 +1016,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         *p8 = k8;
     }
     if (use_dict)
-        for (uint32_t i = tid; i < (uint32_t)kDictSlots; i += kT) {
+        for (uint32_t i = tid; i < (uint32_t)Geo::kSlots; i += kT) {
             const uint32_t v = dcnt[i];
-            uint32_t* pd = &t.dict_cnt[(uint64_t)blockIdx.x * kDictSlots + i];
+            uint32_t* pd = &t.dict_cnt[(uint64_t)blockIdx.x * Geo::kSlots + i];
             hits += v - (resume ? *pd : 0u);
             *pd = v;
         }
@@ -1908,23 +1927,24 @@ __global__ void __launch_bounds__(1024) seg_scan_kernel(const uint32_t* tmp, uin
 // block owns 64 slots; its 16 waves each sum every 16th workgroup's row
 // (coalesced 256 B per wave), then the partial sums meet in LDS.
 constexpr int kEmitSlots = 64;
+template <class G>
 __global__ void __launch_bounds__(1024) dict_emit_kernel(Tables t, uint32_t nwg) {
     __shared__ unsigned long long part[16][kEmitSlots];
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t i = blockIdx.x * kEmitSlots + lane;
     unsigned long long sum = 0;
-    if (i < (uint32_t)kDictSlots)
-        for (uint32_t g = wv; g < nwg; g += 16) sum += t.dict_cnt[(uint64_t)g * kDictSlots + i];
+    if (i < (uint32_t)G::kSlots)
+        for (uint32_t g = wv; g < nwg; g += 16) sum += t.dict_cnt[(uint64_t)g * G::kSlots + i];
     part[wv][lane] = sum;
     __syncthreads();
     if (wv != 0) return;
     sum = 0;
     for (int w = 0; w < 16; w++) sum += part[w][lane];
     uint64_t k0 = 0, k1 = 0;
-    if (i < (uint32_t)kDictSlots) {
+    if (i < (uint32_t)G::kSlots) {
         const uint32_t set = i >> 1, way = i & 1;
         const uint4 sv = t.dict[set];
-        if (set >= (uint32_t)kDictShortSets) {
+        if (set >= (uint32_t)G::kShort) {
             k0 = way ? 0 : ((uint64_t)sv.y << 32) | sv.x;
             k1 = ((uint64_t)sv.w << 32) | sv.z;
         } else {
@@ -1987,13 +2007,14 @@ __global__ void dict_cands_kernel(Recs r, const uint32_t* order, uint64_t lim, u
 // hottest candidates get a fix-up pass in rank order: one that lost takes the
 // way of the coldest key in its two sets when that key is colder.
 constexpr uint32_t kDictHot = 4096;
+template <class G>
 __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uint64_t lim, uint4* dict) {
-    __shared__ uint4 S[kDictSets];
-    __shared__ uint32_t fill[kDictSets];
-    __shared__ uint32_t rk[kDictSets][2];    // candidate index (rank) of the key in each way, ~0u = empty
+    __shared__ uint4 S[G::kSets];
+    __shared__ uint32_t fill[G::kSets];
+    __shared__ uint32_t rk[G::kSets][2];    // candidate index (rank) of the key in each way, ~0u = empty
     __shared__ uint32_t hot[kDictHot / 32];  // placed bits of the kDictHot hottest candidates
     const uint32_t tid = threadIdx.x;
-    for (uint32_t i = tid; i < (uint32_t)kDictSets; i += 1024) {
+    for (uint32_t i = tid; i < (uint32_t)G::kSets; i += 1024) {
         S[i] = make_uint4(0, 0, 0, 0);
         fill[i] = 0;
         rk[i][0] = rk[i][1] = ~0u;
@@ -2009,7 +2030,7 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uin
         if (k0 != 0) {
             const bool mid = k1 != 0;
             uint32_t s1, s2;
-            dict_sets(fold32(c.x, c.y, c.z, c.w), mid, s1, s2);
+            dict_sets<G>(fold32(c.x, c.y, c.z, c.w), mid, s1, s2);
             const uint32_t ways = mid ? 1u : 2u;
             uint32_t s = s1, w = atomicAdd(&fill[s1], 1u);
             if (w >= ways) { s = s2; w = atomicAdd(&fill[s2], 1u); }
@@ -2040,7 +2061,7 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uin
                     tried = true;
                     const bool mid = (c.z | c.w) != 0;
                     uint32_t s1, s2;
-                    dict_sets(fold32(c.x, c.y, c.z, c.w), mid, s1, s2);
+                    dict_sets<G>(fold32(c.x, c.y, c.z, c.w), mid, s1, s2);
                     const uint32_t ways = mid ? 1u : 2u;
                     uint32_t bs = s1, bw = 0, br = rk[s1][0];  // the coldest way of the two sets
                     for (uint32_t k = 0; k < 2 * ways; k++) {
@@ -2065,7 +2086,7 @@ __global__ void __launch_bounds__(1024) dict_build_kernel(const uint4* cand, uin
         }
     }
     __syncthreads();
-    for (uint32_t i = tid; i < (uint32_t)kDictSets; i += 1024) dict[i] = S[i];
+    for (uint32_t i = tid; i < (uint32_t)G::kSets; i += 1024) dict[i] = S[i];
 }
 
 // ------------------------------------------------------------ launchers
@@ -2096,7 +2117,7 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     return true;
 #endif
     if (t.sp.nb == kSpillBucketsHi) {  // high-cardinality layout (ablation modes apply to the default one only)
-        if (t.hi_staged && !t.dict)  // no dictionary: its LDS write-combines the 8-byte spill streams
+        if (t.hi_staged)  // the mini dictionary: its LDS write-combines the 8-byte spill streams
             wc_map_kernel<0, kWavesPerWG, kSpillBucketsHi, true><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
         else
             wc_map_kernel<0, 12, kSpillBucketsHi><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
@@ -2158,7 +2179,8 @@ void launch_seg_layout(const Tables& t, uint32_t* tmp, uint64_t* off8, uint64_t*
 }
 
 void launch_dict_emit(const Tables& t, uint32_t nwg, hipStream_t s) {
-    dict_emit_kernel<<<(kDictSlots + kEmitSlots - 1) / kEmitSlots, 1024, 0, s>>>(t, nwg);
+    if (t.hi_staged) dict_emit_kernel<DictMini><<<(DictMini::kSlots + kEmitSlots - 1) / kEmitSlots, 1024, 0, s>>>(t, nwg);
+    else dict_emit_kernel<DictFull><<<(DictFull::kSlots + kEmitSlots - 1) / kEmitSlots, 1024, 0, s>>>(t, nwg);
 }
 
 void launch_sample_gather(const uint8_t* in, uint64_t /*n*/, uint64_t win, uint64_t stride, uint32_t nwin, uint8_t* dst,
@@ -2171,10 +2193,11 @@ void launch_dict_keys(const Recs& r, uint32_t* keys, uint32_t* idx, hipStream_t 
 }
 
 // cand: scratch for kDictCands uint4
-void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, hipStream_t s) {
+void launch_dict_build(const Recs& r, const uint32_t* order, uint64_t n, uint4* cand, uint4* dict, bool mini, hipStream_t s) {
     const uint64_t lim = n < kDictCands ? n : kDictCands;
     if (lim) dict_cands_kernel<<<(unsigned)((lim + 255) / 256), 256, 0, s>>>(r, order, lim, cand);
-    dict_build_kernel<<<1, 1024, 0, s>>>(cand, lim, dict);
+    if (mini) dict_build_kernel<DictMini><<<1, 1024, 0, s>>>(cand, lim, dict);
+    else dict_build_kernel<DictFull><<<1, 1024, 0, s>>>(cand, lim, dict);
 }
 
 }  // namespace mrg

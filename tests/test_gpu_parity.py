@@ -201,8 +201,8 @@ def test_wc_bucket_aggregator_overflow(ctx, rounds, big):
 @pytest.mark.parametrize("rounds,stage", [(0, -1), (1, -1), (0, 1), (1, 1)])
 def test_wc_high_cardinality_buckets(ctx, rounds, stage):
     """2048 spill buckets (high-cardinality layout: 12-wave map workgroups, 4x
-    the aggregator workgroups; stage 1: no dictionary, 16-wave workgroups
-    write-combining the 8-byte streams in LDS), forced and chosen by the feedback
+    the aggregator workgroups; stage 1: the 1088-key mini dictionary, 16-wave
+    workgroups write-combining the 8-byte streams in LDS), forced and chosen by the feedback
     rule: exact on a 3M-word vocabulary, in rounds or with every miss counted in HBM."""
     voc = C.Vocab(C.KIND_ASCII, 1.07, 3_000_000, 16)
     files = [bytes(voc.fill_files([26_000_000], [16], C.wc_params(vocab_lo=0, vocab_hi=3_000_000))[0])]
@@ -237,7 +237,8 @@ def test_wc_staged_spill(ctx_dict, case):
     (groups reaching past a stream's capacity, the rest through the HBM table),
     host input mapped piece by piece (resumed launches: cursors and groups carry
     over), and mixed-script text with long words; all exact, with the dictionary
-    option on (the staged kernel has none: the split is mapped without it)."""
+    option on (the staged kernel's mini dictionary: 1024 short + 64 mid keys, built
+    from the same sample; its hits are counted)."""
     c = ctx_dict
     c.set_option("spill_buckets", 2048)
     c.set_option("hi_stage", 1)
@@ -258,7 +259,9 @@ def test_wc_staged_spill(ctx_dict, case):
             files = cases.synthetic(C.KIND_UTF8, 300_000, [5_000_000, 3_000_001], 74, 0.0005) + \
                 [cases.long_words(2_000_000, 3)]
             check(c, "wc", files, nreduces=(1, 10))
-        assert c.stats()["spill_buckets"] == 2048 and c.stats()["dict_hits"] == 0
+        assert c.stats()["spill_buckets"] == 2048 and c.stats()["dict_hits"] > 0
+        # the next split of the context: the kept mini image is re-checked on its sample
+        check(c, "wc", files[:1], nreduces=(10,))
     finally:
         for k in ("spill_buckets", "hi_stage", "spill_stream_keys", "ingest_piece", "ingest_min"):
             c.set_option(k, 0)
