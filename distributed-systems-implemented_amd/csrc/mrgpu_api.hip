@@ -887,6 +887,7 @@ static int ingest_map(mrg_ctx* c, Ingest& g, uint64_t chunk_bytes, uint64_t len,
 static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce, LetterTables lt, mrg_parts** out,
                   const uint8_t* host = nullptr) {
     int rc;
+    const auto t_call = std::chrono::steady_clock::now();  // (MRG_DEBUG_TIMES diagnostics)
     c->lo_log2_cur = c->lo_log2;
     c->spill_nb = c->spill_buckets_opt ? (uint32_t)c->spill_buckets_opt : c->next_nb;
     if (c->spill_alt) std::swap(c->spool.p, c->spool_alt.p), std::swap(c->spool.cap, c->spool_alt.cap);
@@ -970,6 +971,12 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         if (launch_collect(t, c->lo_log2_cur > 0, c->s)) return fail(c, MRG_EDEVICE, "collect failed");
         if ((rc = read_counters(c))) return rc;
         Counters h = *c->h_ctr;
+        if (c->debug_times)
+            fprintf(stderr, "[mrg wc] attempt %d: status %#x, %.3f ms since the call; nrec %llu, spilled %llu, ovf %llu, "
+                    "dict hits %llu, buckets %u, staged %d, dict %d\n", attempt, h.status,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count(),
+                    (unsigned long long)h.nrec, (unsigned long long)h.spilled, (unsigned long long)h.spill_ovf,
+                    (unsigned long long)h.dict_hits, c->spill_nb, (int)staged, (int)have_dict);
         if (h.status & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", h.status);
         if ((h.status & kStRecFull) && h.long_bytes + 16 > c->recarena.cap && h.nrec <= c->rec_cap) {
             // only the arena was short: grow it and run the collect again (not the map)
@@ -2233,6 +2240,7 @@ int mrg_exchange_group(mrg_ctx* const* ctxs, int P, const mrg_parts* const* loca
 int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, const uint8_t* pat, size_t plen,
                 uint32_t nreduce, void** bytes, size_t* nb, uint64_t* offsets) {
     if (!c || !bytes || !nb || !offsets) return MRG_EINVAL;
+    const auto t_job = std::chrono::steady_clock::now();
     int drc;
     if ((drc = bind(c)) || (drc = drain_async(c))) return drc;  // (its pinned output buffer is separate)
     mrg_parts* p = nullptr;
@@ -2295,6 +2303,10 @@ int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, cons
     if (n && !direct) HCHK(c, hipMemcpyAsync(c->h_out, d, n, hipMemcpyDeviceToHost, c->s));
     HCHK(c, hipEventRecord(c->ev[7], c->s));
     HCHK(c, hipEventSynchronize(c->ev[7]));
+    if (c->debug_times)
+        fprintf(stderr, "[mrg job] %.3f ms (map total %.3f, reduce %.3f, d2h %.3f ms of events)\n",
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_job).count(),
+                keep.map_total_ms, ev_ms(c->ev[4], c->ev[5]), ev_ms(c->ev[6], c->ev[7]));
     keep.reduce_ms = ev_ms(c->ev[4], c->ev[5]);
     keep.d2h_ms = ev_ms(c->ev[6], c->ev[7]);
     keep.output_bytes = n;

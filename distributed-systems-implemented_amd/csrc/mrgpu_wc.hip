@@ -201,6 +201,29 @@ __device__ __forceinline__ void wait_vmem_iter_wide() {
     asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
 }
 __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// vmcnt(n) for a wave-uniform n (the counted wait after an iteration that issued
+// extra VMEM operations: long-word records, the start-offset list).  n must not
+// exceed the operations issued after the awaited DMA (fewer only waits longer);
+// past 15 it waits for vmcnt(15).
+template <int N>
+__device__ __forceinline__ void vmcnt_imm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+__device__ __forceinline__ void wait_vmem_upto(uint32_t n) {
+    switch (n) {
+        case 3: vmcnt_imm<3>(); break;
+        case 4: vmcnt_imm<4>(); break;
+        case 5: vmcnt_imm<5>(); break;
+        case 6: vmcnt_imm<6>(); break;
+        case 7: vmcnt_imm<7>(); break;
+        case 8: vmcnt_imm<8>(); break;
+        case 9: vmcnt_imm<9>(); break;
+        case 10: vmcnt_imm<10>(); break;
+        case 11: vmcnt_imm<11>(); break;
+        case 12: vmcnt_imm<12>(); break;
+        case 13: vmcnt_imm<13>(); break;
+        case 14: vmcnt_imm<14>(); break;
+        default: vmcnt_imm<15>(); break;
+    }
+}
 // The staged (kS) loop: the flush's 4 stores and the DMA follow the awaited DMA
 __device__ __forceinline__ void wait_vmem_iter_staged() { asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); }
 
@@ -344,7 +367,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // mode (benchmark ablation only, compile-time; results are wrong unless 0):
     // 1 = stream input only, 2 = tokenize only (no per-word work), 4 = per-word
     // key extraction without the dictionary, 16 = no spill append (misses dropped),
-    // 32 = spill cursors but no stores, 8 = dictionary counters not updated;
+    // 32 = spill cursors but no stores, 8 = dictionary counters not updated,
+    // 64 = non-ASCII chunks classified by the ASCII rule (no rune decoding);
     // 0x100 / 0x4000 / 0x8000 (exact) = input loads with the default policy /
     // sc1 / sc0 sc1 instead of nt.  (Measured and removed, DESIGN.md §6: the 4
     // hottest keys counted by ballots into SGPRs; key bytes by three aligned
@@ -427,6 +451,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // spill store instructions the previous iteration issued after the DMA now
     // awaited: 2 (staged appends) or kVmemWide (appends from the word slots)
     bool wide_prev = false;
+    // VMEM operations the previous iteration issued beyond those counted above
+    // (only ones it certainly issued: an uncounted one only lengthens the wait)
+    uint32_t xv = 0;
     // kS: every wave runs the workgroup's trip count (its barriers), a chunk past
     // cend counting as empty
     const uint32_t cw0 = cbeg + blockIdx.x * NW;
@@ -435,10 +462,15 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     for (uint32_t c = c0; kS ? trip < ktrips : c < cend;
          c += stride, cs += cstep, kf = k, k = k == kRing - 1 ? 0 : k + 1, trip++) {
         // chunk c's DMA (issued two iterations ago) has landed
-        if constexpr (kS) wait_vmem_iter_staged();
-        else if (wide_prev) wait_vmem_iter_wide();
-        else wait_vmem_iter();
+        if (xv == 0) {
+            if constexpr (kS) wait_vmem_iter_staged();
+            else if (wide_prev) wait_vmem_iter_wide();
+            else wait_vmem_iter();
+        } else {
+            wait_vmem_upto((kS ? 5u : wide_prev ? (uint32_t)kVmemWide + 1u : (uint32_t)kVmemPerIter) + xv);
+        }
         wide_prev = false;
+        xv = 0;
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
         const uint32_t bufa = ring0 + k * kSlotStride;  // = lds_addr(buf)
         lds_uint4* b4 = (lds_uint4*)buf;
@@ -462,7 +494,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint32_t hi = (ca.x | ca.y | ca.z | ca.w) & 0x80808080u;
             const bool ascii = __ballot(hi != 0) == 0;
             uint32_t mA;
-            if (ascii) {
+            if (ascii || (mode & 64) != 0) {  // (mode 64, ablation: no rune decoding)
                 mA = ascii_mask16(ca);
             } else {
                 // UTF-8: ASCII letters by SWAR, one loop turn per lead byte, letter
@@ -604,7 +636,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     // words: a same-address atomic per chunk serialized the whole kernel,
                     // 207 ms per 10 GB), with one store per chunk: the starts are staged
                     // in the list slot, whose entries are all read by now (one pass).
-                    // The extra store only lengthens the next counted wait.
+                    // The extra stores are counted (xv) by the next iteration's wait.
                     if (mLng[0] | mLng[1] | mLng[2]) {
                         if (passes == 1) {
                             // Words of 17-32 bytes that end inside the window leave as
@@ -658,6 +690,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                     __builtin_amdgcn_raw_buffer_store_b128((u32x4){k[0], k[1], k[2], k[3]}, rsr,
                                                                            ro == kOutOfRange ? kOutOfRange : ro + 16u * hf, 0, 0);
                                 }
+                                xv += 2;  // the two record stores (the next wait counts them)
                                 if (rbase + (uint32_t)__popcll(mR) > rcap && lane == 0) set_status(tr.ctr, kStLrecFull);
                                 mFall[u] = mLng[u] & ~mR;
                             }
@@ -696,6 +729,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                 const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
                                 __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
                                                                       lane < nlong ? lane * 8u : kOutOfRange, 0, 0);
+                                xv += 1;
                                 lbase += nlong;
                                 lleft -= nlong;
                             }
@@ -2128,6 +2162,7 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M, kWavesPerWG, kSpillBucketsLo><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;
             MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(8) MRG_MAP_MODE(16) MRG_MAP_MODE(32)
+            MRG_MAP_MODE(64) MRG_MAP_MODE(64 | 2)
 #undef MRG_MAP_MODE
             default: wc_map_kernel<0, kWavesPerWG, kSpillBucketsLo><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
         }

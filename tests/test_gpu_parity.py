@@ -259,6 +259,7 @@ def test_wc_staged_spill(ctx_dict, case):
             files = cases.synthetic(C.KIND_UTF8, 300_000, [5_000_000, 3_000_001], 74, 0.0005) + \
                 [cases.long_words(2_000_000, 3)]
             check(c, "wc", files, nreduces=(1, 10))
+            gpu_partitioned(c, "wc", files[:1], 10)  # (the long-word file alone has no dictionary hits)
         assert c.stats()["spill_buckets"] == 2048 and c.stats()["dict_hits"] > 0
         # the next split of the context: the kept mini image is re-checked on its sample
         check(c, "wc", files[:1], nreduces=(10,))
