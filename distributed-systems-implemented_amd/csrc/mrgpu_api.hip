@@ -888,6 +888,11 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
                   const uint8_t* host = nullptr) {
     int rc;
     const auto t_call = std::chrono::steady_clock::now();  // (MRG_DEBUG_TIMES diagnostics)
+    auto mark = [&](const char* what) {
+        if (c->debug_times)
+            fprintf(stderr, "[mrg wc] %s: %.3f ms since the call\n", what,
+                    std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count());
+    };
     c->lo_log2_cur = c->lo_log2;
     c->spill_nb = c->spill_buckets_opt ? (uint32_t)c->spill_buckets_opt : c->next_nb;
     if (c->spill_alt) std::swap(c->spool.p, c->spool_alt.p), std::swap(c->spool.cap, c->spool_alt.cap);
@@ -910,6 +915,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         const double need = 1.3 * c->words_per_byte / (2.0 * 0.75 / 16.0);
         if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
     }
+    mark("dictionary");
     // the sample may have raised spill_scale: size the streams for this split now,
     // not only from the next call on (overflowing streams merge through HBM: slow)
     if ((rc = ensure_spill(c, len))) {
@@ -917,6 +923,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         return rc;
     }
     HCHK(c, hipEventRecord(c->ev[10], c->s));
+    mark("spill layout");
     for (int attempt = 0; attempt < 8; attempt++) {
         c->lo_log2 = std::max(c->lo_log2, c->lo_log2_cur);  // long words: the grown size sticks for later wc maps
         if ((rc = ensure_tables(c)) || (rc = ensure_recbuf(c))) {
@@ -937,6 +944,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             t.lrec_cap = c->lrec_cap;
         }
         clear_for_run(c, t);
+        mark("tables");
         HCHK(c, hipEventRecord(c->ev[0], c->s));
         if (ing.npieces && attempt == 0) {  // the first pass runs while the host input streams in
             rc = ingest_map(c, ing, kWcChunkBytes, len, [&](uint64_t cb, uint64_t ce, bool resume) {
@@ -969,6 +977,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             t.out = rec_view(c);
         }
         if (launch_collect(t, c->lo_log2_cur > 0, c->s)) return fail(c, MRG_EDEVICE, "collect failed");
+        mark("launched");
         if ((rc = read_counters(c))) return rc;
         Counters h = *c->h_ctr;
         if (c->debug_times)

@@ -643,29 +643,38 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             // 32-byte key records, read here from the slot (wc_lrec_kernel
                             // counts them: no second decode of the input); longer words and
                             // words running past the window take the start-offset list.
+                            // The batch's long words are first compacted into the list slot
+                            // (its entries are all read by now: one pass), so one lane per
+                            // long word does the rest in a single round (per word slot, a
+                            // round for the one or two long words of each 64 cost ~3x).
                             // The length comes from the letter masks of the word's lane and
                             // the next two (ds_bpermute; lanes past 63 are unknown bytes,
                             // taken as letters, so a word reaching them falls back).
-                            uint64_t mFall[kBatch];
-                            const Tables& tr = cold(t);
+                            lds_u16* lst16 = (lds_u16*)L.ring[wv][kf];
+                            uint32_t nlong = 0;
         #pragma unroll
                             for (int u = 0; u < kBatch; u++) {
-                                mFall[u] = mLng[u];
+                                if (__builtin_amdgcn_inverse_ballot_w64(mLng[u])) lst16[nlong + mbcnt64(mLng[u])] = (uint16_t)e[u];
+                                nlong += (uint32_t)__popcll(mLng[u]);
+                            }
+                            wave_sync();
+                            const bool have = lane < nlong;  // nlong <= 59 (> 16-byte words of 992 bytes)
+                            const uint32_t p = have ? lst16[lane] & 0x3FFu : 0u;
+                            const Tables& tr = cold(t);
 #ifdef MRG_NO_LREC  // (A/B variant: every long word through the start-offset list)
-                                continue;
-#endif
-                                if (mLng[u] == 0 || tr.lrec == nullptr) continue;
-                                const uint32_t p = e[u] & 0x3FFu, lw = p >> 4;
-                                const uint32_t m0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lw << 2), (int)mA);
-                                const uint32_t m1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lw + 1) << 2), (int)mA);
-                                const uint32_t m2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lw + 2) << 2), (int)mA);
-                                const uint64_t win = (uint64_t)(m0 & 0xFFFFu) |
-                                                     ((uint64_t)(lw + 1 < 64u ? m1 & 0xFFFFu : 0xFFFFu) << 16) |
-                                                     ((uint64_t)(lw + 2 < 64u ? m2 & 0xFFFFu : 0xFFFFu) << 32) |
-                                                     (0xFFFFull << 48);
-                                const uint32_t wl = (uint32_t)__builtin_ctzll((~win >> (p & 15u)) | (1ull << 63));
-                                const uint64_t mR = mLng[u] & __ballot(wl <= 32u);
-                                if (mR == 0) continue;
+                            const uint64_t mR = 0;
+#else
+                            const uint32_t lw = p >> 4;
+                            const uint32_t m0 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(lw << 2), (int)mA);
+                            const uint32_t m1 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lw + 1) << 2), (int)mA);
+                            const uint32_t m2 = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((lw + 2) << 2), (int)mA);
+                            const uint64_t win = (uint64_t)(m0 & 0xFFFFu) |
+                                                 ((uint64_t)(lw + 1 < 64u ? m1 & 0xFFFFu : 0xFFFFu) << 16) |
+                                                 ((uint64_t)(lw + 2 < 64u ? m2 & 0xFFFFu : 0xFFFFu) << 32) |
+                                                 (0xFFFFull << 48);
+                            const uint32_t wl = (uint32_t)__builtin_ctzll((~win >> (p & 15u)) | (1ull << 63));
+                            const uint64_t mR = tr.lrec != nullptr ? __ballot(have && wl <= 32u) : 0ull;
+                            if (mR) {
                                 uint32_t rbase = 0;
                                 if (lane == 0) rbase = atomicAdd(&L.lrec_n, (uint32_t)__popcll(mR));
                                 rbase = __builtin_amdgcn_readfirstlane(rbase);
@@ -692,19 +701,13 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                 }
                                 xv += 2;  // the two record stores (the next wait counts them)
                                 if (rbase + (uint32_t)__popcll(mR) > rcap && lane == 0) set_status(tr.ctr, kStLrecFull);
-                                mFall[u] = mLng[u] & ~mR;
                             }
-                            if (mFall[0] | mFall[1] | mFall[2]) {
-                                lds_u64* lst = (lds_u64*)L.ring[wv][kf];
-                                uint32_t nlong = 0;
-            #pragma unroll
-                                for (int u = 0; u < kBatch; u++) {
-                                    if (__builtin_amdgcn_inverse_ballot_w64(mFall[u]))
-                                        lst[nlong + mbcnt64(mFall[u])] = cs - kBack + (e[u] & 0x3FFu);
-                                    nlong += (uint32_t)__popcll(mFall[u]);
-                                }
+#endif
+                            const uint64_t mFall = __ballot(have) & ~mR;
+                            if (mFall) {
+                                const uint32_t nfall = (uint32_t)__popcll(mFall);
                                 const Tables& tc = cold(t);
-                                if (nlong > lleft) {  // a fresh range (rare): close the old one, one atomic, drain
+                                if (nfall > lleft) {  // a fresh range (rare): close the old one, one atomic, drain
                                     list_close(tc, lbase, lleft, lane);
                                     const uint32_t want = kLongReserve;
                                     unsigned long long b0 = 0;
@@ -726,12 +729,13 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                 const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
                                     (void*)(lptr + lbase), (short)0, (int)(room < (0xFFFFFF00ull >> 3) ? room * 8u : 0xFFFFFF00ull),
                                     0x00020000);
-                                const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
-                                __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
-                                                                      lane < nlong ? lane * 8u : kOutOfRange, 0, 0);
+                                const uint64_t v = cs - kBack + p;  // the word's input offset
+                                __builtin_amdgcn_raw_buffer_store_b64(
+                                    (u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
+                                    __builtin_amdgcn_inverse_ballot_w64(mFall) ? mbcnt64(mFall) * 8u : kOutOfRange, 0, 0);
                                 xv += 1;
-                                lbase += nlong;
-                                lleft -= nlong;
+                                lbase += nfall;
+                                lleft -= nfall;
                             }
                         } else {  // several passes (> 192 words): the list slot is still needed
         #pragma unroll
