@@ -223,12 +223,13 @@ struct mrg_ctx {
     bool seg_sync = true;               // size the miss segments from this split's totals (host read)
     bool out_direct = true;             // mrg_run_job: output lines written straight into pinned host memory
     bool grep_literal = false;          // grep: regexp metacharacters taken literally (QuoteMeta) instead of refused
-    DevBuf lrec, lrec_cnt;              // wc: 32-byte long-word records [map workgroup][lrec_cap], their counts
-    uint32_t lrec_cap = 4096;           // records per map workgroup region (grows on kStLrecFull)
+    DevBuf lrec, lrec_cnt;              // wc: 32-byte long-word records [map wave][lrec_cap], their counts
+    uint32_t lrec_cap = 1024;           // records per map wave's region (grows on kStLrecFull)
     bool lrec_on = true;                // option long_records (-1: every long word through the offset list)
-    // 2048-bucket (high-cardinality) splits: no dictionary, the map kernel
-    // write-combines its 8-byte spill streams in that LDS (option hi_stage)
-    bool hi_stage = false;
+    // 2048-bucket (high-cardinality) splits: the mini dictionary (DictMini), the
+    // map kernel write-combines its 8-byte spill streams in the LDS the full one
+    // would take (option hi_stage)
+    bool hi_stage = true;
     uint64_t arena_hint = 0;            // wc: long-key bytes expected in a split (the previous one's + 25 %)
     DevBuf jmeta, jtmp, jlines, jout;    // JSON-lines export (reference intermediate format)
     DevBuf ghits, glines, gdefer;        // grep: sorted hits, resolved (start, end) lines, deferred hits
@@ -722,8 +723,12 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
         // spills 0.04).  A split whose sample misses its (first-level) dictionary
         // more often gets proportionally longer streams, 30 % over the estimate
         // (the final dictionary only hits more).  Never shrinks within a context.
+        // (The staged map's streams are sized from the previous split's words
+        // instead, wc_map: its sample rate, measured with the mini dictionary over
+        // windows that may hold a file's vocabulary-first region, overestimated it
+        // and regrew a ~100 GB pool mid-run: 3.5 s.)
         const double need = 1.3 * rate / (2.0 * 0.75 / 16.0);
-        if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
+        if (!mini && need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
     }
     c->stats.dict_keys = nrec;
     c->dict_valid = true;
@@ -937,8 +942,8 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         t.out = rec_view(c);
         t.out_cap = c->rec_cap;
         if (c->lrec_on) {
-            HCHK(c, c->lrec.ensure_grow((size_t)nwg * c->lrec_cap * 32));
-            HCHK(c, c->lrec_cnt.ensure((size_t)kMaxMapWGs * 4));
+            HCHK(c, c->lrec.ensure_grow((size_t)nwg * kWavesPerWG * c->lrec_cap * 32));
+            HCHK(c, c->lrec_cnt.ensure((size_t)kMaxMapWGs * kWavesPerWG * 4));
             t.lrec = (uint4*)c->lrec.p;
             t.lrec_cnt = (uint32_t*)c->lrec_cnt.p;
             t.lrec_cap = c->lrec_cap;
@@ -999,11 +1004,15 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         c->arena_hint = h.long_bytes + h.long_bytes / 4;
         if (len) c->words_per_byte = (double)(h.dict_hits + h.spilled + h.spill_ovf) / (double)len;
         if (h.status & kStLrecFull) {  // a record region filled up: size them for this split's busiest workgroup
-            std::vector<uint32_t> cnt(nwg);
-            HCHK(c, hipMemcpy(cnt.data(), c->lrec_cnt.p, (size_t)nwg * 4, hipMemcpyDeviceToHost));
+            std::vector<uint32_t> cnt((size_t)nwg * kWavesPerWG);
+            HCHK(c, hipMemcpy(cnt.data(), c->lrec_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
             const uint32_t mx = *std::max_element(cnt.begin(), cnt.end());
-            c->lrec_cap = (uint32_t)std::min<uint64_t>(std::max<uint64_t>((uint64_t)mx + mx / 4 + 1024, 2ull * c->lrec_cap),
-                                                       1u << 26);
+            const uint64_t want = std::max<uint64_t>((uint64_t)mx + mx / 4 + 1024, 2ull * c->lrec_cap);
+            // (a split of almost nothing but 17-32-byte words: past 2^20 records per
+            // wave the regions would take more HBM than the input; the offset list then
+            // takes every long word, for the rest of the context)
+            if (want > (1u << 20)) c->lrec_on = false;
+            else c->lrec_cap = (uint32_t)want;
         }
         if (grow_on_overflow(c, h.status & (kStListFull | kStShortFull | kStLongFull | kStRecFull | kStSegFull)) ||
             (h.status & kStLrecFull))
@@ -1293,12 +1302,12 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set_compact_ties(c->rws, v >= 0);
     } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default) or via a copy (-1)
         c->out_direct = v >= 0;
-    } else if (!strcmp(name, "hi_stage")) {  // 2048-bucket splits: LDS write-combined spill, no dictionary (1) or not (-1)
-        c->hi_stage = v > 0;
+    } else if (!strcmp(name, "hi_stage")) {  // 2048-bucket splits: mini dictionary + LDS write-combined spill (default) or not (-1)
+        c->hi_stage = v >= 0;
     } else if (!strcmp(name, "long_records")) {  // wc: words of 17-32 bytes as key records (default) or offsets (-1)
         c->lrec_on = v >= 0;
     } else if (!strcmp(name, "lrec_cap")) {  // records per map workgroup region (tests of the overflow path)
-        c->lrec_cap = v > 0 ? (uint32_t)std::min<int64_t>(v, 1 << 26) : 4096u;
+        c->lrec_cap = v > 0 ? (uint32_t)std::min<int64_t>(v, 1 << 22) : 1024u;
     } else if (!strcmp(name, "grep_literal")) {  // grep: metacharacters quoted (1) instead of refused (0)
         c->grep_literal = v > 0;
     } else if (!strcmp(name, "tie_rank")) {  // grep reduce: tied runs ranked per run (1, default) or merge-sorted (0)

@@ -171,8 +171,9 @@ struct Tables {
     uint32_t* dict_cnt;     // [nwg][kDictSlots] per-map-workgroup dictionary counts
     unsigned long long* dbg;  // diagnostics (MRG_DEBUG_TIMES): per-workgroup s_memrealtime stamps, or nullptr
     // wc words of 17-32 bytes that end inside their map window: the key bytes as
-    // 32-byte zero-padded records (two uint4), region [map workgroup][lrec_cap];
-    // lrec_cnt[g] = records workgroup g appended (past lrec_cap: kStLrecFull).
+    // 32-byte zero-padded records (two uint4), one region of lrec_cap records per
+    // map wave ([workgroup][kWavesPerWG]); lrec_cnt[r] = records region r holds
+    // (past lrec_cap: kStLrecFull).
     // nullptr: every long word goes to the start-offset list (wc_long_kernel).
     uint4* lrec;
     uint32_t* lrec_cnt;

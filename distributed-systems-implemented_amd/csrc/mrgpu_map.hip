@@ -141,7 +141,7 @@ __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restr
 
 // Words of 17-32 bytes handed over by the map kernel as 32-byte zero-padded key
 // records (the map read them from its LDS window; no decode of the input here):
-// one workgroup per map workgroup's record region.  Each lane hashes a record
+// one workgroup per map workgroup's kWavesPerWG record regions (one per wave).  Each lane hashes a record
 // (FNV-1a-64 of its bytes, the same hash wc_long_kernel and the LongTable use,
 // so a word that reached the table by either path meets itself there) and counts
 // it in an LDS table confirmed by comparing the two records' 32 bytes (equal
@@ -160,8 +160,8 @@ __global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t) {
     __shared__ LrecLds A;
     const uint32_t g = blockIdx.x;
     const uint32_t cap = t.lrec_cap;
-    uint32_t n = t.lrec_cnt[g];
-    if (n > cap) n = cap;  // (overflowed regions are flagged; the map is repeated)
+    uint32_t n = 0;
+    for (int r = 0; r < kWavesPerWG; r++) n += t.lrec_cnt[g * kWavesPerWG + r];
     if (n == 0) return;
     for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
         A.h[i] = 0;
@@ -169,8 +169,10 @@ __global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t) {
         A.cnt[i] = 0;
     }
     __syncthreads();
-    const uint4* recs = t.lrec + (uint64_t)g * cap * 2;
-    for (uint32_t i = threadIdx.x; i < n; i += kLongWG) {
+    for (int r = 0; r < kWavesPerWG; r++)
+    for (uint32_t i = threadIdx.x, nr = min(t.lrec_cnt[g * kWavesPerWG + r], cap); i < nr; i += kLongWG) {
+        // (nr: overflowed regions are flagged and the map repeated)
+        const uint4* recs = t.lrec + ((uint64_t)g * kWavesPerWG + r) * cap * 2;
         const uint4 a = recs[2 * i], b = recs[2 * i + 1];
         const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
         uint64_t h = kFnv64Off;
@@ -888,7 +890,7 @@ __global__ void clear_tables_kernel(Tables t, bool short_table) {
         const uint64_t nc = 2ull * t.sp.nb * t.sp.nwg;
         for (uint64_t i = i0; i < nc; i += stride) t.sp.counts[i] = 0;
     }
-    if (t.lrec_cnt && i0 < (uint64_t)kMaxMapWGs) t.lrec_cnt[i0] = 0;  // (workgroups the map does not launch stay 0)
+    if (t.lrec_cnt && i0 < (uint64_t)kMaxMapWGs * kWavesPerWG) t.lrec_cnt[i0] = 0;  // (regions the map does not use stay 0)
     if (short_table)
         for (uint64_t i = i0; i <= t.sh_mask; i += stride) t.sh[i] = ShortSlot{0, kUnwritten, 0, 0};
     for (uint64_t i = i0; i <= t.lo_mask; i += stride) t.lo[i] = LongSlot{0, nullptr, 0, 0};

@@ -78,7 +78,6 @@ struct alignas(16) MapLdsT {
     // spill cursors: [0, NB) 8-byte streams, [NB, 2 NB) 16-byte streams, then per-lane dummies for hits
     uint32_t curs[2 * NB + kWave];
     uint32_t lt2[kLetterUnique * 8];            // letter tables (non-ASCII chunks): l2 pages
-    uint32_t lrec_n;                            // 32-byte long-word records this workgroup appended
     // letters among code points < U+0800 (2-byte runes: one table read), except
     // in the default 256-bucket layout (the others have no LDS left: l1 / l2 there)
     static constexpr bool kB2 = NB == kSpillBucketsLo;
@@ -401,7 +400,6 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         curs[b] = v;
         if (kS && b < (uint32_t)NB) L.fl[b] = (uint16_t)v;  // everything before the cursor is written
     }
-    if (tid == 0) L.lrec_n = resume && t.lrec ? t.lrec_cnt[blockIdx.x] : 0u;
     for (uint32_t i = tid; i < (uint32_t)kLetterUnique * 8; i += kT) L.lt2[i] = lt.l2[i];
     for (uint32_t i = tid; i < (uint32_t)kLetterLdsPages; i += kT) L.lt1[i] = lt.l1[i];
     if (MapLdsT<NW, NB, kS>::kB2 && tid < 64) L.lb2[tid] = lt.b2[tid];
@@ -426,6 +424,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         (void*)(t.sp.pool + (uint64_t)blockIdx.x * NB * sub), (short)0, (int)(NB * sub * 16u),
         0x00020000);
     uint32_t ovf = 0, utf8_chunks = 0;
+    // this wave's 32-byte long-word records so far (its own region: no atomic)
+    const uint32_t lreg = blockIdx.x * kWavesPerWG + wv;
+    uint32_t lrec_w = resume && t.lrec ? __builtin_amdgcn_readfirstlane(t.lrec_cnt[lreg]) : 0u;
     uint64_t acc = 0;
     // this wave's reserved range of the long-word list: [lbase, lbase + lleft)
     uint64_t lbase = 0;
@@ -675,13 +676,12 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             const uint32_t wl = (uint32_t)__builtin_ctzll((~win >> (p & 15u)) | (1ull << 63));
                             const uint64_t mR = tr.lrec != nullptr ? __ballot(have && wl <= 32u) : 0ull;
                             if (mR) {
-                                uint32_t rbase = 0;
-                                if (lane == 0) rbase = atomicAdd(&L.lrec_n, (uint32_t)__popcll(mR));
-                                rbase = __builtin_amdgcn_readfirstlane(rbase);
+                                const uint32_t rbase = lrec_w;
+                                lrec_w += (uint32_t)__popcll(mR);
                                 const uint32_t rcap = tr.lrec_cap;
                                 const uint32_t idx = rbase + mbcnt64(mR);
                                 const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-                                    (void*)(tr.lrec + (uint64_t)blockIdx.x * rcap * 2u), (short)0, (int)(rcap * 32u), 0x00020000);
+                                    (void*)(tr.lrec + (uint64_t)lreg * rcap * 2u), (short)0, (int)(rcap * 32u), 0x00020000);
                                 const uint32_t ro = __builtin_amdgcn_inverse_ballot_w64(mR) && idx < rcap ? idx * 32u : kOutOfRange;
                                 // the key's 32 bytes from the slot, zero past its length, 16 at a time
         #pragma unroll
@@ -700,7 +700,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                                                            ro == kOutOfRange ? kOutOfRange : ro + 16u * hf, 0, 0);
                                 }
                                 xv += 2;  // the two record stores (the next wait counts them)
-                                if (rbase + (uint32_t)__popcll(mR) > rcap && lane == 0) set_status(tr.ctr, kStLrecFull);
+                                if (lrec_w > rcap && lane == 0) set_status(tr.ctr, kStLrecFull);
                             }
 #endif
                             const uint64_t mFall = __ballot(have) & ~mR;
@@ -1043,7 +1043,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 if (f + j < sub8) t.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
         }
     }
-    if (tid == 0 && t.lrec) t.lrec_cnt[blockIdx.x] = L.lrec_n;
+    if (lane == 0 && t.lrec) t.lrec_cnt[lreg] = lrec_w;
     unsigned long long spilled = 0, hits = 0;
     for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {  // (this launch's share: minus the resumed values)
         const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[NB + b], sub);

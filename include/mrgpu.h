@@ -206,6 +206,11 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        previous split's aggregated keys (256 default,
  *                                        2048 high-cardinality; 512 the earlier default)
  *   spill_hi_keys                        aggregated keys above which 2048 are chosen
+ *   hi_stage (-1: off)                   2048-bucket splits: a 1088-key mini dictionary and
+ *                                        8-byte spill records write-combined in LDS (32-byte
+ *                                        stores; default) instead of the full dictionary
+ *   long_records (-1: off)               wc words of 17-32 bytes leave the map as 32-byte key
+ *                                        records (default) instead of the start-offset list
  *   agg_rounds, agg_carry_min, agg_big0 (0: by layout, 1 big, -1 small tables),
  *                                        agg_big_later   bucket aggregation rounds
  *   dict (-1: off), dict_warm (-1: off), dict_keep (permille; -1: always rebuild),

@@ -101,7 +101,7 @@ def test_wc_long_words_many(wctx, list_cap, lrec):
     """Mixed-script text with many words over 16 bytes, and splits made only of
     17-70-byte words: words of 17-32 bytes ending inside the map window leave as
     32-byte key records (lrec 0; lrec 8: 8-record regions that overflow, are
-    regrown from the busiest workgroup's count and re-run; -1: records off), the
+    regrown from the busiest map wave's count and re-run; -1: records off), the
     rest go to the map waves' reserved ranges of the long-word list with their
     closing holes (list overflow + re-run: a 300-entry list), and both long-word
     kernels' LDS pre-aggregation of hot long words."""
