@@ -249,7 +249,9 @@ struct mrg_ctx {
     int agg_big0 = 0;
     bool agg_big_later = true;
     double spill_scale = 1.0;           // spill stream capacity factor (from the dictionary sample's miss rate)
-    double words_per_byte = 0.0;        // words per input byte of the previous wc split (no-dictionary spill sizing)
+    double words_per_byte = 0.0;        // words per input byte of the previous wc split (staged spill sizing)
+    double spilled_per_byte = 0.0;      // spill records per input byte of the previous wc split
+    bool prev_staged = false;           // the previous wc split ran the staged map
     bool debug_times = getenv("MRG_DEBUG_TIMES") != nullptr;
     uint64_t rec_cap = 1u << 21;       // record output buffer capacity (grows on overflow)
     bool sh_clean = false;             // ShortTable known to be empty (skip its clear)
@@ -450,7 +452,11 @@ static int ensure_spill(mrg_ctx* c, uint64_t n) {
     c->spill_nwg = nwg;
     c->spill_sub_keys = sub;
     c->spill_sub8 = sub8;
-    HCHK(c, c->spool.ensure_grow((sub * sizeof(uint4) + sub8 * sizeof(uint64_t)) * nb * nwg));
+    const size_t pool = (sub * sizeof(uint4) + sub8 * sizeof(uint64_t)) * nb * nwg;
+    if (c->debug_times && pool > c->spool.cap)
+        fprintf(stderr, "[mrg spill] pool %.2f -> %.2f GB (scale %.3f, %llu buckets)\n", c->spool.cap / 1e9,
+                (pool + pool / 4) / 1e9, c->spill_scale, (unsigned long long)nb);
+    HCHK(c, c->spool.ensure_grow(pool));
     HCHK(c, c->spmeta.ensure((size_t)2 * nb * nwg * sizeof(uint32_t)));
     return MRG_OK;
 }
@@ -903,22 +909,28 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
     if (c->spill_alt) std::swap(c->spool.p, c->spool_alt.p), std::swap(c->spool.cap, c->spool_alt.cap);
     Ingest ing;
     if (host && (rc = ingest_start(c, ing, host, (uint8_t*)in, len))) return rc;
+    const bool staged = c->spill_nb == kSpillBucketsHi && c->hi_stage;  // (its kernel has the mini dictionary)
+    // The staged 2048-bucket map's streams are sized from the previous split (a
+    // worker's map tasks are alike), 30 % over: its spill records per byte if it
+    // ran staged too, else its words per byte (as if every word spilled: the mini
+    // dictionary takes few).  Set before the pool is sized, so it grows at most
+    // once; the sample's rate (measured with the level-1 dictionary) is not used.
+    if (staged) {
+        const double est = c->prev_staged ? c->spilled_per_byte : c->words_per_byte;
+        const double need = 1.3 * est / (2.0 * 0.75 / 16.0);
+        if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
+        if (c->debug_times)
+            fprintf(stderr, "[mrg spill] staged sizing: %s %.4f per byte -> scale %.3f\n",
+                    c->prev_staged ? "spilled" : "words", est, c->spill_scale);
+    }
     if ((rc = ensure_spill(c, len))) return rc;
     const uint32_t nwg = c->spill_nwg;
     HCHK(c, c->dict_cnt.ensure((size_t)nwg * kDictSlots * sizeof(uint32_t)));
     HCHK(c, hipEventRecord(c->ev[9], c->s));
     bool have_dict = false;
-    const bool staged = c->spill_nb == kSpillBucketsHi && c->hi_stage;  // (its kernel has the mini dictionary)
     if (c->dict_mode >= 0 && len >= c->dict_min_bytes && (rc = build_dict(c, in, len, lt, &have_dict, staged, host))) {
         ingest_finish(c, ing);
         return rc;
-    }
-    // the staged 2048-bucket map's mini dictionary takes few of the words (the
-    // sample's spill rate was measured with a full one): its streams are sized
-    // as if every word spilled, from the previous split's words per byte, 30 % over
-    if (staged && c->words_per_byte > 0) {
-        const double need = 1.3 * c->words_per_byte / (2.0 * 0.75 / 16.0);
-        if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
     }
     mark("dictionary");
     // the sample may have raised spill_scale: size the streams for this split now,
@@ -1002,7 +1014,11 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             h = *c->h_ctr;
         }
         c->arena_hint = h.long_bytes + h.long_bytes / 4;
-        if (len) c->words_per_byte = (double)(h.dict_hits + h.spilled + h.spill_ovf) / (double)len;
+        if (len) {
+            c->words_per_byte = (double)(h.dict_hits + h.spilled + h.spill_ovf) / (double)len;
+            c->spilled_per_byte = (double)(h.spilled + h.spill_ovf) / (double)len;
+            c->prev_staged = staged;
+        }
         if (h.status & kStLrecFull) {  // a record region filled up: size them for this split's busiest workgroup
             std::vector<uint32_t> cnt((size_t)nwg * kWavesPerWG);
             HCHK(c, hipMemcpy(cnt.data(), c->lrec_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
@@ -1025,6 +1041,18 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             const uint64_t agg_keys = h.nrec > (uint64_t)kDictSlots ? h.nrec - kDictSlots : 0;
             if (agg_keys > c->spill_hi_keys) c->next_nb = kSpillBucketsHi;
             else if (agg_keys < c->spill_hi_keys / 3 * 2) c->next_nb = kSpillBucketsLo;
+            // switching to the staged map: size its pool now (this split's words per
+            // byte, as the next call would), so the next split does not pay the
+            // reallocation (~2.4 s for C5's ~100 GB pool)
+            if (c->next_nb == kSpillBucketsHi && c->hi_stage && !staged && !c->spill_buckets_opt && len) {
+                const double need = 1.3 * c->words_per_byte / (2.0 * 0.75 / 16.0);
+                if (need > c->spill_scale) c->spill_scale = std::min(need, 8.0);
+                const uint32_t nb_now = c->spill_nb;
+                c->spill_nb = kSpillBucketsHi;
+                rc = ensure_spill(c, len);
+                c->spill_nb = nb_now;
+                if (rc) return rc;
+            }
         }
         // the parts object takes over the record buffer and arena (no copy); the
         // next map task gets cached blocks
