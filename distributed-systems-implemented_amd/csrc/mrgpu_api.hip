@@ -2401,10 +2401,40 @@ int mrg_run_job_async(mrg_ctx* c, int app, const void* buf, size_t len, int kind
     J.offsets.assign((size_t)use->nreduce + 1, 0);
     uint8_t* d = nullptr;
     uint64_t n = 0;
-    rc = reduce_common(c, use, 0xFFFFFFFFu, &d, &n, J.offsets.data());
+    // wc: the lines go straight into this job's pinned buffer (as mrg_run_job's),
+    // so there is no transfer left to overlap; grep: device buffer + the copy below
+    const bool direct_ok = c->out_direct && use->app == MRG_APP_WC;
+    if (direct_ok) {
+        const uint64_t bound = reduce_out_bound(use->r, use->app) + 1;
+        if (bound > J.cap) {
+            if (J.host) hipHostFree(J.host);
+            J.host = nullptr;
+            J.cap = 0;
+            const size_t cap = bound + bound / 4 + 4096;
+            if (hipHostMalloc((void**)&J.host, cap, hipHostMallocDefault) != hipSuccess) {
+                mrg_parts_free(use);
+                return fail(c, MRG_ENOMEM, "pinned output alloc");
+            }
+            J.cap = cap;
+        }
+    }
+    rc = reduce_common(c, use, 0xFFFFFFFFu, &d, &n, J.offsets.data(), direct_ok ? (uint8_t*)J.host : nullptr,
+                       direct_ok ? J.cap : 0);
     const uint64_t nkeys = use->r.n;
     mrg_parts_free(use);
     if (rc) return rc;
+    if (d == (uint8_t*)J.host && d) {  // written in place (the reduce ended with a stream synchronize)
+        HCHK(c, hipEventRecord(J.start, c->os));
+        HCHK(c, hipEventRecord(J.done, c->os));
+        keep.reduce_ms = ev_ms(c->ev[4], c->ev[5]);
+        keep.output_bytes = n;
+        keep.distinct_keys = nkeys;
+        J.n = n;
+        J.stats = keep;
+        c->stats = keep;
+        c->aj_count++;
+        return MRG_OK;
+    }
     if (n + 1 > J.cap) {
         if (J.host) hipHostFree(J.host);
         J.host = nullptr;

@@ -163,9 +163,11 @@ int mrg_run_job(mrg_ctx* ctx, int app, const void* buf, size_t len, int input_ki
  * cross PCIe on a second stream into a context-owned pinned buffer while the
  * caller queues the next job, whose map overlaps that transfer.  At most two
  * jobs are queued (a third call returns MRG_EINVAL); mrg_job_wait returns the
- * oldest queued job's output (bytes valid until the next mrg_job_wait on this
- * context; offsets[nreduce + 1] as mrg_run_job) and its stats (d2h_ms = its
- * transfer).  Any other reduce on the context first waits for queued transfers. */
+ * oldest queued job's output (bytes valid until the next mrg_run_job_async or
+ * mrg_job_wait on this context; offsets[nreduce + 1] as mrg_run_job) and its
+ * stats (d2h_ms = its transfer; wc jobs write their lines straight into the
+ * pinned buffer, as mrg_run_job does, and have none).  Any other reduce on the
+ * context first waits for queued transfers. */
 int mrg_run_job_async(mrg_ctx* ctx, int app, const void* buf, size_t len, int input_kind, const uint8_t* pat,
                       size_t plen, uint32_t nreduce);
 int mrg_job_wait(mrg_ctx* ctx, void** bytes, size_t* n, uint64_t* offsets);
