@@ -752,6 +752,7 @@ def main():
             "distinct_keys": int(last["distinct_keys"]),
             "dict_hit_words": int(last["dict_hits"]),
             "spilled_words": int(last["lds_overflow"]),
+            "spill_record_bytes": int(last.get("spill_record_bytes", 0)),
             "spill_region_full_words": int(last["spill_ovf"]),
             "aggregator_miss_words": int(last["agg_miss"]),
             "aggregation_rounds": int(last["agg_rounds"]),

@@ -1076,6 +1076,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         c->stats.collect_ms = ev_ms(c->ev[2], c->ev[3]);
         c->stats.lds_overflow = h.spilled + h.spill_ovf;
         c->stats.spill_ovf = h.spill_ovf;
+        c->stats.spill_record_bytes = 8 * (h.spilled - h.spilled16) + 16 * h.spilled16;
         c->stats.agg_miss = h.agg_miss;
         c->stats.agg_rounds = (uint64_t)__builtin_popcountll(h.round_mask);
         c->stats.spill_buckets = c->spill_nb;

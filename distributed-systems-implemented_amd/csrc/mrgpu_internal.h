@@ -66,6 +66,7 @@ struct Counters {
     unsigned long long nlines;     // grep: matching line occurrences resolved (one per line, not per hit)
     unsigned long long ndefer;     // grep: hits whose line bounds lie beyond a lane's scan window
     unsigned long long nrec_base;  // ctr->nrec before the collect (a collect-only retry restores it)
+    unsigned long long spilled16;  // of `spilled`: 16-byte records (keys of 9-16 bytes)
     unsigned long long pad[1];
 };
 

@@ -1044,12 +1044,13 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         }
     }
     if (lane == 0 && t.lrec) t.lrec_cnt[lreg] = lrec_w;
-    unsigned long long spilled = 0, hits = 0;
+    unsigned long long spilled = 0, hits = 0, sp16 = 0;
     for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {  // (this launch's share: minus the resumed values)
         const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[NB + b], sub);
         uint32_t* p16 = &t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x];
         uint32_t* p8 = &t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
         spilled += k + k8 - (resume ? *p16 + *p8 : 0u);
+        sp16 += k - (resume ? *p16 : 0u);
         *p16 = k;
         *p8 = k8;
     }
@@ -1063,6 +1064,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
     block_add4<NW>(&t.ctr->spilled, &t.ctr->dict_hits, &t.ctr->spill_ovf, &t.ctr->chunks_utf8, spilled, hits,
                             ovf, lane == 0 ? utf8_chunks : 0, (unsigned long long*)&L.ring[0][0][0]);
+    block_add4<NW>(&t.ctr->spilled16, nullptr, nullptr, nullptr, sp16, 0, 0, 0, (unsigned long long*)&L.ring[0][0][0]);
     if (t.dbg && tid == 0) t.dbg[2 * (NB + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -2166,7 +2168,7 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M, kWavesPerWG, kSpillBucketsLo><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;
             MRG_MAP_MODE(1) MRG_MAP_MODE(2) MRG_MAP_MODE(4) MRG_MAP_MODE(8) MRG_MAP_MODE(16) MRG_MAP_MODE(32)
-            MRG_MAP_MODE(64) MRG_MAP_MODE(64 | 2)
+            MRG_MAP_MODE(64) MRG_MAP_MODE(64 | 2) MRG_MAP_MODE(0x100)
 #undef MRG_MAP_MODE
             default: wc_map_kernel<0, kWavesPerWG, kSpillBucketsLo><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
         }

@@ -79,6 +79,7 @@ class Stats(ctypes.Structure):
         ("rccl_nranks", ctypes.c_int64),
         ("rccl_rank", ctypes.c_int64),
         ("device", ctypes.c_int64),
+        ("spill_record_bytes", ctypes.c_uint64),
     ]
 
     def as_dict(self):

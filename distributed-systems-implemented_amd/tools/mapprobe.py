@@ -60,7 +60,8 @@ def main():
             r = {"grid": g, "mode": m, "map_kernel_ms": min(ts), "GBps": buf.size / min(ts) / 1e6,
                  "map_total_ms": st["map_total_ms"], "agg_ms": st["agg_ms"], "long_ms": st["long_ms"],
                  "collect_ms": st["collect_ms"], "spilled": st["lds_overflow"], "agg_miss": st["agg_miss"],
-                 "dict_ms": st["dict_ms"], "dict_hits": st["dict_hits"]}
+                 "dict_ms": st["dict_ms"], "dict_hits": st["dict_hits"],
+                 "spill_record_bytes": st.get("spill_record_bytes", 0)}
             print(json.dumps(r), flush=True)
             res.append(r)
     ctx.set_option("map_mode", 0)

@@ -105,6 +105,7 @@ typedef struct {
                                  0 for mrg_exchange_group (peer copies) or no exchange */
     int64_t rccl_rank;        /* exchange: this context's rank per ncclCommUserRank (-1: none) */
     int64_t device;           /* the HIP device this context drives (ncclCommCuDevice when attached) */
+    uint64_t spill_record_bytes; /* wc map: bytes of spill records written (8 per short key, 16 per 9-16-byte key) */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);
