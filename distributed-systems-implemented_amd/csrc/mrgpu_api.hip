@@ -252,6 +252,8 @@ struct mrg_ctx {
     double words_per_byte = 0.0;        // words per input byte of the previous wc split (staged spill sizing)
     double spilled_per_byte = 0.0;      // spill records per input byte of the previous wc split
     bool prev_staged = false;           // the previous wc split ran the staged map
+    bool prev_ascii = false;            // the previous wc split had no UTF-8 chunk (its map: the lean variant)
+    bool lean_on = true;                // option map_lean (-1: never the lean variant)
     bool debug_times = getenv("MRG_DEBUG_TIMES") != nullptr;
     uint64_t rec_cap = 1u << 21;       // record output buffer capacity (grows on overflow)
     bool sh_clean = false;             // ShortTable known to be empty (skip its clear)
@@ -407,6 +409,7 @@ static Tables make_tables(mrg_ctx* c) {
     t.dict_cnt = (uint32_t*)c->dict_cnt.p;
     t.dbg = c->debug_times && c->dbg.ensure(2 * (kSpillBucketsHi + kMaxMapWGs) * 8) == hipSuccess ? (unsigned long long*)c->dbg.p : nullptr;
     t.hi_staged = 0;
+    t.lean = 0;
     t.lrec = nullptr;  // set by wc_map for the split's map (sample maps and grep use the offset list)
     t.lrec_cnt = nullptr;
     t.lrec_cap = 0;
@@ -950,6 +953,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         Tables t = make_tables(c);
         t.dict = have_dict ? (const uint4*)c->dict.p : nullptr;
         t.hi_staged = staged ? 1u : 0u;
+        t.lean = c->lean_on && c->prev_ascii ? 1u : 0u;
         t.nreduce = nreduce;
         t.out = rec_view(c);
         t.out_cap = c->rec_cap;
@@ -1018,6 +1022,7 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             c->words_per_byte = (double)(h.dict_hits + h.spilled + h.spill_ovf) / (double)len;
             c->spilled_per_byte = (double)(h.spilled + h.spill_ovf) / (double)len;
             c->prev_staged = staged;
+            c->prev_ascii = h.chunks_utf8 == 0;
         }
         if (h.status & kStLrecFull) {  // a record region filled up: size them for this split's busiest workgroup
             std::vector<uint32_t> cnt((size_t)nwg * kWavesPerWG);
@@ -1333,6 +1338,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         c->out_direct = v >= 0;
     } else if (!strcmp(name, "hi_stage")) {  // 2048-bucket splits: mini dictionary + LDS write-combined spill (default) or not (-1)
         c->hi_stage = v >= 0;
+    } else if (!strcmp(name, "map_lean")) {  // wc: the all-ASCII map variant after an all-ASCII split (default) or never (-1)
+        c->lean_on = v >= 0;
     } else if (!strcmp(name, "long_records")) {  // wc: words of 17-32 bytes as key records (default) or offsets (-1)
         c->lrec_on = v >= 0;
     } else if (!strcmp(name, "lrec_cap")) {  // records per map workgroup region (tests of the overflow path)

@@ -310,7 +310,6 @@ __device__ __forceinline__ uint32_t flags_to_bits16(uint32_t f0, uint32_t f1, ui
 // 15 is used, which depends on bytes >= 9).
 // The letter bits (relative to q0 - 3) of the rune whose lead byte is at q0 - 3
 // + i, given its 4 bytes w (Go's acceptance ranges; 0 if invalid or no letter).
-// Split in two halves so that two leads' LDS reads can be in flight together:
 // lead_decode gives the code point, its continuation count and validity;
 // lead_word the table word holding its letter bit.
 struct LeadRune {
@@ -348,10 +347,10 @@ __device__ __forceinline__ uint32_t lead_word(const LeadRune& r, LdsLetters L) {
 //     acceptance ranges and, if valid and a letter, marks all its bytes;
 //   - continuation bytes outside a valid sequence and invalid leads are
 //     U+FFFD, not letters (nothing to do).
-// Work is one loop turn per TWO lead bytes of the lane (their LDS reads in
-// flight together: the rune bytes, then the table word).  first: the look-back
-// lane (q0 = 0), whose bytes before the slot read as 0 (only its bit 15 is used,
-// which depends on bytes >= 9).
+// Work is one loop turn per lead byte of the lane (a two-leads-per-turn version
+// measured slower: C2u map 23.0 vs 18.3 ms).  first: the look-back lane (q0 =
+// 0), whose bytes before the slot read as 0 (only its bit 15 is used, which
+// depends on bytes >= 9).
 __device__ __forceinline__ uint32_t utf8_mask16(const lds_u8* slot, uint32_t q0, bool first, LdsLetters L) {
     const lds_u32* s4 = (const lds_u32*)(slot + q0);
     const uint32_t w0 = first ? 0u : s4[-1], w1 = s4[0], w2 = s4[1], w3 = s4[2], w4 = s4[3];
@@ -360,17 +359,11 @@ __device__ __forceinline__ uint32_t utf8_mask16(const lds_u8* slot, uint32_t q0,
     uint32_t leads = (flags_to_bits16(lead_flags4(w0), lead_flags4(w1), lead_flags4(w2), lead_flags4(w3)) >> 1) |
                      (flags_to_bits16(lead_flags4(w4), 0u, 0u, 0u) << 15);
     while (leads) {
-        const uint32_t i1 = __builtin_ctz(leads);
+        const uint32_t i = __builtin_ctz(leads);
         leads &= leads - 1;
-        const bool two = leads != 0;
-        const uint32_t i2 = two ? __builtin_ctz(leads) : i1;
-        leads &= leads - 1;  // (no-op when none was left)
-        const uint32_t wa = *(const lds_u32_unaligned*)(slot + q0 + i1 - 3);
-        const uint32_t wb = *(const lds_u32_unaligned*)(slot + q0 + i2 - 3);
-        const LeadRune ra = lead_decode(wa), rb = lead_decode(wb);
-        const uint32_t ta = lead_word(ra, L), tb = lead_word(rb, L);
-        if (ra.valid && ((ta >> (ra.cp & 31u)) & 1u)) m |= ((((2u << ra.need) - 1u) << i1) >> 3) & 0xFFFFu;
-        if (two && rb.valid && ((tb >> (rb.cp & 31u)) & 1u)) m |= ((((2u << rb.need) - 1u) << i2) >> 3) & 0xFFFFu;
+        const LeadRune r = lead_decode(*(const lds_u32_unaligned*)(slot + q0 + i - 3));
+        const uint32_t tw = lead_word(r, L);
+        if (r.valid && ((tw >> (r.cp & 31u)) & 1u)) m |= ((((2u << r.need) - 1u) << i) >> 3) & 0xFFFFu;
     }
     return m;
 }

@@ -182,6 +182,7 @@ struct Tables {
     // 2048-bucket layout without a dictionary: the map kernel variant that
     // write-combines its 8-byte spill streams in LDS (mrgpu_wc.hip, kS)
     uint32_t hi_staged;
+    uint32_t lean;          // wc map: the all-ASCII variant (the previous split had no UTF-8 chunk)
 };
 
 struct LetterTables {

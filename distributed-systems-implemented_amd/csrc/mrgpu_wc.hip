@@ -200,29 +200,22 @@ __device__ __forceinline__ void wait_vmem_iter_wide() {
     asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
 }
 __device__ __forceinline__ void wait_vmem_all() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
-// vmcnt(n) for a wave-uniform n (the counted wait after an iteration that issued
-// extra VMEM operations: long-word records, the start-offset list).  n must not
-// exceed the operations issued after the awaited DMA (fewer only waits longer);
-// past 15 it waits for vmcnt(15).
+// The counted wait after an iteration that issued xv VMEM operations beyond
+// the loop's base count B (long-word record and list stores, appends from the
+// word slots): vmcnt(B + x) for the largest x in {0, 1, 2, 4} not above xv (a
+// smaller count only waits longer).  A short compare chain: a full switch over
+// xv compiled to a jump table whose SGPRs pushed 8 more of the loop's scalars
+// into VGPR-lane spills.
 template <int N>
 __device__ __forceinline__ void vmcnt_imm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
-__device__ __forceinline__ void wait_vmem_upto(uint32_t n) {
-    switch (n) {
-        case 3: vmcnt_imm<3>(); break;
-        case 4: vmcnt_imm<4>(); break;
-        case 5: vmcnt_imm<5>(); break;
-        case 6: vmcnt_imm<6>(); break;
-        case 7: vmcnt_imm<7>(); break;
-        case 8: vmcnt_imm<8>(); break;
-        case 9: vmcnt_imm<9>(); break;
-        case 10: vmcnt_imm<10>(); break;
-        case 11: vmcnt_imm<11>(); break;
-        case 12: vmcnt_imm<12>(); break;
-        case 13: vmcnt_imm<13>(); break;
-        case 14: vmcnt_imm<14>(); break;
-        default: vmcnt_imm<15>(); break;
-    }
+template <int B>
+__device__ __forceinline__ void wait_vmem_extra(uint32_t xv) {
+    if (xv >= 4) vmcnt_imm<B + 4>();
+    else if (xv >= 2) vmcnt_imm<B + 2>();
+    else if (xv == 1) vmcnt_imm<B + 1>();
+    else vmcnt_imm<B>();
 }
+
 // The staged (kS) loop: the flush's 4 stores and the DMA follow the awaited DMA
 __device__ __forceinline__ void wait_vmem_iter_staged() { asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); }
 
@@ -359,7 +352,7 @@ __device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint
 // sc1, 0x8000 = sc0 sc1)
 constexpr int dma_policy(uint32_t mode) { return (mode & 0x100) ? 0 : (mode & 0x4000) ? 2 : (mode & 0x8000) ? 3 : 1; }
 
-template <uint32_t mode, int NW = kWavesPerWG, int NB = kSpillBuckets, bool kS = false>
+template <uint32_t mode, int NW = kWavesPerWG, int NB = kSpillBuckets, bool kS = false, bool kLean = false>
 __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t cbeg,
                                                           uint32_t cend, uint32_t ctail, int resume, Tables t,
                                                           LetterTables lt) {
@@ -425,8 +418,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         0x00020000);
     uint32_t ovf = 0, utf8_chunks = 0;
     // this wave's 32-byte long-word records so far (its own region: no atomic)
-    const uint32_t lreg = blockIdx.x * kWavesPerWG + wv;
-    uint32_t lrec_w = resume && t.lrec ? __builtin_amdgcn_readfirstlane(t.lrec_cnt[lreg]) : 0u;
+    // (in a VGPR, uniform: an SGPR live across the loop would be spilled)
+    uint32_t lrec_w = resume && t.lrec ? t.lrec_cnt[blockIdx.x * kWavesPerWG + wv] : 0u;
+    asm volatile("" : "+v"(lrec_w));
     uint64_t acc = 0;
     // this wave's reserved range of the long-word list: [lbase, lbase + lleft)
     uint64_t lbase = 0;
@@ -449,11 +443,12 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // kf = the free slot (the word list now, chunk c + 2*stride next) = the slot
     // before k; both rotate as loop-carried scalars
     uint32_t kf = kRing - 1;
-    // spill store instructions the previous iteration issued after the DMA now
-    // awaited: 2 (staged appends) or kVmemWide (appends from the word slots)
-    bool wide_prev = false;
-    // VMEM operations the previous iteration issued beyond those counted above
-    // (only ones it certainly issued: an uncounted one only lengthens the wait)
+    // VMEM operations the previous iteration issued after the DMA now awaited,
+    // beyond the base count (2 spill stores + the DMA; kS: 4 flush stores + the
+    // DMA): kVmemWide - 2 after appends from the word slots, plus long-word record
+    // and list stores.  Only operations it certainly issued are counted (an
+    // uncounted one only lengthens the wait).  One scalar: the loop's SGPRs are
+    // scarce (hipcc spills the excess to VGPR lanes, reloaded every chunk).
     uint32_t xv = 0;
     // kS: every wave runs the workgroup's trip count (its barriers), a chunk past
     // cend counting as empty
@@ -463,14 +458,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     for (uint32_t c = c0; kS ? trip < ktrips : c < cend;
          c += stride, cs += cstep, kf = k, k = k == kRing - 1 ? 0 : k + 1, trip++) {
         // chunk c's DMA (issued two iterations ago) has landed
-        if (xv == 0) {
-            if constexpr (kS) wait_vmem_iter_staged();
-            else if (wide_prev) wait_vmem_iter_wide();
-            else wait_vmem_iter();
-        } else {
-            wait_vmem_upto((kS ? 5u : wide_prev ? (uint32_t)kVmemWide + 1u : (uint32_t)kVmemPerIter) + xv);
-        }
-        wide_prev = false;
+        if constexpr (kS) wait_vmem_extra<5>(xv);
+        else wait_vmem_extra<kVmemPerIter>(xv);
         xv = 0;
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
         const uint32_t bufa = ring0 + k * kSlotStride;  // = lds_addr(buf)
@@ -518,11 +507,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     wait_vmem_all();
                     wave_sync();
                 }
-#if MRG_UTF8_WAVE
-                mA = utf8_mask16_wave(buf, lane, (lds_u8*)L.ring[wv][kf], lds_lt);
-#else
-                mA = utf8_mask16(buf, 16 * lane, lane == 0, lds_lt);
-#endif
+                if constexpr (MRG_UTF8_WAVE && !kLean) mA = utf8_mask16_wave(buf, lane, (lds_u8*)L.ring[wv][kf], lds_lt);
+                else mA = utf8_mask16(buf, 16 * lane, lane == 0, lds_lt);
             }
             if (kS && c >= cend) mA = 0;  // a trip past this wave's last chunk: nothing to count
             // Word starts (a letter byte whose predecessor is not one) in the owned lanes
@@ -638,7 +624,51 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     // 207 ms per 10 GB), with one store per chunk: the starts are staged
                     // in the list slot, whose entries are all read by now (one pass).
                     // The extra stores are counted (xv) by the next iteration's wait.
-                    if (mLng[0] | mLng[1] | mLng[2]) {
+                    if (kLean && (mLng[0] | mLng[1] | mLng[2])) {
+                        // kLean (splits whose predecessor was all ASCII): every long word
+                        // through the start-offset list, the round-3 code, which keeps
+                        // the loop's scalars out of VGPR-lane spills (the record path
+                        // below costs the ASCII loop ~2 %)
+                        if (passes == 1) {
+                            lds_u64* lst = (lds_u64*)L.ring[wv][kf];
+                            uint32_t nlong = 0;
+        #pragma unroll
+                            for (int u = 0; u < kBatch; u++) {
+                                if (__builtin_amdgcn_inverse_ballot_w64(mLng[u]))
+                                    lst[nlong + mbcnt64(mLng[u])] = cs - kBack + (e[u] & 0x3FFu);
+                                nlong += (uint32_t)__popcll(mLng[u]);
+                            }
+                            const Tables& tc = cold(t);
+                            if (nlong > lleft) {  // a fresh range (rare): close the old one, one atomic, drain
+                                list_close(tc, lbase, lleft, lane);
+                                const uint32_t want = kLongReserve;
+                                unsigned long long b0 = 0;
+                                if (lane == 0) b0 = atomicAdd(&tc.ctr->nlist, (unsigned long long)want);
+                                lbase = readfirstlane64(b0);
+                                lleft = want;
+                                if (lbase + want > tc.list_cap && lane == 0) set_status(tc.ctr, kStListFull);
+                                wait_vmem_all();
+                            }
+                            uint64_t* lptr;
+                            uint64_t lcap;
+                            cold_list(t, lptr, lcap);
+                            const uint64_t room = lbase < lcap ? lcap - lbase : 0;
+                            const __amdgpu_buffer_rsrc_t rsl = __builtin_amdgcn_make_buffer_rsrc(
+                                (void*)(lptr + lbase), (short)0, (int)(room < (0xFFFFFF00ull >> 3) ? room * 8u : 0xFFFFFF00ull),
+                                0x00020000);
+                            const unsigned long long v = lst[lane];  // nlong <= 59 (> 16-byte words of 992 bytes)
+                            __builtin_amdgcn_raw_buffer_store_b64((u32x2){(uint32_t)v, (uint32_t)(v >> 32)}, rsl,
+                                                                  lane < nlong ? lane * 8u : kOutOfRange, 0, 0);
+                            xv += 1;
+                            lbase += nlong;
+                            lleft -= nlong;
+                        } else {  // several passes (> 192 words): the list slot is still needed
+        #pragma unroll
+                            for (int u = 0; u < kBatch; u++)
+                                if (__builtin_amdgcn_inverse_ballot_w64(mLng[u])) list_append(cold(t), cs - kBack + (e[u] & 0x3FFu));
+                            wait_vmem_all();
+                        }
+                    } else if (mLng[0] | mLng[1] | mLng[2]) {
                         if (passes == 1) {
                             // Words of 17-32 bytes that end inside the window leave as
                             // 32-byte key records, read here from the slot (wc_lrec_kernel
@@ -676,12 +706,13 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             const uint32_t wl = (uint32_t)__builtin_ctzll((~win >> (p & 15u)) | (1ull << 63));
                             const uint64_t mR = tr.lrec != nullptr ? __ballot(have && wl <= 32u) : 0ull;
                             if (mR) {
-                                const uint32_t rbase = lrec_w;
-                                lrec_w += (uint32_t)__popcll(mR);
+                                const uint32_t rbase = __builtin_amdgcn_readfirstlane(lrec_w);
+                                lrec_w = rbase + (uint32_t)__popcll(mR);
+                                asm volatile("" : "+v"(lrec_w));
                                 const uint32_t rcap = tr.lrec_cap;
                                 const uint32_t idx = rbase + mbcnt64(mR);
                                 const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
-                                    (void*)(tr.lrec + (uint64_t)lreg * rcap * 2u), (short)0, (int)(rcap * 32u), 0x00020000);
+                                    (void*)(tr.lrec + (uint64_t)(blockIdx.x * kWavesPerWG + wv) * rcap * 2u), (short)0, (int)(rcap * 32u), 0x00020000);
                                 const uint32_t ro = __builtin_amdgcn_inverse_ballot_w64(mR) && idx < rcap ? idx * 32u : kOutOfRange;
                                 // the key's 32 bytes from the slot, zero past its length, 16 at a time
         #pragma unroll
@@ -700,7 +731,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                                                            ro == kOutOfRange ? kOutOfRange : ro + 16u * hf, 0, 0);
                                 }
                                 xv += 2;  // the two record stores (the next wait counts them)
-                                if (lrec_w > rcap && lane == 0) set_status(tr.ctr, kStLrecFull);
+                                if (rbase + (uint32_t)__popcll(mR) > rcap && lane == 0) set_status(tr.ctr, kStLrecFull);
                             }
 #endif
                             const uint64_t mFall = __ballot(have) & ~mR;
@@ -984,7 +1015,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     // several passes: a different count, drain
                     // (2048 buckets: drained — the 4096 streams per workgroup then leave
                     // L2 less fragmented: C5 map 39.8 ms counted vs 35.5 drained)
-                    if (passes == 1 && NB != kSpillBucketsHi) wide_prev = true;
+                    if (passes == 1 && NB != kSpillBucketsHi) xv += (uint32_t)kVmemWide - 2u;
                     else wait_vmem_all();
                 }
             }
@@ -1043,7 +1074,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 if (f + j < sub8) t.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
         }
     }
-    if (lane == 0 && t.lrec) t.lrec_cnt[lreg] = lrec_w;
+    if (lane == 0 && t.lrec) t.lrec_cnt[blockIdx.x * kWavesPerWG + wv] = lrec_w;
     unsigned long long spilled = 0, hits = 0, sp16 = 0;
     for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {  // (this launch's share: minus the resumed values)
         const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[NB + b], sub);
@@ -2164,6 +2195,10 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
         return true;
     }
     if (t.sp.nb == kSpillBucketsLo) {  // the default layout (ablation modes: mapprobe.py)
+        if (t.lean && mode == 0) {  // splits after an all-ASCII one: fewer scalars spilled in the loop
+            wc_map_kernel<0, kWavesPerWG, kSpillBucketsLo, false, true><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
+            return true;
+        }
         switch (mode) {
 #define MRG_MAP_MODE(M) \
     case M: wc_map_kernel<M, kWavesPerWG, kSpillBucketsLo><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); break;

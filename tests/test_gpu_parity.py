@@ -96,6 +96,24 @@ def test_wc_synthetic(wctx, kind, V, seed, inv):
         assert wctx.stats()["dict_hits"] > 0
 
 
+@pytest.mark.parametrize("lean", [0, -1])
+def test_wc_lean_after_ascii(wctx, lean):
+    """A split after an all-ASCII one maps with the lean variant (long words all
+    through the start-offset list, UTF-8 by the per-lane lead loop): exact on
+    mixed-script text with long words, on the window-end and invalid UTF-8
+    cases, and on ASCII again; lean -1 keeps the full variant."""
+    wctx.set_option("map_lean", lean)
+    ascii = cases.synthetic(C.KIND_ASCII, 20000, [1_000_000], 31)
+    mixed = cases.synthetic(C.KIND_UTF8, 20000, [1_500_000], 32, 0.0005) + [cases.long_words(500_000, 3)]
+    edge = cases.edge_cases()
+    try:
+        for f in [ascii[0], mixed[0], ascii[0], mixed[1], ascii[0]] + edge["utf8_slot_tail"] + [ascii[0]] + \
+                edge["invalid_utf8"]:
+            assert gpu_partitioned(wctx, "wc", [f], 10) == O.c_partitioned("wc", [f], 10)
+    finally:
+        wctx.set_option("map_lean", 0)
+
+
 @pytest.mark.parametrize("list_cap,lrec", [(0, 0), (300, 0), (0, 8), (300, -1)])
 def test_wc_long_words_many(wctx, list_cap, lrec):
     """Mixed-script text with many words over 16 bytes, and splits made only of
