@@ -725,7 +725,10 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
             return rc;
         // a warm dictionary that still hits this split's sample about as well as it
         // hit its own split is kept: the candidate sort and placement are skipped
-        const bool keep = warm && c->dict_keep > 0 && c->dict_frac_built > 0 && frac >= c->dict_keep * c->dict_frac_built;
+        // (or within half a point of it: the mini dictionary hits ~13 % of C5's
+        // words, where 3 % relative is sample noise and a rebuild costs ~1 ms)
+        const bool keep = warm && c->dict_keep > 0 && c->dict_frac_built > 0 &&
+                          (frac >= c->dict_keep * c->dict_frac_built || frac >= c->dict_frac_built - 0.005);
         c->dict_fresh = !keep;
         if (!keep && nrec && (rc = dict_from_recs(c, nrec, mini))) return rc;
         // Spill streams hold 0.094 8-byte records per input byte at scale 1 (C2

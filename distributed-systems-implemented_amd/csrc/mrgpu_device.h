@@ -294,24 +294,9 @@ __device__ __forceinline__ uint32_t flags_to_bits16(uint32_t f0, uint32_t f1, ui
     return (lo | (hi << 8)) >> 7;
 }
 
-// Letter mask of the 16 slot bytes [q0, q0 + 16) with Go's decoding semantics
-// (strings.FieldsFunc's range loop + unicode.IsLetter, mrapps/wc.go:23,26;
-// SURVEY.md Appendix A.1), for a slot in LDS whose bytes [q0 - 4, q0 + 19) are
-// readable:
-//   - ASCII letters by SWAR;
-//   - every lead byte (>= 0xC0) in [q0 - 3, q0 + 16) starts a rune: a lead is
-//     never a continuation byte, so no valid sequence can cover it (the local
-//     rune-start rule always holds); its sequence is checked with Go's
-//     acceptance ranges and, if valid and a letter, marks all its bytes;
-//   - continuation bytes outside a valid sequence and invalid leads are
-//     U+FFFD, not letters (nothing to do).
-// Work is one loop turn per lead byte of the lane (LDS reads only).  first: the
-// look-back lane (q0 = 0), whose bytes before the slot read as 0 (only its bit
-// 15 is used, which depends on bytes >= 9).
-// The letter bits (relative to q0 - 3) of the rune whose lead byte is at q0 - 3
-// + i, given its 4 bytes w (Go's acceptance ranges; 0 if invalid or no letter).
-// lead_decode gives the code point, its continuation count and validity;
-// lead_word the table word holding its letter bit.
+// One lead byte's rune (Go's acceptance ranges):
+// lead_decode gives the code point, its continuation count and validity from the
+// rune's 4 bytes w; lead_word the table word holding its letter bit.
 struct LeadRune {
     uint32_t cp, need;
     bool valid;
