@@ -74,6 +74,30 @@ def log(msg):
     print(f"[bench r{os.environ.get('RANK', '0')}] {msg}", file=sys.stderr, flush=True)
 
 
+class heartbeat:
+    """A progress line every `every` s while a long host-side step runs (the
+    full-size oracle check of C5 takes minutes; a silent GPU box command is
+    taken to be hung)."""
+
+    def __init__(self, what: str, every: float = 30.0):
+        import threading
+        self.what, self.every, self.stop = what, every, threading.Event()
+        self.t = threading.Thread(target=self._run, daemon=True)
+
+    def _run(self):
+        t0 = time.time()
+        while not self.stop.wait(self.every):
+            log(f"{self.what}: {time.time() - t0:.0f} s")
+
+    def __enter__(self):
+        self.t.start()
+        return self
+
+    def __exit__(self, *exc):
+        self.stop.set()
+        self.t.join()
+
+
 def file_params(w: dict, i: int, nfiles: int):
     if w["app"] == "grep":
         return C.grep_params(PATTERN)
@@ -505,10 +529,11 @@ def main():
     nsplits = args.splits if args.splits > 0 else (3 if world == 1 else 2)
     t0 = time.time()
     devs = []
-    for sp in range(nsplits):
-        host = gen_corpus(w, rank, args.file_mb, args.files, sp)
-        devs.append(upload(host, local))
-        del host
+    with heartbeat("generating the splits"):
+        for sp in range(nsplits):
+            host = gen_corpus(w, rank, args.file_mb, args.files, sp)
+            devs.append(upload(host, local))
+            del host
     nbytes = int(devs[0].numel())
     log(f"generated {nsplits} x {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
 
@@ -601,7 +626,8 @@ def main():
         p, n, offs = run_step(sp)
         out = ctypes.string_at(p, n) if n else b""
         parts = [out[offs[i]:offs[i + 1]] for i in range(args.nreduce)]
-        ck = check_output(parts, args.nreduce, w["app"])
+        with heartbeat(f"output checks of split {sp}"):
+            ck = check_output(parts, args.nreduce, w["app"])
         if sp == 0:
             ck["deterministic"] = hashlib.sha256(out).hexdigest() == hashlib.sha256(
                 ctypes.string_at(*run_step(0)[:2])).hexdigest()
@@ -621,8 +647,9 @@ def main():
                 ck["total_words_independent"] = int(ti.item())
                 ck["total_words_match"] = ck["total_words_independent"] == ck[key]
         if not args.no_oracle and not shared:
-            host = download(devs[sp])
-            ck.update(oracle_exact_check(w, host, parts, args.nreduce, rank, world))
+            with heartbeat(f"oracle check of split {sp}"):
+                host = download(devs[sp])
+                ck.update(oracle_exact_check(w, host, parts, args.nreduce, rank, world))
             del host
         del out, parts
         per_split.append(ck)
