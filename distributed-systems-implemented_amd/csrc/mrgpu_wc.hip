@@ -418,15 +418,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         0x00020000);
     uint32_t ovf = 0, utf8_chunks = 0;
     // this wave's 32-byte long-word records so far (its own region: no atomic)
-    // (in a VGPR, uniform: an SGPR live across the loop would be spilled; the
-    // lean variant writes no records; the count array's address through cold():
-    // kept in SGPRs across the loop it cost 9 more spilled scalars)
-    uint32_t lrec_w = 0;
-    if constexpr (!kLean) {
-        const Tables& tq = cold(t);
-        if (resume && tq.lrec) lrec_w = tq.lrec_cnt[blockIdx.x * kWavesPerWG + wv];
-        asm volatile("" : "+v"(lrec_w));
-    }
+    // (in a VGPR, uniform: an SGPR live across the loop would be spilled)
+    uint32_t lrec_w = resume && t.lrec ? t.lrec_cnt[blockIdx.x * kWavesPerWG + wv] : 0u;
+    asm volatile("" : "+v"(lrec_w));
     uint64_t acc = 0;
     // this wave's reserved range of the long-word list: [lbase, lbase + lleft)
     uint64_t lbase = 0;
@@ -1048,9 +1042,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 __builtin_amdgcn_raw_buffer_store_b128(lo, rs8, whole ? o : kOutOfRange, 0, 0);
                 __builtin_amdgcn_raw_buffer_store_b128(hi, rs8, whole ? o + 16u : kOutOfRange, 0, 0);
                 if (grp && !whole) {  // the group reaches past the stream's capacity: its records below it
-                    const Tables& tc = cold(t);
                     for (uint32_t j = 0; j < 4u; j++)
-                        if (f + j < sub8) tc.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
+                        if (f + j < sub8) t.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
                     rare = true;
                 }
                 if (grp) L.fl[b] = (uint16_t)cc;
@@ -1069,10 +1062,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             ds.set(cin, cn, cs + 3 * cstep);
         }
     }
-    // (the tail reads the Tables fields through cold(): kernarg values the
-    // compiler would otherwise keep in SGPRs across the loop)
-    const Tables& tt = cold(t);
-    list_close(tt, lbase, lleft, lane);
+    list_close(t, lbase, lleft, lane);
     wait_vmem_all();  // the ring's last DMAs land before the workgroup's LDS is reused
 
     __syncthreads();
@@ -1081,33 +1071,32 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             const uint32_t cc = curs[b];
             const uint32_t f = cc - ((cc - (uint32_t)L.fl[b]) & 0xFFFFu);
             for (uint32_t j = 0; f + j < cc; j++)
-                if (f + j < sub8) tt.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
+                if (f + j < sub8) t.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
         }
     }
-    if constexpr (!kLean)
-        if (lane == 0 && tt.lrec) tt.lrec_cnt[blockIdx.x * kWavesPerWG + wv] = lrec_w;
+    if (lane == 0 && t.lrec) t.lrec_cnt[blockIdx.x * kWavesPerWG + wv] = lrec_w;
     unsigned long long spilled = 0, hits = 0, sp16 = 0;
     for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {  // (this launch's share: minus the resumed values)
         const uint32_t k8 = min((uint32_t)curs[b], sub8), k = min((uint32_t)curs[NB + b], sub);
-        uint32_t* p16 = &tt.sp.counts[(uint64_t)b * tt.sp.nwg + blockIdx.x];
-        uint32_t* p8 = &tt.sp.counts8[(uint64_t)b * tt.sp.nwg + blockIdx.x];
+        uint32_t* p16 = &t.sp.counts[(uint64_t)b * t.sp.nwg + blockIdx.x];
+        uint32_t* p8 = &t.sp.counts8[(uint64_t)b * t.sp.nwg + blockIdx.x];
         spilled += k + k8 - (resume ? *p16 + *p8 : 0u);
         sp16 += k - (resume ? *p16 : 0u);
         *p16 = k;
         *p8 = k8;
     }
-    if (tt.dict != nullptr)
+    if (use_dict)
         for (uint32_t i = tid; i < (uint32_t)Geo::kSlots; i += kT) {
             const uint32_t v = dcnt[i];
-            uint32_t* pd = &tt.dict_cnt[(uint64_t)blockIdx.x * Geo::kSlots + i];
+            uint32_t* pd = &t.dict_cnt[(uint64_t)blockIdx.x * Geo::kSlots + i];
             hits += v - (resume ? *pd : 0u);
             *pd = v;
         }
-    if (acc == 0x5eed5eedull) atomicAdd(&tt.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
-    block_add4<NW>(&tt.ctr->spilled, &tt.ctr->dict_hits, &tt.ctr->spill_ovf, &tt.ctr->chunks_utf8, spilled, hits,
+    if (acc == 0x5eed5eedull) atomicAdd(&t.ctr->pad[0], 1ull);  // keeps ablation builds honest (no DCE)
+    block_add4<NW>(&t.ctr->spilled, &t.ctr->dict_hits, &t.ctr->spill_ovf, &t.ctr->chunks_utf8, spilled, hits,
                             ovf, lane == 0 ? utf8_chunks : 0, (unsigned long long*)&L.ring[0][0][0]);
-    block_add4<NW>(&tt.ctr->spilled16, nullptr, nullptr, nullptr, sp16, 0, 0, 0, (unsigned long long*)&L.ring[0][0][0]);
-    if (tt.dbg && tid == 0) tt.dbg[2 * (NB + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
+    block_add4<NW>(&t.ctr->spilled16, nullptr, nullptr, nullptr, sp16, 0, 0, 0, (unsigned long long*)&L.ring[0][0][0]);
+    if (t.dbg && tid == 0) t.dbg[2 * (NB + blockIdx.x) + 1] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ------------------------------------------------------------ bucket aggregator tables
