@@ -2412,11 +2412,13 @@ int mrg_run_job_async(mrg_ctx* c, int app, const void* buf, size_t len, int kind
     J.offsets.assign((size_t)use->nreduce + 1, 0);
     uint8_t* d = nullptr;
     uint64_t n = 0;
-    // wc: the lines go straight into this job's pinned buffer (as mrg_run_job's),
-    // so there is no transfer left to overlap; grep: device buffer + the copy below
-    const bool direct_ok = c->out_direct && use->app == MRG_APP_WC;
+    // wc with a small output (C2: 10 MB): the lines go straight into this job's
+    // pinned buffer (as mrg_run_job's); a large one (C5: 110 MB, ~2 ms over PCIe
+    // inside the formatting kernel) and grep: device buffer + the copy below,
+    // which overlaps the next job's map
+    const uint64_t bound = reduce_out_bound(use->r, use->app) + 1;
+    const bool direct_ok = c->out_direct && use->app == MRG_APP_WC && bound <= (64ull << 20);
     if (direct_ok) {
-        const uint64_t bound = reduce_out_bound(use->r, use->app) + 1;
         if (bound > J.cap) {
             if (J.host) hipHostFree(J.host);
             J.host = nullptr;
