@@ -254,6 +254,7 @@ struct mrg_ctx {
     bool prev_staged = false;           // the previous wc split ran the staged map
     bool prev_ascii = false;            // the previous wc split had no UTF-8 chunk (its map: the lean variant)
     bool lean_on = true;                // option map_lean (-1: never the lean variant)
+    uint64_t async_direct_max = 64ull << 20;  // option async_direct_max: larger async wc outputs copy on the output stream
     bool debug_times = getenv("MRG_DEBUG_TIMES") != nullptr;
     uint64_t rec_cap = 1u << 21;       // record output buffer capacity (grows on overflow)
     bool sh_clean = false;             // ShortTable known to be empty (skip its clear)
@@ -1341,6 +1342,8 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         c->out_direct = v >= 0;
     } else if (!strcmp(name, "hi_stage")) {  // 2048-bucket splits: mini dictionary + LDS write-combined spill (default) or not (-1)
         c->hi_stage = v >= 0;
+    } else if (!strcmp(name, "async_direct_max")) {  // bytes (0: default 64 MB; -1: every async wc output copied)
+        c->async_direct_max = v > 0 ? (uint64_t)v : v < 0 ? 0ull : (64ull << 20);
     } else if (!strcmp(name, "map_lean")) {  // wc: the all-ASCII map variant after an all-ASCII split (default) or never (-1)
         c->lean_on = v >= 0;
     } else if (!strcmp(name, "long_records")) {  // wc: words of 17-32 bytes as key records (default) or offsets (-1)
@@ -2417,7 +2420,7 @@ int mrg_run_job_async(mrg_ctx* c, int app, const void* buf, size_t len, int kind
     // inside the formatting kernel) and grep: device buffer + the copy below,
     // which overlaps the next job's map
     const uint64_t bound = reduce_out_bound(use->r, use->app) + 1;
-    const bool direct_ok = c->out_direct && use->app == MRG_APP_WC && bound <= (64ull << 20);
+    const bool direct_ok = c->out_direct && use->app == MRG_APP_WC && bound <= c->async_direct_max;
     if (direct_ok) {
         if (bound > J.cap) {
             if (J.host) hipHostFree(J.host);

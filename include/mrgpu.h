@@ -236,6 +236,10 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        variants
  *   grep_literal (1: on)                 grep patterns with regexp metacharacters matched as
  *                                        literals (QuoteMeta) instead of refused with MRG_EINVAL
+ *   async_direct_max (bytes; -1: none)   mrg_run_job_async: wc outputs up to this bound (default
+ *                                        64 MB) are written straight into the pinned buffer,
+ *                                        larger ones copied on the output stream
+ *   map_lean (-1: off)                   wc: the all-ASCII map variant after an all-ASCII split
  *   out_direct (-1: off)                 mrg_run_job (wc) writes the output lines straight into
  *                                        its pinned host buffer (default) instead of a
  *                                        device buffer + copy */

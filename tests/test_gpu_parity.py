@@ -881,13 +881,21 @@ def test_run_job_output_to_host(ctx, direct):
         ctx.set_option("out_direct", 0)
 
 
-@pytest.mark.parametrize("app", ["wc", "grep:distributed"])
+@pytest.mark.parametrize("app", ["wc", "wc-copied", "grep:distributed"])
 def test_run_job_async_pipelined(ctx, app):
     """mrg_run_job_async / mrg_job_wait: jobs queued two deep (the second job's
     map overlaps the first's output transfer), outputs returned in order and
     byte-equal to the oracle; a third queued job is refused; a synchronous job
-    after async ones waits for their transfers."""
+    after async ones waits for their transfers.  wc outputs are written straight
+    into the pinned buffer, or (wc-copied: option async_direct_max -1, as C5's
+    110 MB outputs are) formatted in device memory and copied on the output stream."""
     from mrgpu.lib import MrgError
+    if app == "wc-copied":
+        ctx.set_option("async_direct_max", -1)
+        try:
+            return test_run_job_async_pipelined(ctx, "wc")
+        finally:
+            ctx.set_option("async_direct_max", 0)
     a = MRG_APP_WC if app == "wc" else MRG_APP_GREP
     pat = b"" if app == "wc" else b"distributed"
     if app == "wc":
