@@ -1007,10 +1007,10 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         Counters h = *c->h_ctr;
         if (c->debug_times)
             fprintf(stderr, "[mrg wc] attempt %d: status %#x, %.3f ms since the call; nrec %llu, spilled %llu, ovf %llu, "
-                    "dict hits %llu, buckets %u, staged %d, dict %d\n", attempt, h.status,
+                    "dict hits %llu, buckets %u, staged %d, dict %d, long records past the LDS table %llu\n", attempt, h.status,
                     std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count(),
                     (unsigned long long)h.nrec, (unsigned long long)h.spilled, (unsigned long long)h.spill_ovf,
-                    (unsigned long long)h.dict_hits, c->spill_nb, (int)staged, (int)have_dict);
+                    (unsigned long long)h.dict_hits, c->spill_nb, (int)staged, (int)have_dict, (unsigned long long)h.lds_miss);
         if (h.status & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", h.status);
         if ((h.status & kStRecFull) && h.long_bytes + 16 > c->recarena.cap && h.nrec <= c->rec_cap) {
             // only the arena was short: grow it and run the collect again (not the map)

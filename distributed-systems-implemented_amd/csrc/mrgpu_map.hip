@@ -163,6 +163,7 @@ __global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t) {
     uint32_t n = 0;
     for (int r = 0; r < kWavesPerWG; r++) n += t.lrec_cnt[g * kWavesPerWG + r];
     if (n == 0) return;
+    uint32_t direct = 0;
     for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
         A.h[i] = 0;
         A.rep[i] = kRepUnpub;
@@ -212,7 +213,14 @@ __global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t) {
                 }
             }
         }
-        if (!done) long_insert(t, h, (const uint8_t*)(uintptr_t)me, len, 1);
+        if (!done) {
+            long_insert(t, h, (const uint8_t*)(uintptr_t)me, len, 1);
+            direct++;
+        }
+    }
+    if (t.dbg) {  // (MRG_DEBUG_TIMES diagnostics: records that missed the LDS table)
+        const uint64_t d = wave_sum(direct);
+        if ((threadIdx.x & 63) == 0 && d) atomicAdd(&t.ctr->lds_miss, (unsigned long long)d);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
