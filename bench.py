@@ -465,6 +465,90 @@ def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: 
     return res
 
 
+def group_rehearsal(args) -> dict:
+    """The owner side of C5's weak-scaling shuffle at C5's key counts, on ONE GPU:
+    P contexts (ranks) in this process, each mapping its own C5 split (Zipf s=0.8
+    over 1e7 words, every vocabulary word once up front: >= 1e7 distinct keys per
+    rank, the splits shrunk so P of them fit one device), R = 64, then
+    mrg_exchange_group (the same count / pack / unpack / exact re-aggregation code
+    as the RCCL path, with peer copies in place of ncclAllToAllv) and every owner's
+    reduce (partitions r % P).  Checked byte for byte against the C oracle: each
+    rank's split counted by oracle/mrcount.c, merged per partition (the reduce
+    over every split's intermediates, worker.go:123-146).  Reports what E(P) must
+    absorb on each owner: the unpack + re-aggregation of P ranks' records and the
+    owner's reduce.  NOT an RCCL or xGMI measurement (no communicator exists)."""
+    w = WORKLOADS["c5"]
+    P, R = args.group_ranks, w["nreduce"]
+    O = _oracle()
+    threads = min(16, os.cpu_count() or 1)
+    devs, want_parts = [], []
+    t0 = time.time()
+    with heartbeat("group rehearsal: splits + oracle counts"):
+        for g in range(P):
+            host = gen_corpus(w, g, args.group_file_mb, args.group_files, 0)
+            devs.append(upload(host, 0))
+            want_parts.append(O.c_count_mt("wc", host, R, threads))
+            del host
+    with heartbeat("group rehearsal: oracle merge"):
+        want = O.c_merge_parts("wc", want_parts)
+    del want_parts
+    nbytes = [int(d.numel()) for d in devs]
+    log(f"[group] {P} splits of {nbytes[0] / 1e9:.2f} GB + oracle in {time.time() - t0:.1f} s")
+    ctxs = [Context(0) for _ in range(P)]
+    steps = []
+    outs = None
+    try:
+        for step in range(max(1, args.group_steps)):
+            local = [ctxs[g].map(MRG_APP_WC, None, device_ptr=devs[g].data_ptr(), nbytes=nbytes[g], nreduce=R)
+                     for g in range(P)]
+            mst = [c.stats() for c in ctxs]
+            torch.cuda.synchronize()
+            te = time.perf_counter()
+            owned = Context.exchange_group(ctxs, local)
+            te = time.perf_counter() - te
+            est = [c.stats() for c in ctxs]
+            recv = [o.info()[0] for o in owned]
+            outs, rst = [], []
+            for g in range(P):
+                outs.append(ctxs[g].reduce_all(owned[g]))
+                rst.append(ctxs[g].stats())
+            steps.append({
+                "distinct_keys_per_rank": [int(s["distinct_keys"]) for s in mst],
+                "map_kernel_ms": [round(s["map_kernel_ms"], 3) for s in mst],
+                "map_total_ms": [round(s["map_total_ms"], 3) for s in mst],
+                "records_per_owner_after_reaggregation": [int(x) for x in recv],
+                "exchange_unpack_ms": [round(s["exchange_unpack_ms"], 3) for s in est],
+                "shuffle_send_bytes": [int(s["shuffle_send_bytes"]) for s in est],
+                "owner_reduce_ms": [round(s["reduce_ms"], 3) for s in rst],
+                "exchange_group_wall_ms": round(te * 1e3, 3)})
+            for q in local + owned:
+                q.free()
+    finally:
+        for c in ctxs:
+            c.close()
+    bad = [(g, r) for g in range(P) for r in range(R) if outs[g][r] != (want[r] if r % P == g else b"")]
+    last = steps[-1]
+    res = {"metric": "group rehearsal of the P-rank shuffle at C5 key counts (one GPU, peer copies; not RCCL)",
+           "ranks": P, "nreduce": R, "split_bytes_per_rank": nbytes[0],
+           "workload": f"{w['desc']}; {args.group_files} files x {args.group_file_mb} MB per rank (seed per rank)",
+           "steps": len(steps),
+           "min_distinct_keys_per_rank": min(last["distinct_keys_per_rank"]),
+           "exchange_unpack_ms_max": max(last["exchange_unpack_ms"]),
+           "exchange_unpack_ms_mean": round(sum(last["exchange_unpack_ms"]) / P, 3),
+           "owner_reduce_ms_max": max(last["owner_reduce_ms"]),
+           "owner_reduce_ms_mean": round(sum(last["owner_reduce_ms"]) / P, 3),
+           "records_received_per_owner": last["records_per_owner_after_reaggregation"],
+           "per_step": steps,
+           "checks": {"exact_vs_oracle": not bad, "mismatched": bad[:16],
+                      "oracle_output_bytes": sum(len(x) for x in want)},
+           "note": "P contexts on one device drive mrg_exchange_group: owner counts, per-owner packing, peer "
+                   "copies (where mrg_exchange calls ncclAllToAllv), unpack and exact re-aggregation on each owner "
+                   "(exchange_unpack_ms, from the owner's own unpack start), then the owner's reduce of partitions "
+                   "r % P.  No RCCL communicator exists here, so no xGMI rate or E(P) is measured: those need the "
+                   "driver's 8-GPU node."}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -491,7 +575,18 @@ def main():
     ap.add_argument("--rehearsal", action="store_true",
                     help="allow more ranks than visible GPUs (ranks share devices, no RCCL exchange: not a measurement)")
     ap.add_argument("--opt", action="append", default=[], help="library option name=value (experiments; repeatable)")
+    ap.add_argument("--group-rehearsal", action="store_true",
+                    help="one GPU: P contexts at C5 key counts through mrg_exchange_group (not RCCL; prints its own line)")
+    ap.add_argument("--group-ranks", type=int, default=8)
+    ap.add_argument("--group-files", type=int, default=100, help="C5 files per rank (all of them: every word once)")
+    ap.add_argument("--group-file-mb", type=int, default=10)
+    ap.add_argument("--group-steps", type=int, default=2)
     args = ap.parse_args()
+    if args.group_rehearsal:
+        torch.zeros(1, device="cuda:0").add_(1)
+        torch.cuda.synchronize()
+        print(json.dumps(group_rehearsal(args)), flush=True)
+        return
     w = WORKLOADS[args.workload]
     args.file_mb = args.file_mb or w["file_mb"]
     args.files = args.files or w["files"]

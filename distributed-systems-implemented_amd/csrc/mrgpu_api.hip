@@ -209,7 +209,7 @@ struct mrg_ctx {
     ExchSide* exch = nullptr;  // RCCL shuffle buffers, kept across calls (no hipMalloc / hipFree per step)
     int device = 0;
     hipStream_t s = nullptr;
-    hipEvent_t ev[13] = {};  // 0-3, 8-10: map phases; 4-5 reduce; 6-7 exchange / d2h; 12 exchange end
+    hipEvent_t ev[14] = {};  // 0-3, 8-10: map phases; 4-5 reduce; 6-7 exchange / d2h; 12 exchange end; 13 unpack start
     std::string err;
     uint8_t* d_l1 = nullptr;
     uint32_t* d_l2 = nullptr;
@@ -575,6 +575,10 @@ static int ensure_recbuf(mrg_ctx* c) {
     HCHK(c, c->recarena.ensure_cached(16, c->device));
     return MRG_OK;
 }
+
+// Total bytes the map's long-word record regions may take: the
+// split's size, at least 256 MiB.
+static uint64_t lrec_bytes_cap(uint64_t len) { return std::max<uint64_t>(len, 256ull << 20); }
 
 // Diagnostics: distribution of per-workgroup start/end stamps (100 MHz) of the
 // last aggregation kernel, relative to the earliest start.
@@ -961,9 +965,20 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         t.nreduce = nreduce;
         t.out = rec_view(c);
         t.out_cap = c->rec_cap;
+        // The 17-32-byte key records: every map wave gets a region of lrec_cap
+        // records.  Their total is capped (lrec_bytes_cap: the split's size, at least
+        // 256 MiB); past it, or when the allocation fails, the records are turned off
+        // for the context and every long word takes the start-offset list (the same
+        // counts, more work for wc_long_kernel) instead of failing the map.
         if (c->lrec_on) {
-            HCHK(c, c->lrec.ensure_grow((size_t)nwg * kWavesPerWG * c->lrec_cap * 32));
-            HCHK(c, c->lrec_cnt.ensure((size_t)kMaxMapWGs * kWavesPerWG * 4));
+            const uint64_t want = (uint64_t)nwg * kWavesPerWG * c->lrec_cap * 32;
+            if (want > lrec_bytes_cap(len) || c->lrec.ensure_grow(want) != hipSuccess ||
+                c->lrec_cnt.ensure((size_t)kMaxMapWGs * kWavesPerWG * 4) != hipSuccess) {
+                (void)hipGetLastError();  // (a failed allocation leaves no sticky error to report later)
+                c->lrec_on = false;
+            }
+        }
+        if (c->lrec_on) {
             t.lrec = (uint4*)c->lrec.p;
             t.lrec_cnt = (uint32_t*)c->lrec_cnt.p;
             t.lrec_cap = c->lrec_cap;
@@ -1033,10 +1048,10 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             HCHK(c, hipMemcpy(cnt.data(), c->lrec_cnt.p, cnt.size() * 4, hipMemcpyDeviceToHost));
             const uint32_t mx = *std::max_element(cnt.begin(), cnt.end());
             const uint64_t want = std::max<uint64_t>((uint64_t)mx + mx / 4 + 1024, 2ull * c->lrec_cap);
-            // (a split of almost nothing but 17-32-byte words: past 2^20 records per
-            // wave the regions would take more HBM than the input; the offset list then
-            // takes every long word, for the rest of the context)
-            if (want > (1u << 20)) c->lrec_on = false;
+            // (every wave's region is sized for the busiest one: a split dense in
+            // 17-32-byte words would need regions past lrec_bytes_cap; the offset list
+            // then takes every long word, for the rest of the context)
+            if (want > (1u << 20) || (uint64_t)nwg * kWavesPerWG * want * 32 > lrec_bytes_cap(len)) c->lrec_on = false;
             else c->lrec_cap = (uint32_t)want;
         }
         if (grow_on_overflow(c, h.status & (kStListFull | kStShortFull | kStLongFull | kStRecFull | kStSegFull)) ||
@@ -1354,11 +1369,11 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         c->grep_literal = v > 0;
     } else if (!strcmp(name, "tie_rank")) {  // grep reduce: tied runs ranked per run (1, default) or merge-sorted (0)
         reduce_ws_set_tie_rank(c->rws, v != 0);
-    } else if (!strcmp(name, "own_sort")) {  // reduce radix passes: hand-written LSD sort (1, default) or rocPRIM (0)
+    } else if (!strcmp(name, "own_sort")) {  // (compatibility: every sort is the hand-written one since round 5)
         reduce_ws_set_own_sort(c->rws, v != 0);
     } else if (!strcmp(name, "sort_prefix32")) {  // wc reduce: single pass on the top 32 key bits (1, default) or all (0)
         reduce_ws_set_prefix32(c->rws, v != 0);
-    } else if (!strcmp(name, "sort_bins")) {  // wc reduce: hand-written sample sort (1) or rocPRIM (0, -1: default)
+    } else if (!strcmp(name, "sort_bins")) {  // wc reduce: hand-written sample sort (1) or the radix passes (0, -1: default)
         reduce_ws_set_bin_sort(c->rws, v > 0);
     } else if (!strcmp(name, "grep_sort_k1")) {  // grep radix over 16 key bytes (default) or 8 (-1)
         reduce_ws_set(c->rws, 0, -1, v >= 0 ? 1 : 0);
@@ -2105,6 +2120,7 @@ static int exch_finish(mrg_ctx* c, const mrg_parts* local, int P, ExchSide& x, m
                        hipEvent_t done = nullptr) {
     int rc;
     const ExchPlan& pl = x.plan;
+    HCHK(c, hipEventRecord(c->ev[13], c->s));  // the owner's unpack + re-aggregation starts
     std::vector<uint64_t> hsrc(2 * P);
     for (int o = 0; o < P; o++) { hsrc[o] = pl.rd[o] / sizeof(WireRec); hsrc[P + o] = pl.ard[o]; }
     HCHK(c, x.rmeta.ensure(16 * P));
@@ -2208,7 +2224,7 @@ static int exchange_rccl(mrg_ctx* c, const mrg_parts* local, int P, mrg_parts** 
     // exchange_ms: counts + payload all-to-alls + the owner's unpack and exact
     // re-aggregation; the first two alone are exchange_a2a_ms (the xGMI part)
     c->stats.exchange_a2a_ms = ev_ms(c->ev[6], c->ev[7]);
-    c->stats.exchange_unpack_ms = ev_ms(c->ev[7], c->ev[12]);
+    c->stats.exchange_unpack_ms = ev_ms(c->ev[13], c->ev[12]);
     c->stats.exchange_ms = ev_ms(c->ev[6], c->ev[12]);
     exch_bytes(pl, P, c->rank, &c->stats);
     comm_identity(c);
@@ -2287,7 +2303,9 @@ int mrg_exchange_group(mrg_ctx* const* ctxs, int P, const mrg_parts* const* loca
         if ((rc = bind(ctxs[j]))) return undo(rc);
         if ((rc = exch_finish(ctxs[j], local[j], P, xs[j], &owned[j], ctxs[j]->ev[12]))) return undo(rc);
         ctxs[j]->stats.exchange_a2a_ms = ev_ms(ctxs[j]->ev[6], ctxs[j]->ev[7]);
-        ctxs[j]->stats.exchange_unpack_ms = ev_ms(ctxs[j]->ev[7], ctxs[j]->ev[12]);
+        // (from the owner's own unpack start: the contexts' finishes run one after
+        // another on this host thread, so ev[7] -> ev[12] would include the others')
+        ctxs[j]->stats.exchange_unpack_ms = ev_ms(ctxs[j]->ev[13], ctxs[j]->ev[12]);
         ctxs[j]->stats.exchange_ms = ev_ms(ctxs[j]->ev[6], ctxs[j]->ev[12]);
         ctxs[j]->stats.rccl_nranks = 0;  // peer copies, no communicator
         ctxs[j]->stats.rccl_rank = -1;

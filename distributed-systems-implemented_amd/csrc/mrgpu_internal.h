@@ -279,11 +279,11 @@ void reduce_ws_free(ReduceWs*);
 void reduce_ws_set(ReduceWs*, int digit_bits, int fold_part, int grep_k1);
 // Tied runs merge-sorted on compact key copies (default) or on the records.
 void reduce_ws_set_compact_ties(ReduceWs*, bool on);
-// The single-key wc sort pass by the hand-written bucketed sort (default) or rocPRIM onesweep.
+// The single-key wc sort pass by the hand-written bucketed sort (option) or the radix passes (default).
 void reduce_ws_set_bin_sort(ReduceWs*, bool on);
 // The wc single-key pass on the key's top 32 bits (default) or the whole 60/64-bit key.
 void reduce_ws_set_prefix32(ReduceWs*, bool on);
-// Radix passes by the hand-written sort (default) or rocPRIM onesweep.
+// (compatibility: the radix passes are always the hand-written sort)
 void reduce_ws_set_own_sort(ReduceWs*, bool on);
 // grep's tied runs ranked per run (default) or all merge-sorted together.
 void reduce_ws_set_tie_rank(ReduceWs*, bool on);

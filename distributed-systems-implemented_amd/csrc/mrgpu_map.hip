@@ -701,8 +701,8 @@ __global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __r
 }
 
 // ------------------------------------------------------------ collect
-// ShortTable: the occupied slots are compacted by rocprim select first
-// (select_used_short), so record i is written at base + i with no shared cursor.
+// ShortTable: every claim appends its slot index to the claim list (sh_list), so
+// record i is the list's i-th slot, written at base + i with no shared cursor.
 // The ShortTable's claimed slots (its claim list, ctr->short_used entries) as
 // records at ctr->nrec; nrec_add_kernel then advances ctr->nrec past them.
 __global__ void collect_short_kernel(Tables t) {

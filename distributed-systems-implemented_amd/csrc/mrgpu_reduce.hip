@@ -14,8 +14,6 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <rocprim/device/device_merge_sort.hpp>
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 
@@ -47,22 +45,22 @@ struct DBuf {
 };
 
 struct ReduceWs {
-    DBuf perm_a, perm_b, key_a, key_b, tmp, lineoff, out, flags, sel, offs, ext, tiek, bins, runs;
+    DBuf perm_a, perm_b, key_a, key_b, lineoff, out, flags, sel, offs, ext, tiek, bins, runs;
     uint64_t* h_pinned = nullptr;  // small pinned staging
     int digit_bits = 0;            // radix digit of the 64-bit key passes: 8, 10, 0 = by app (grep 10, wc 8)
     bool fold_part = true;         // wc: partition folded into the top bits of the k0 sort key
     bool grep_k1 = true;           // grep: radix passes over the first 16 key bytes (else 8, more ties)
     bool compact_ties = true;      // tied runs merge-sorted on compact key copies (TieKey)
-    // single-key wc sorts by the hand-written sample sort below instead of rocPRIM
-    // onesweep: exact, but measured slower (C2 reduce 0.70 vs 0.42 ms, C5 4.4 vs
+    // single-key wc sorts by the hand-written sample sort below instead of the
+    // radix passes: exact, but measured slower (C2 reduce 0.70 vs 0.42 ms, C5 4.4 vs
     // 2.5 ms: its LDS bitonic bin sorts and scattered writes), so off by default
     bool bin_sort = false;
     // the wc single-key pass sorts only the key's top 32 bits ((partition, first
     // key bits): four 8-bit onesweep passes over u32 keys instead of six 10-bit
     // passes over u64 ones); keys tied on them are ordered by fix_ties
     bool prefix32 = true;
-    // radix passes by the hand-written LSD sort (mrgpu_sort.hip: one launch per
-    // pass, no memsets) instead of rocPRIM onesweep
+    // (compatibility option: the radix passes are always the hand-written LSD sort,
+    // mrgpu_sort.hip; rocPRIM's onesweep was the alternative until round 4)
     bool own_sort = true;
     // grep (16-byte passes): tied runs ordered by rank per run (waves / workgroups)
     // instead of one merge sort of every tied key
@@ -94,7 +92,7 @@ ReduceWs* reduce_ws_new() {
 
 void reduce_ws_free(ReduceWs* w) {
     if (!w) return;
-    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->tmp, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek, &w->bins, &w->runs};
+    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek, &w->bins, &w->runs};
     for (DBuf* b : bs) b->release();
     if (w->h_pinned) hipHostFree(w->h_pinned);
     radix_ws_free(w->rx);
@@ -349,7 +347,8 @@ __global__ void __launch_bounds__(kScanThreads) flag_positions_kernel(const uint
     const uint32_t t = scan_take_tile(st, &tile_w);
     const uint64_t i0 = (uint64_t)t * kScanTile + (uint64_t)threadIdx.x * kScanPer;
     uint32_t bb = 0;
-    if (i0 + kScanPer <= n) {
+    // (f may start at any byte, e.g. lng = tie + n: the 16-byte load only where aligned)
+    if (i0 + kScanPer <= n && ((uintptr_t)(f + i0) & 15u) == 0) {
         const uint4 v = *(const uint4*)(f + i0);
         const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -357,7 +356,7 @@ __global__ void __launch_bounds__(kScanThreads) flag_positions_kernel(const uint
 #pragma unroll
             for (int b = 0; b < 4; b++) bb |= (((w[q] >> (8 * b)) & 0xFFu) != 0 ? 1u : 0u) << (4 * q + b);
     } else {
-        for (uint32_t k = 0; i0 + k < n; k++) bb |= (f[i0 + k] != 0 ? 1u : 0u) << k;
+        for (uint32_t k = 0; k < kScanPer && i0 + k < n; k++) bb |= (f[i0 + k] != 0 ? 1u : 0u) << k;
     }
     uint64_t tot;
     const uint64_t ex = block_excl_scan_u64((uint64_t)__popc(bb), red, &tot);
@@ -747,11 +746,11 @@ __global__ void select_kernel(Recs src, uint32_t mod, uint32_t want, Recs dst, u
 // Equal keys end up adjacent in any order: tie runs are ordered by full key
 // comparison afterwards (fix_ties), exactly as after the radix sort.  A bin of
 // more than 8192 keys (thousands of keys tied on their first 8 bytes) sets
-// flags[1], and the caller repeats the pass with rocPRIM.
+// flags[1], and the caller repeats the pass with the radix passes.
 // Measured (MI355X, rocprofv3): C2 (1e6 keys) sample 81 us, count 12, offsets
 // 58, scatter 25, bin sorts 92 us = 0.70 ms reduce against onesweep's 0.42; C5
 // (1e7) 1.6 ms of sort kernels against ~1.8 ms.  Option sort_bins=1 (tests run
-// both); the default stays rocPRIM.
+// both); the default stays the radix passes.
 constexpr uint32_t kBinMax = 8192;        // bins at most (LDS: splitters + histogram)
 constexpr uint32_t kBinGroups = 256;      // count / scatter workgroups at most
 constexpr uint32_t kBinSample = 16384;    // sample keys at most (one LDS bitonic sort)
@@ -948,53 +947,18 @@ static inline unsigned grid_for(uint64_t n) {
         if (_e != hipSuccess) return (int)_e;     \
     } while (0)
 
-// rocPRIM's default radix sort runs a block sort + ~30 merge launches per sort
-// below 1 Mi items (its merge_sort_limit), which is exactly our size range
-// (~1e6 distinct keys); onesweep is several times faster there.
-using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config, rocprim::default_config,
-                                               (size_t)64 * 1024>;
-// 10-bit digits: a 64-bit key in 7 passes instead of 8 (each onesweep pass is a
-// ~25 us launch plus two look-back-state memsets at these sizes)
-using OnesweepCfg10 = rocprim::radix_sort_config<
-    rocprim::default_config, rocprim::default_config,
-    rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>, rocprim::kernel_config<512, 12>, 10,
-                                        rocprim::block_radix_rank_algorithm::match>,
-    (size_t)64 * 1024>;
-
+// The radix passes are the hand-written ones of mrgpu_sort.hip (no library
+// sort on any path: round 5 removed rocPRIM's onesweep, the option own_sort = 0
+// is kept for compatibility and runs the same passes).
 template <class K>
 static int sort_pass(ReduceWs* ws, K* keys_in, K* keys_out, uint32_t* v_in, uint32_t* v_out, uint64_t n, unsigned bits,
                      hipStream_t s) {
-    if (ws->own_sort) {
-        if constexpr (sizeof(K) == 8) return radix_sort_pairs_u64(ws->rx, keys_in, keys_out, v_in, v_out, n, bits, s);
-        else return radix_sort_pairs_u32(ws->rx, keys_in, keys_out, v_in, v_out, n, bits, s);
-    }
-    size_t tb = 0;
-    if (sizeof(K) == 8 && ws->digit_bits == 10 && bits > 32) {
-        RCHK(rocprim::radix_sort_pairs<OnesweepCfg10>(nullptr, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
-        RCHK(ws->tmp.ensure(tb));
-        RCHK(rocprim::radix_sort_pairs<OnesweepCfg10>(ws->tmp.p, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits,
-                                                      s));
-        return 0;
-    }
-    RCHK(rocprim::radix_sort_pairs<OnesweepCfg>(nullptr, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
-    RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::radix_sort_pairs<OnesweepCfg>(ws->tmp.p, tb, keys_in, keys_out, v_in, v_out, (size_t)n, 0u, bits, s));
-    return 0;
+    if constexpr (sizeof(K) == 8) return radix_sort_pairs_u64(ws->rx, keys_in, keys_out, v_in, v_out, n, bits, s);
+    else return radix_sort_pairs_u32(ws->rx, keys_in, keys_out, v_in, v_out, n, bits, s);
 }
 
 int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, unsigned bits, hipStream_t s) {
-    if (ws->own_sort) return radix_sort_keys_u64(ws->rx, k_in, k_out, n, bits, s);
-    size_t tb = 0;
-    if (ws->digit_bits != 8 && bits > 32) {  // (grep hit positions: 4 passes of 10 bits for a 34-bit split)
-        RCHK(rocprim::radix_sort_keys<OnesweepCfg10>(nullptr, tb, k_in, k_out, (size_t)n, 0u, bits, s));
-        RCHK(ws->tmp.ensure(tb));
-        RCHK(rocprim::radix_sort_keys<OnesweepCfg10>(ws->tmp.p, tb, k_in, k_out, (size_t)n, 0u, bits, s));
-        return 0;
-    }
-    RCHK(rocprim::radix_sort_keys<OnesweepCfg>(nullptr, tb, k_in, k_out, (size_t)n, 0u, bits, s));
-    RCHK(ws->tmp.ensure(tb));
-    RCHK(rocprim::radix_sort_keys<OnesweepCfg>(ws->tmp.p, tb, k_in, k_out, (size_t)n, 0u, bits, s));
-    return 0;
+    return radix_sort_keys_u64(ws->rx, k_in, k_out, n, bits, s);
 }
 
 // In-place sort of device keys (4 or 8 bytes) with optional u32 values
@@ -1026,6 +990,91 @@ int sort_u32_pairs(ReduceWs* ws, uint32_t* k_in, uint32_t* k_out, uint32_t* v_in
     return sort_pass<uint32_t>(ws, k_in, k_out, v_in, v_out, n, bits, s);
 }
 
+// ---- comparison merge sort of u32 items (hand-written; replaces rocPRIM's) --
+// Items are record / key indices ordered by a comparator over device memory
+// (FullLess, CompactLess).  The keys they name are distinct, so the order is
+// total and stability is moot.  Two stages:
+//  - tile_sort_kernel: one 1024-thread workgroup sorts kSortTile items by a
+//    bitonic network in LDS (the padding past m compares above every item);
+//  - merge_pass_kernel: sorted runs of width w merged pairwise into runs of 2w,
+//    one item per thread: its rank in the partner run by binary search (left
+//    items count the partner's smaller items, right items the partner's items
+//    not greater), so each item lands at its own position with no shared
+//    cursor — ceil(log2(m / kSortTile)) passes.
+constexpr uint32_t kSortTile = 2048;
+
+template <class Less>
+__global__ void __launch_bounds__(1024) tile_sort_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                         uint32_t m, Less less) {
+    __shared__ uint32_t it[kSortTile];
+    const uint32_t base = blockIdx.x * kSortTile;
+    for (uint32_t i = threadIdx.x; i < kSortTile; i += 1024) it[i] = base + i < m ? in[base + i] : ~0u;
+    __syncthreads();
+    for (uint32_t size = 2; size <= kSortTile; size <<= 1) {
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            for (uint32_t t = threadIdx.x; t < kSortTile / 2; t += 1024) {
+                const uint32_t i = 2 * t - (t & (stride - 1)), j = i + stride;
+                const uint32_t A = it[i], B = it[j];
+                // A > B; ~0u is padding, above every item
+                const bool gt = A == ~0u ? B != ~0u : B != ~0u && less(B, A);
+                if (gt == ((i & size) == 0)) {
+                    it[i] = B;
+                    it[j] = A;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t i = threadIdx.x; i < kSortTile; i += 1024)
+        if (base + i < m) out[base + i] = it[i];
+}
+
+template <class Less>
+__global__ void __launch_bounds__(256) merge_pass_kernel(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                         uint32_t m, uint32_t w, Less less) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride) {
+        const uint64_t blk = i / (2ull * w) * (2ull * w);
+        const uint64_t mid = blk + w < m ? blk + w : m, end = blk + 2ull * w < m ? blk + 2ull * w : m;
+        const uint32_t x = in[i];
+        uint64_t pos;
+        if (i < mid) {  // left run: the partner's items less than x come first
+            uint64_t lo = mid, hi = end;
+            while (lo < hi) {
+                const uint64_t md = (lo + hi) >> 1;
+                if (less(in[md], x)) lo = md + 1;
+                else hi = md;
+            }
+            pos = (i - blk) + (lo - mid);
+        } else {  // right run: the partner's items not greater than x come first
+            uint64_t lo = blk, hi = mid;
+            while (lo < hi) {
+                const uint64_t md = (lo + hi) >> 1;
+                if (!less(x, in[md])) lo = md + 1;
+                else hi = md;
+            }
+            pos = (i - mid) + (lo - blk);
+        }
+        out[blk + pos] = x;
+    }
+}
+
+// Sorts a[0, m) (device, m known on the host); b is scratch of m items.
+// Returns the buffer holding the result (a or b).
+template <class Less>
+static uint32_t* merge_sort_u32(uint32_t* a, uint32_t* b, uint32_t m, Less less, hipStream_t s) {
+    if (m == 0) return a;
+    const uint32_t tiles = (m + kSortTile - 1) / kSortTile;
+    tile_sort_kernel<<<tiles, 1024, 0, s>>>(a, b, m, less);
+    uint32_t *src = b, *dst = a;
+    const unsigned g = (unsigned)std::min<uint64_t>(((uint64_t)m + 255) / 256, 4096);
+    for (uint64_t w = kSortTile; w < m; w <<= 1) {
+        merge_pass_kernel<<<g, 256, 0, s>>>(src, dst, m, (uint32_t)w, less);
+        std::swap(src, dst);
+    }
+    return src;
+}
+
 // The members of long tied runs (lng[i] != 0): compacted in order, merge-sorted
 // by full (partition, key) comparison, written back to the same positions.  The
 // runs are contiguous and already in (partition, prefix) order, which the full
@@ -1043,7 +1092,6 @@ static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
         RCHK(ws->scan.prepare(ntiles, s, &st));
         flag_positions_kernel<<<(unsigned)ntiles, kScanThreads, 0, s>>>(lng, n, pos, d_m, st);
     }
-    size_t tb = 0;
     RCHK(hipMemcpyAsync(ws->h_pinned + 8, d_m, 4, hipMemcpyDeviceToHost, s));
     RCHK(hipStreamSynchronize(s));
     const uint32_t m = (uint32_t)(ws->h_pinned[8] & 0xFFFFFFFFu);
@@ -1052,23 +1100,25 @@ static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
     uint32_t* vb = va + n;
     const unsigned g = (unsigned)((m + 255) / 256 < 4096 ? (m + 255) / 256 : 4096);
     gather_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, va);
-    tb = 0;
+    const uint32_t* sorted;
     if (ext && ws->compact_ties) {
         RCHK(ws->tiek.ensure((size_t)m * (sizeof(TieKey) + 8) + 64));
         TieKey* K = ws->tiek.as<TieKey>();
         uint32_t* ia = (uint32_t*)(K + m);
         uint32_t* ib = ia + m;
         tie_keys_kernel<<<g, 256, 0, s>>>(r, ext, va, d_m, K, ia);
-        RCHK(rocprim::merge_sort(nullptr, tb, ia, ib, (size_t)m, CompactLess{K, r}, s));
-        RCHK(ws->tmp.ensure(tb));
-        RCHK(rocprim::merge_sort(ws->tmp.p, tb, ia, ib, (size_t)m, CompactLess{K, r}, s));
-        untie_perm_kernel<<<g, 256, 0, s>>>(va, ib, d_m, vb);
+        const uint32_t* io = merge_sort_u32(ia, ib, m, CompactLess{K, r}, s);
+        untie_perm_kernel<<<g, 256, 0, s>>>(va, io, d_m, vb);
+        sorted = vb;
     } else {
-        RCHK(rocprim::merge_sort(nullptr, tb, va, vb, (size_t)m, FullLess{r, ext}, s));
-        RCHK(ws->tmp.ensure(tb));
-        RCHK(rocprim::merge_sort(ws->tmp.p, tb, va, vb, (size_t)m, FullLess{r, ext}, s));
+        sorted = merge_sort_u32(va, vb, m, FullLess{r, ext}, s);
     }
-    scatter_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, vb);
+    scatter_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, sorted);
+    static const bool dbg = getenv("MRG_DEBUG_TIES") != nullptr;
+    if (dbg) {
+        RCHK(hipStreamSynchronize(s));
+        fprintf(stderr, "[ties] long runs: %u members merge-sorted\n", m);
+    }
     return 0;
 }
 
@@ -1393,7 +1443,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     // that fix_ties orders by full comparison; if a run is long (many keys with
     // one 8-byte prefix), everything is sorted again with the k1 pass.
     // the single-key pass by the hand-written bucketed sort (bins of the
-    // partition and the first key bits); rocPRIM when a bin overflowed
+    // partition and the first key bits); the radix passes when a bin overflowed
     bool use_bins = ws->bin_sort;
     auto bin_pass = [&](int which, uint32_t fold_bits) -> int {
         gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, nullptr, n, which, ws->key_a.as<uint64_t>(), nullptr, fold_bits);
@@ -1510,7 +1560,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
             // merge sort of the run members
             // (a run over 64 needs 65 distinct keys sharing the sort key's prefix:
             // 9-16-byte keys, or longer ones; <= 8-byte keys differ within 2^fold)
-            if (bins_over) {  // a bin overflowed: the whole pass again with rocPRIM
+            if (bins_over) {  // a bin overflowed: the whole pass again with the radix passes
                 use_bins = false;
                 RCHK(hipMemsetAsync(flags + 1, 0, 8, s));
                 if ((e = sort_all(false))) return e;

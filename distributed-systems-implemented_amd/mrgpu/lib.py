@@ -332,10 +332,12 @@ class Context:
     def job_wait(self, copy_out: bool = True):
         """The oldest queued job's output: list of mr-out-r bytes (or (ptr, n, offsets))."""
         queued = getattr(self, "_async_nreduce", [])
-        nreduce = queued.pop(0) if queued else 1  # (none queued: the library reports the error)
+        nreduce = queued[0] if queued else 1  # (none queued: the library reports the error)
         p, n = c_void_p(), c_size_t()
         offs = (c_uint64 * (nreduce + 1))()
         self._check(self.L.mrg_job_wait(self.h, byref(p), byref(n), offs), "mrg_job_wait")
+        if queued:  # dequeued only once the library has handed the job back (a failed wait keeps both queues equal)
+            queued.pop(0)
         if not copy_out:
             return p.value, n.value, list(offs)
         data = ctypes.string_at(p, n.value) if n.value else b""

@@ -76,7 +76,8 @@ typedef struct mrg_parts mrg_parts;
 typedef struct {
     double map_kernel_ms;     /* the tokenizer/aggregation kernel alone (dominant kernel) */
     double map_total_ms;      /* map: every kernel from first launch to last */
-    double exchange_ms;       /* RCCL all-to-all (0 when single-GPU) */
+    double exchange_ms;       /* the whole shuffle: count + payload all-to-alls (exchange_a2a_ms) and the
+                                 owner's unpack + exact re-aggregation (exchange_unpack_ms); 0 when single-GPU */
     double reduce_ms;         /* collect + sort + format */
     double d2h_ms;            /* output bytes to host */
     uint64_t input_bytes;     /* bytes mapped */
@@ -100,7 +101,8 @@ typedef struct {
     uint64_t spill_buckets;   /* wc: hash buckets of the map's spill (256 by default; 2048 for high-cardinality splits; 512 by option) */
     double exchange_a2a_ms;   /* exchange: the count and payload all-to-alls alone (exchange_ms also holds the
                                  owner's unpack + exact re-aggregation) */
-    double exchange_unpack_ms;/* exchange: unpack of the received records + re-aggregation on the owner */
+    double exchange_unpack_ms;/* exchange: unpack of the received records + re-aggregation on the owner, from
+                                 the owner's own unpack start (mrg_exchange_group: its finish step alone) */
     int64_t rccl_nranks;      /* exchange: ranks of the communicator as RCCL reports them (ncclCommCount);
                                  0 for mrg_exchange_group (peer copies) or no exchange */
     int64_t rccl_rank;        /* exchange: this context's rank per ncclCommUserRank (-1: none) */

@@ -831,6 +831,50 @@ def test_exchange_group_c5_shape():
             assert outs[i][r] == (want[r] if r % P == i else b""), f"rank {i} partition {r}"
 
 
+def test_exchange_group_c5_p8_full_keys():
+    """C5's owner side at C5's key counts: 8 ranks, nReduce = 64,
+    each rank's split holds EVERY word of the Zipf(0.8, 1e7) vocabulary once (100
+    files, each emitting its 1e5-word share up front, as bench.py's C5 corpus) plus
+    sampled words, so every rank maps >= 1e7 distinct keys and each owner unpacks
+    and re-aggregates ~8 x 1.25e6 records.  Owner r % 8 of every partition must
+    equal the oracle's merge of all ranks' outputs (worker.go:123-146); the other
+    partitions must be empty."""
+    from concurrent.futures import ThreadPoolExecutor
+    from mrgpu import Context
+    P, R, V, NF = 8, 64, 10**7, 100
+    voc = C.Vocab(C.KIND_ASCII, 0.8, V, 5)
+    SZ = 1_500_000  # > a file's 1e5-word vocabulary share
+    files = []
+    for g in range(P):
+        buf = np.empty(NF * SZ, dtype=np.uint8)
+
+        def one(i, g=g, buf=buf):  # (the C generator releases the GIL)
+            voc.fill_files([SZ], [5 + 1000 * g + i], C.wc_params(vocab_lo=V * i // NF, vocab_hi=V * (i + 1) // NF),
+                           threads=1, out=buf[i * SZ:(i + 1) * SZ])
+        with ThreadPoolExecutor(8) as ex:
+            list(ex.map(one, range(NF)))
+        files.append(buf.tobytes())
+    with ThreadPoolExecutor(4) as ex:  # the C oracle releases the GIL
+        per = list(ex.map(lambda f: O.c_count_mt("wc", f, R, 4), files))
+    want = O.c_merge_parts("wc", per)
+    del per
+    ctxs = [Context(0) for _ in range(P)]
+    try:
+        local = [ctxs[i].map(MRG_APP_WC, files[i], nreduce=R) for i in range(P)]
+        keys = [c.stats()["distinct_keys"] for c in ctxs]
+        assert min(keys) >= V, keys
+        owned = Context.exchange_group(ctxs, local)
+        for i in range(P):
+            out = ctxs[i].reduce_all(owned[i])
+            for r in range(R):
+                assert out[r] == (want[r] if r % P == i else b""), f"rank {i} partition {r}"
+        for q in local + owned:
+            q.free()
+    finally:
+        for c in ctxs:
+            c.close()
+
+
 @pytest.mark.parametrize("app", ["wc", "grep:distributed", "wc-2048"])
 def test_host_input_streamed_in_pieces(ctx, app):
     """Host input copied piece by piece on a second stream while the map runs
