@@ -125,9 +125,6 @@ __device__ __forceinline__ void dict_sets(uint32_t h, bool mid, uint32_t& s1, ui
     dict_set_addrs<G>(h, mid, a1, a2);
     s1 = a1 >> 4;
     s2 = a2 >> 4;
-#ifdef MRG_DICT1
-    s2 = s1;  // single-choice placement: a key lives only in its first set
-#endif
 }
 
 // Spill bucket of a key: bits 11..18 (256 buckets), 11..19 (512) or 10..20 (2048) of its hash.
@@ -785,36 +782,6 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     }
                     bool hit[kBatch];
                     uint64_t mHit[kBatch];  // lane mask of hit[]
-#ifdef MRG_DICT1
-                    if (use_dict) {
-                        // single-choice lookup: one 16-byte set read per word
-                        u32x4 A[kBatch];
-                        uint32_t a1[kBatch];
-        #pragma unroll
-                        for (int u = 0; u < kBatch; u++) {
-                            uint32_t a2;
-                            dict_set_addrs<Geo>(hh[u], __builtin_amdgcn_inverse_ballot_w64(mMid[u]), a1[u], a2);
-                            A[u] = *(const lds_uint4*)((const lds_u8*)dset + a1[u]);
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-        #pragma unroll
-                        for (int u = 0; u < kBatch; u++) {
-                            const bool mid = __builtin_amdgcn_inverse_ballot_w64(mMid[u]);
-                            const uint64_t kk = mid ? k1[u] : k0[u];
-                            const uint64_t alo = ((uint64_t)A[u].y << 32) | A[u].x, ahi = ((uint64_t)A[u].w << 32) | A[u].z;
-                            const uint64_t mMidU = mMid[u];
-                            const uint64_t mA0 = __ballot(alo == k0[u]), mA1 = __ballot(ahi == kk);
-                            mHit[u] = mOk[u] & ((mA0 & mA1) | (~mMidU & (mA0 | mA1)));
-                            hit[u] = __builtin_amdgcn_inverse_ballot_w64(mHit[u]);
-                            const uint64_t mWay = ~mMidU & ~mA0;
-                            const uint32_t cofs = (a1[u] >> 1) + (__builtin_amdgcn_inverse_ballot_w64(mWay) ? 4u : 0u);
-                            bool cnt_lds = hit[u];
-                            if constexpr ((mode & 8) != 0) cnt_lds = false;
-                            if (cnt_lds)
-                                __hip_atomic_fetch_add((lds_u32*)((lds_u8*)dcnt + cofs), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
-                    } else
-#endif
                     if (use_dict) {
                         u32x4 A[kBatch], B[kBatch];
                         uint32_t a1[kBatch], a2[kBatch];  // byte offsets of the two sets

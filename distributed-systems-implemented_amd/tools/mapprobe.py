@@ -57,7 +57,8 @@ def main():
                 st = ctx.stats()
                 ts.append(st["map_kernel_ms"])
                 p.free()
-            r = {"grid": g, "mode": m, "map_kernel_ms": min(ts), "GBps": buf.size / min(ts) / 1e6,
+            r = {"grid": g, "mode": m, "map_kernel_ms": min(ts), "all_ms": [round(x, 3) for x in ts],
+                 "GBps": buf.size / min(ts) / 1e6,
                  "map_total_ms": st["map_total_ms"], "agg_ms": st["agg_ms"], "long_ms": st["long_ms"],
                  "collect_ms": st["collect_ms"], "spilled": st["lds_overflow"], "agg_miss": st["agg_miss"],
                  "dict_ms": st["dict_ms"], "dict_hits": st["dict_hits"],
