@@ -222,8 +222,12 @@ struct mrg_ctx {
     DevBuf segmeta, seg8[2], seg16[2];  // multi-round aggregation: layout + ping-pong miss segments
     bool seg_sync = true;               // size the miss segments from this split's totals (host read)
     bool out_direct = true;             // mrg_run_job: output lines written straight into pinned host memory
+    bool out_direct_grep = true;        // ... for grep too (out_direct = 1: wc only)
+    bool grep_sort_hits = false;        // grep: hits sorted by position before line resolution (option grep_sort_hits)
+    bool grep_emit = true;              // grep: records written by the table insert (option grep_emit; 0: collect pass)
     bool grep_literal = false;          // grep: regexp metacharacters taken literally (QuoteMeta) instead of refused
     DevBuf lrec, lrec_cnt;              // wc: 32-byte long-word records [map wave][lrec_cap], their counts
+    DevBuf lrec_aux;                    // wc: their bucket offsets and bucket-ordered indices (launch_wc_lrec)
     uint32_t lrec_cap = 1024;           // records per map wave's region (grows on kStLrecFull)
     bool lrec_on = true;                // option long_records (-1: every long word through the offset list)
     // 2048-bucket (high-cardinality) splits: the mini dictionary (DictMini), the
@@ -414,6 +418,10 @@ static Tables make_tables(mrg_ctx* c) {
     t.lrec = nullptr;  // set by wc_map for the split's map (sample maps and grep use the offset list)
     t.lrec_cnt = nullptr;
     t.lrec_cap = 0;
+    t.lrec_off = t.lrec_idx = nullptr;
+    t.lrec_part = nullptr;
+    t.lrec_pcnt = nullptr;
+    t.lrec_bkt = nullptr;
     return t;
 }
 
@@ -972,8 +980,10 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
         // counts, more work for wc_long_kernel) instead of failing the map.
         if (c->lrec_on) {
             const uint64_t want = (uint64_t)nwg * kWavesPerWG * c->lrec_cap * 32;
-            if (want > lrec_bytes_cap(len) || c->lrec.ensure_grow(want) != hipSuccess ||
-                c->lrec_cnt.ensure((size_t)kMaxMapWGs * kWavesPerWG * 4) != hipSuccess) {
+            if (want > lrec_bytes_cap(len) || want / 32 >= (1ull << 32) ||  // (record indices are 32-bit)
+                c->lrec.ensure_grow(want) != hipSuccess ||
+                c->lrec_cnt.ensure((size_t)kMaxMapWGs * kWavesPerWG * 4) != hipSuccess ||
+                c->lrec_aux.ensure_grow(kLrecAuxOff + want / 8 + want / 32 + kLrecPartBytes) != hipSuccess) {
                 (void)hipGetLastError();  // (a failed allocation leaves no sticky error to report later)
                 c->lrec_on = false;
             }
@@ -982,6 +992,12 @@ static int wc_map(mrg_ctx* c, const uint8_t* in, uint64_t len, uint32_t nreduce,
             t.lrec = (uint4*)c->lrec.p;
             t.lrec_cnt = (uint32_t*)c->lrec_cnt.p;
             t.lrec_cap = c->lrec_cap;
+            t.lrec_off = (uint32_t*)c->lrec_aux.p;
+            t.lrec_idx = (uint32_t*)((char*)c->lrec_aux.p + kLrecAuxOff);
+            t.lrec_bkt = (uint8_t*)(t.lrec_idx + (uint64_t)nwg * kWavesPerWG * c->lrec_cap);  // (a byte per record after the indices)
+            // the partials after the indices (the buffer only grows: the current capacity's end)
+            t.lrec_part = (LrecPart*)(((uintptr_t)c->lrec_aux.p + c->lrec_aux.cap - kLrecPartBytes + 255) & ~(uintptr_t)255);
+            t.lrec_pcnt = (uint32_t*)(t.lrec_part + 512ull * 4096);
         }
         clear_for_run(c, t);
         mark("tables");
@@ -1190,15 +1206,19 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
         HCHK(c, c->glines.ensure_grow(nhits * 16 + 64));
         HCHK(c, c->gdefer.ensure_grow(nhits * 8 + 64));
         t = make_tables(c);
-        unsigned bits = 1;
-        while (bits < 64 && (len >> bits) != 0) bits++;
-        if (nhits && sort_u64_keys(c->rws, t.list, (uint64_t*)c->ghits.p, nhits, bits, c->s))
-            return fail(c, MRG_EDEVICE, "grep: hit sort failed");
-        launch_grep_resolve(in, len, (uint32_t)plen, t, nhits, c->s);
+        if (c->grep_sort_hits) {
+            unsigned bits = 1;
+            while (bits < 64 && (len >> bits) != 0) bits++;
+            if (nhits && sort_u64_keys(c->rws, t.list, (uint64_t*)c->ghits.p, nhits, bits, c->s))
+                return fail(c, MRG_EDEVICE, "grep: hit sort failed");
+        } else {
+            t.hits = t.list;  // the map kernel's order (grep_resolve_kernel: unsorted)
+        }
+        launch_grep_resolve(in, len, (uint32_t)plen, t, nhits, c->grep_sort_hits, c->s);
         HCHK(c, hipGetLastError());
         if ((rc = read_counters(c))) return rc;
         if (c->h_ctr->ndefer) {
-            launch_grep_resolve_long(in, len, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, c->s);
+            launch_grep_resolve_long(in, len, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, c->grep_sort_hits, c->s);
             HCHK(c, hipGetLastError());
             if ((rc = read_counters(c))) return rc;
         }
@@ -1210,24 +1230,51 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
         int need = 14;
         while (need < 24 && (1ull << need) * 7 < nlines * 10) need++;
         c->lo_log2_cur = need;
+        // emit (default): the insert writes each distinct line's record as it
+        // claims the line's slot, into parts sized for every occurrence (records
+        // <= nlines, arena <= the lines' bytes); option grep_emit = 0: insert,
+        // then collect the table (round 4).
+        const bool emit = c->grep_emit;
+        mrg_parts* p = nullptr;
+        if (emit && (rc = parts_alloc(c, nlines, c->h_ctr->line_bytes, MRG_APP_GREP, nreduce, &p))) return rc;
         bool ok = false;
         for (int grow = 0; grow < 8 && !ok; grow++) {
-            if ((rc = ensure_tables(c))) return rc;
+            if ((rc = ensure_tables(c))) { if (p) mrg_parts_free(p); return rc; }
             t = make_tables(c);
+            if (emit) {
+                t.out = p->r;
+                t.out_cap = nlines;
+                t.nreduce = nreduce;
+            }
             clear_long_table(t, c->s);
-            launch_grep_insert(in, t, nlines, c->s);
+            launch_grep_insert(in, t, nlines, emit, c->s);
             HCHK(c, hipGetLastError());
-            if ((rc = read_counters(c))) return rc;
+            if ((rc = read_counters(c))) { if (p) mrg_parts_free(p); return rc; }
             const uint32_t st = c->h_ctr->status;
-            if (st & kStSpin) return fail(c, MRG_EDEVICE, "hash table publish timed out (status %#x)", st);
+            if (st & (kStSpin | kStRecFull)) {
+                if (p) mrg_parts_free(p);
+                return fail(c, MRG_EDEVICE, "grep: line table insert failed (status %#x)", st);
+            }
             if (st & kStLongFull) c->lo_log2_cur += 2;
             else ok = true;
         }
-        if (!ok) return fail(c, MRG_ENOMEM, "grep: line table kept overflowing");
+        if (!ok) { if (p) mrg_parts_free(p); return fail(c, MRG_ENOMEM, "grep: line table kept overflowing"); }
         HCHK(c, hipEventRecord(c->ev[2], c->s));
         c->stats.map_kernel_ms = ev_ms(c->ev[0], c->ev[1]);
-        mrg_parts* p = nullptr;
-        if ((rc = collect_parts(c, MRG_APP_GREP, nreduce, &p))) return rc;
+        if (emit) {
+            const Counters& h = *c->h_ctr;
+            if (h.nrec != h.long_used || h.arena != h.long_bytes || h.nrec > nlines) {
+                mrg_parts_free(p);
+                return fail(c, MRG_EDEVICE, "grep: emitted %llu records / %llu bytes for %llu lines / %llu bytes",
+                            h.nrec, h.arena, h.long_used, h.long_bytes);
+            }
+            p->r.n = h.nrec;
+            p->r.arena_n = h.arena;
+            c->stats.distinct_keys = h.nrec;
+            c->stats.long_keys = h.nrec;
+        } else if ((rc = collect_parts(c, MRG_APP_GREP, nreduce, &p))) {
+            return rc;
+        }
         HCHK(c, hipEventRecord(c->ev[3], c->s));
         HCHK(c, hipEventSynchronize(c->ev[3]));
         c->stats.map_total_ms = ev_ms(c->ev[0], c->ev[3]);
@@ -1298,7 +1345,7 @@ void mrg_close(mrg_ctx* c) {
     if (c->comm) ncclCommDestroy(c->comm);
     DevBuf* bs[] = {&c->sh, &c->shl, &c->lo, &c->list, &c->ctr, &c->staging, &c->pat, &c->spool, &c->spool_alt, &c->spmeta,
                     &c->bflag, &c->dict, &c->dict_cnt, &c->sample, &c->recbuf, &c->recarena, &c->sortbuf,
-                    &c->segmeta, &c->seg8[0], &c->seg8[1], &c->seg16[0], &c->seg16[1], &c->lrec, &c->lrec_cnt};
+                    &c->segmeta, &c->seg8[0], &c->seg8[1], &c->seg16[0], &c->seg16[1], &c->lrec, &c->lrec_cnt, &c->lrec_aux};
     for (DevBuf* b : bs) b->release();
     if (c->d_l1) hipFree(c->d_l1);
     if (c->d_l2) hipFree(c->d_l2);
@@ -1353,8 +1400,13 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         reduce_ws_set(c->rws, 0, v >= 0 ? 1 : 0, -1);
     } else if (!strcmp(name, "sort_compact_ties")) {  // tied runs merge-sorted on key copies (-1: on the records)
         reduce_ws_set_compact_ties(c->rws, v >= 0);
-    } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default) or via a copy (-1)
+    } else if (!strcmp(name, "grep_emit")) {  // 0: insert the lines, then collect the LongTable (round-4 path)
+        c->grep_emit = v >= 0 ? v != 0 : true;
+    } else if (!strcmp(name, "grep_sort_hits")) {  // 1: the position sort before line resolution (round-4 path)
+        c->grep_sort_hits = v > 0;
+    } else if (!strcmp(name, "out_direct")) {  // mrg_run_job: lines into pinned host memory (default), via a copy (-1), wc only (1)
         c->out_direct = v >= 0;
+        c->out_direct_grep = v >= 0 && v != 1;
     } else if (!strcmp(name, "hi_stage")) {  // 2048-bucket splits: mini dictionary + LDS write-combined spill (default) or not (-1)
         c->hi_stage = v >= 0;
     } else if (!strcmp(name, "async_direct_max")) {  // bytes (0: default 64 MB; -1: every async wc output copied)
@@ -2340,14 +2392,13 @@ int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, cons
         if (rc) return rc;
         use = o;
     }
-    // wc: the output lines are written straight into the context's pinned host
+    // The output lines are written straight into the context's pinned host
     // buffer by the formatting kernel (sized for the output's bound up front), so
     // the transfer overlaps the formatting and the copy's host round trip goes
-    // (C2: 0.56 -> 0.50 ms for reduce + transfer).  grep keeps the device buffer
-    // + copy: its ~160-byte lines overflow the kernel's LDS staging in some
-    // blocks, whose byte-wise stores to host memory made the direct write slower
-    // than the copy (C3 2.66 vs 2.63 ms).  Option out_direct = -1: always the copy.
-    const bool direct_ok = c->out_direct && use->app == MRG_APP_WC;
+    // (C2: 0.56 -> 0.50 ms for reduce + transfer; C3 ~0.1 ms once grep's blocks
+    // stage 128 lines, not 256, and never fall back to byte stores).  Option
+    // out_direct = -1: always the copy; 1: wc only.
+    const bool direct_ok = c->out_direct && (use->app == MRG_APP_WC || c->out_direct_grep);
     const uint64_t bound = reduce_out_bound(use->r, use->app) + 1;
     const uint64_t need = direct_ok ? bound : 0;
     if (need > c->h_out_cap) {

@@ -578,7 +578,8 @@ __device__ inline void short_insert(const Tables& t, uint64_t k0, uint64_t k1, u
 
 // Long keys: claim = CAS on hash; publish len+1 and rep separately; a prober
 // that needs them before both are visible retries from the outer loop.
-__device__ inline int long_try(const Tables& t, uint64_t h, const uint8_t* rep, uint64_t len, uint64_t cnt) {
+__device__ inline int long_try(const Tables& t, uint64_t h, const uint8_t* rep, uint64_t len, uint64_t cnt,
+                               uint64_t* claimed_slot = nullptr) {
     uint64_t i = (h * 0x9E3779B97F4A7C15ull >> 17) & t.lo_mask;
     for (uint32_t probes = 0; probes <= (uint32_t)kGlobalProbes; probes++) {
         LongSlot* s = &t.lo[i];
@@ -589,6 +590,7 @@ __device__ inline int long_try(const Tables& t, uint64_t h, const uint8_t* rep, 
                 st_agent(&s->len, len + 1);
                 __hip_atomic_store(const_cast<const uint8_t**>(&s->rep), rep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 atomicAdd((unsigned long long*)&s->count, (unsigned long long)cnt);
+                if (claimed_slot) *claimed_slot = i;
                 return kClaimed;
             }
             cur = prev;

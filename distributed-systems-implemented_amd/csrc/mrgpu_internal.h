@@ -67,7 +67,7 @@ struct Counters {
     unsigned long long ndefer;     // grep: hits whose line bounds lie beyond a lane's scan window
     unsigned long long nrec_base;  // ctr->nrec before the collect (a collect-only retry restores it)
     unsigned long long spilled16;  // of `spilled`: 16-byte records (keys of 9-16 bytes)
-    unsigned long long pad[1];
+    unsigned long long line_bytes; // grep: bytes of the resolved line occurrences (the records' arena bound)
 };
 
 // Spill of dictionary misses, hash-partitioned into nb buckets (kSpillBuckets,
@@ -183,6 +183,19 @@ struct Tables {
     // write-combines its 8-byte spill streams in LDS (mrgpu_wc.hip, kS)
     uint32_t hi_staged;
     uint32_t lean;          // wc map: the all-ASCII variant (the previous split had no UTF-8 chunk)
+    // (last: fields the map kernel never reads keep the others' kernarg offsets)
+    uint32_t* lrec_off;  // [256 x nwg + 1] bucket-major offsets of the records by hash bucket (wc_lrec passes)
+    uint32_t* lrec_idx;  // [records] record indices in bucket order
+    struct LrecPart* lrec_part;  // [kLrecGrid][kLrecSlots] per-range distinct keys with counts
+    uint32_t* lrec_pcnt;         // [kLrecGrid] partials per range
+    uint8_t* lrec_bkt;           // [region][lrec_cap] each record's hash bucket (lrec_hist_kernel -> lrec_scatter_kernel)
+};
+// A distinct long-word record of one wc_lrec range: its representative record,
+// FNV-1a-64, length, count and hash bucket.
+struct LrecPart {
+    unsigned long long rep;
+    uint64_t h;
+    uint32_t len, cnt, bucket, pad;
 };
 
 struct LetterTables {
@@ -201,6 +214,10 @@ void clear_tables(const Tables& t, bool short_table, hipStream_t s);
 // Count the map's 32-byte long-word records (one workgroup per map workgroup's
 // region) into the LongTable (mrgpu_map.hip).
 void launch_wc_lrec(const Tables& t, uint32_t nwg, hipStream_t s);
+// bytes of the bucket offsets ahead of the record indices in the lrec aux buffer
+constexpr uint64_t kLrecAuxOff = (256ull * kMaxMapWGs + 64) * 4;
+// the per-range partials of the long-word records (after the indices)
+constexpr uint64_t kLrecPartBytes = 512ull * 4096 * sizeof(LrecPart) + 512 * 4 + 256;
 // ---- wc pipeline (mrgpu_wc.hip) ----
 uint32_t wc_map_grid(uint64_t n, int grid);
 // Chunks [cbeg, cend) of the split (kOwn = 992 input bytes each; default: all);
@@ -233,13 +250,18 @@ void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32
 // grep line resolution, linear in the input (mrgpu_map.hip): t.hits (sorted) ->
 // one (start, end) pair per matching line occurrence in t.lines (ctr->nlines),
 // hits in lines longer than a lane's scan window to t.defer (ctr->ndefer).
-void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, hipStream_t s);
+void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, bool sorted,
+                         hipStream_t s);
 // The deferred hits, one workgroup each (wide coalesced scans).
 void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t ndefer,
-                              uint64_t nhits, hipStream_t s);
+                              uint64_t nhits, bool sorted, hipStream_t s);
 // t.lines -> the LongTable (one distinct line = one slot).
-void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, hipStream_t s);
-// Clear the LongTable and its fill counters (a re-run of launch_grep_insert after growth).
+// emit: each line that claims its slot also writes its record (t.out: key
+// prefix, length, partition, its bytes copied to the arena at ctr->arena) —
+// no collect pass over the table afterwards.
+void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, bool emit, hipStream_t s);
+// Clear the LongTable and its fill counters, and the record / arena cursors (a
+// re-run of launch_grep_insert after growth).
 void clear_long_table(const Tables& t, hipStream_t s);
 void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int grid, hipStream_t s);
 struct ReduceWs;

@@ -140,87 +140,362 @@ __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restr
 }
 
 // Words of 17-32 bytes handed over by the map kernel as 32-byte zero-padded key
-// records (the map read them from its LDS window; no decode of the input here):
-// one workgroup per map workgroup's kWavesPerWG record regions (one per wave).  Each lane hashes a record
-// (FNV-1a-64 of its bytes, the same hash wc_long_kernel and the LongTable use,
-// so a word that reached the table by either path meets itself there) and counts
-// it in an LDS table confirmed by comparing the two records' 32 bytes (equal
-// zero-padded records <=> equal keys: letters are never 0x00).  The HBM
-// LongTable then sees one insert per (workgroup, distinct word), its
-// representative the record itself (the collect copies the key bytes from it).
-constexpr int kLrecSlots = 4096;
+// records (the map read them from its LDS window; no decode of the input here),
+// in one region per map wave.  They are counted by hash bucket, so that every
+// occurrence of a key meets ONE workgroup's LDS table and the HBM LongTable sees
+// one insert per distinct key (round 4 counted them per map workgroup: a
+// workgroup of C2u saw ~40 K distinct words, its 4096-slot table overflowed,
+// and ~4 M records plus ~1 M table entries per split went to the LongTable by
+// CAS, 3.2 ms):
+//   1. lrec_hist_kernel: per map workgroup, its records per bucket (LDS
+//      histogram, bucket = 8 bits of a fold of the record's words), and each
+//      record's bucket as a byte (the scatter reads 1 byte, not 32, per record);
+//   2. lrec_scan_kernel: bucket-major exclusive offsets over (bucket, workgroup);
+//   3. lrec_scatter_kernel: each record's index at its bucket's next position;
+//   4. wc_lrec_kernel: one workgroup per range of the bucket-ordered records
+//      counts them in an LDS table (slot from a cheap mix of the 32 bytes,
+//      confirmed by comparing the two records' 32 bytes: equal zero-padded
+//      records <=> equal keys, letters are never 0x00) and writes each distinct
+//      key once as a partial with its FNV-1a-64 (the hash wc_long_kernel and
+//      the LongTable use, so a word that reached the table by either path meets
+//      itself there); its representative is the record itself (the collect
+//      copies the key bytes from it).  Exact: a full table inserts the record
+//      directly;
+//   5. lrec_merge_kernel: one workgroup per bucket merges the partials of the
+//      ranges the bucket spans and inserts each distinct key once.
+constexpr uint32_t kLrecBuckets = 256;
+#ifndef MRG_LREC_SLOTS
+#define MRG_LREC_SLOTS 2048
+#endif
+constexpr int kLrecSlots = MRG_LREC_SLOTS;
 struct alignas(16) LrecLds {
-    unsigned long long h[kLrecSlots];    // hash | 1 (0: empty)
-    unsigned long long rep[kLrecSlots];  // address of the slot's first record (kRepUnpub until published)
+    unsigned long long h[kLrecSlots];    // hash | 1 (0: not yet written)
+    unsigned long long rep[kLrecSlots];  // address of the slot's first record (0: empty; the claim)
     uint32_t len[kLrecSlots];
     uint32_t cnt[kLrecSlots];
+    u32x4 key[kLrecSlots][2];            // the representative's 32 bytes (valid once h is written)
 };
 
-__global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t) {
+__device__ __forceinline__ uint32_t lrec_bucket(const uint4& a, const uint4& b) {
+    return fold32(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w) >> 24;
+}
+
+// One LDS add for the lanes sharing the first active lane's bucket
+// (a Zipf-hot long word puts most of a workgroup's records in one bucket: one
+// same-address atomic per lane serialized), one per lane for the rest.
+// Returns each lane's position (the add's old value + its rank among the
+// lanes of one add).
+__device__ __forceinline__ uint32_t lrec_bucket_add(uint32_t* cnt, uint32_t b, bool active, bool want_pos) {
+    const uint64_t act = __ballot(active);
+    if (act == 0) return 0;
+    const uint32_t b0 = (uint32_t)__builtin_amdgcn_readlane((int)b, (int)__builtin_ctzll(act));
+    const uint64_t m = __ballot(active && b == b0);
+    uint32_t base = 0;
+    if (active && mbcnt64(m) == 0 && b == b0) base = atomicAdd(&cnt[b0], (uint32_t)__popcll(m));
+    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)__builtin_ctzll(m));
+    uint32_t pos = base + mbcnt64(m);
+    if (active && b != b0) pos = want_pos ? atomicAdd(&cnt[b], 1u) : (atomicAdd(&cnt[b], 1u), 0u);
+    return pos;
+}
+
+__global__ void __launch_bounds__(kLongWG) lrec_hist_kernel(Tables t, uint32_t nwg) {
+    __shared__ uint32_t hist[kLrecBuckets];
+    const uint32_t g = blockIdx.x, cap = t.lrec_cap;
+    for (uint32_t b = threadIdx.x; b < kLrecBuckets; b += kLongWG) hist[b] = 0;
+    __syncthreads();
+    for (int r = 0; r < kWavesPerWG; r++) {
+        const uint4* recs = t.lrec + ((uint64_t)g * kWavesPerWG + r) * cap * 2;
+        const uint32_t nr = min(t.lrec_cnt[g * kWavesPerWG + r], cap);
+        for (uint32_t i0 = 0; i0 < nr; i0 += kLongWG) {  // (workgroup-uniform trip count: whole waves in the adds)
+            const uint32_t i = i0 + threadIdx.x;
+            const bool act = i < nr;
+            const uint32_t b = act ? lrec_bucket(recs[2 * i], recs[2 * i + 1]) : 0u;
+            if (act) t.lrec_bkt[((uint64_t)g * kWavesPerWG + r) * cap + i] = (uint8_t)b;
+            lrec_bucket_add(hist, b, act, false);
+        }
+    }
+    __syncthreads();
+    for (uint32_t b = threadIdx.x; b < kLrecBuckets; b += kLongWG) t.lrec_off[(uint64_t)b * nwg + g] = hist[b];
+}
+
+// Exclusive scan of the kLrecBuckets x nwg counts in place (one workgroup,
+// a multiple of 4 entries per thread read as uint4), the total at
+// [kLrecBuckets * nwg].
+__global__ void __launch_bounds__(1024) lrec_scan_kernel(uint32_t* off, uint32_t nwg) {
+    __shared__ uint32_t part[1024];
+    const uint32_t E = kLrecBuckets * nwg, tid = threadIdx.x;
+    // thread tid owns entries [tid * per, +per), per a multiple of 4 (E = 256 nwg)
+    const uint32_t per = ((E + 1023) / 1024 + 3) & ~3u;
+    uint4* o4 = (uint4*)off;
+    // two passes over the thread's entries (the second reads them from L2): held
+    // in registers they spilled to scratch
+    uint32_t sum = 0;
+    for (uint32_t q = 0; q < per; q += 4) {
+        const uint32_t i = tid * per + q;
+        if (i < E) {
+            const uint4 v = o4[i / 4];
+            sum += v.x + v.y + v.z + v.w;
+        }
+    }
+    part[tid] = sum;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive Hillis-Steele scan of the thread sums
+        const uint32_t x = tid >= d ? part[tid - d] : 0u;
+        __syncthreads();
+        part[tid] += x;
+        __syncthreads();
+    }
+    uint32_t run = part[tid] - sum;
+    for (uint32_t q = 0; q < per; q += 4) {
+        const uint32_t i = tid * per + q;
+        if (i < E) {
+            const uint4 v = o4[i / 4];
+            uint4 e;
+            e.x = run; run += v.x;
+            e.y = run; run += v.y;
+            e.z = run; run += v.z;
+            e.w = run; run += v.w;
+            o4[i / 4] = e;
+        }
+    }
+    if (tid == 1023) off[E] = part[1023];
+}
+
+__global__ void __launch_bounds__(kLongWG) lrec_scatter_kernel(Tables t, uint32_t nwg) {
+    __shared__ uint32_t cur[kLrecBuckets];
+    const uint32_t g = blockIdx.x, cap = t.lrec_cap;
+    for (uint32_t b = threadIdx.x; b < kLrecBuckets; b += kLongWG) cur[b] = t.lrec_off[(uint64_t)b * nwg + g];
+    __syncthreads();
+    for (int r = 0; r < kWavesPerWG; r++) {
+        const uint64_t region = (uint64_t)g * kWavesPerWG + r;
+        const uint32_t nr = min(t.lrec_cnt[g * kWavesPerWG + r], cap);
+        for (uint32_t i0 = 0; i0 < nr; i0 += kLongWG) {
+            const uint32_t i = i0 + threadIdx.x;
+            const bool act = i < nr;
+            const uint32_t b = act ? t.lrec_bkt[region * cap + i] : 0u;
+            const uint32_t pos = lrec_bucket_add(cur, b, act, true);
+            if (act) t.lrec_idx[pos] = (uint32_t)(region * cap + i);
+        }
+    }
+}
+
+// FNV-1a-64 and length of a zero-padded 32-byte record's key.
+__device__ __forceinline__ uint64_t lrec_fnv(const uint4& a, const uint4& b, uint32_t& len) {
+    const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    uint64_t h = kFnv64Off;
+    len = 0;
+    for (int x = 0; x < 32; x++) {
+        const uint32_t c = (w[x >> 2] >> (8 * (x & 3))) & 0xFFu;
+        if (c == 0) break;
+        h = fnv1a64_step(h, c);
+        len++;
+    }
+    return h;
+}
+
+// Count `run` occurrences of the key of record me (bytes a, b; FNV-1a-64 h,
+// len bytes): the LDS table, or the LongTable directly when 16 probes find no
+// room (len 0: h is a table-local hash, not yet the key's FNV-1a-64 and length,
+// computed here for that insert).  A slot is claimed by CAS on its representative's address, so the
+// claim publishes it (a prober never meets a claimed slot it cannot compare
+// with: round 4's hash-first claim sent racing lanes of a hot word to the
+// LongTable); the hash, written after the claim, only skips byte compares.
+__device__ __forceinline__ void lrec_count(LrecLds& A, const Tables& t, const uint4& a, const uint4& b, uint64_t h,
+                                           uint32_t len, unsigned long long me, uint32_t run, uint32_t& direct) {
+    const unsigned long long hk = h | 1ull;
+    uint32_t slot = (uint32_t)(hk >> 20) & (kLrecSlots - 1);
+    for (int probe = 0; probe < 16; probe++, slot = (slot + 1) & (kLrecSlots - 1)) {
+        unsigned long long r = __hip_atomic_load(&A.rep[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (r == 0) {
+            r = atomicCAS(&A.rep[slot], 0ull, me);
+            if (r == 0) {  // claimed (and published): key bytes, length and hash for the others, then count
+                A.key[slot][0] = to_v4(a);
+                A.key[slot][1] = to_v4(b);
+                A.len[slot] = len;
+                __hip_atomic_store(&A.h[slot], hk, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                atomicAdd(&A.cnt[slot], run);
+                return;
+            }
+        }
+        const unsigned long long hs = __hip_atomic_load(&A.h[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (hs != 0 && hs != hk) continue;  // another key
+        uint4 ra, rb;
+        if (hs != 0) {  // the bytes from LDS (no global round trip per probe)
+            ra = from_v4(A.key[slot][0]);
+            rb = from_v4(A.key[slot][1]);
+        } else {  // claimed, not yet published: the representative itself
+            const uint4* rr = (const uint4*)(uintptr_t)r;
+            ra = rr[0];
+            rb = rr[1];
+        }
+        if (ra.x == a.x && ra.y == a.y && ra.z == a.z && ra.w == a.w && rb.x == b.x && rb.y == b.y && rb.z == b.z &&
+            rb.w == b.w) {
+            atomicAdd(&A.cnt[slot], run);
+            return;
+        }
+    }
+    if (len == 0) h = lrec_fnv(a, b, len);
+    long_insert(t, h, (const uint8_t*)(uintptr_t)me, len, run);
+    direct++;
+}
+
+// A cheap 64-bit mix of a record's 32 bytes: the LDS table's slot and compare
+// hash (the FNV-1a-64 the LongTable needs is computed once per distinct key
+// when the partials are written; per record, its byte loop was the kernel's
+// main instruction cost).
+__device__ __forceinline__ uint64_t lrec_mix(const uint4& a, const uint4& b) {
+    const uint64_t x0 = ((uint64_t)a.y << 32 | a.x) ^ __builtin_rotateleft64((uint64_t)b.y << 32 | b.x, 17);
+    const uint64_t x1 = ((uint64_t)a.w << 32 | a.z) ^ __builtin_rotateleft64((uint64_t)b.w << 32 | b.z, 29);
+    return short_hash64(x0, x1) * 0x9E3779B97F4A7C15ull;
+}
+
+// A key cached in a thread's registers with its count so far.
+struct LrecKey {
+    uint4 a, b;
+    uint64_t h;
+    uint32_t run;
+    unsigned long long rep;
+    __device__ __forceinline__ bool same(const uint4& x, const uint4& y) const {
+        return a.x == x.x && a.y == x.y && a.z == x.z && a.w == x.w && b.x == y.x && b.y == y.y && b.z == y.z && b.w == y.w;
+    }
+};
+
+// The bucket-ordered records in kLrecGrid equal contiguous ranges, one per
+// workgroup (a Zipf-hot long word is most of its bucket: ~6 M of C2u's 28 M
+// records in one bucket; a range rarely spans more than one bucket, so its
+// table holds few distinct keys); each thread walks a contiguous share of the
+// range, kLrecBatch records per step with all their loads in flight, and counts
+// runs of equal records in registers before the table (the hot word's runs
+// are long; it is also kept in a two-key register cache).  A workgroup writes
+// its distinct keys with their counts as partials; lrec_merge_kernel then
+// merges each bucket's partials (from the ranges its records span) and inserts
+// every distinct key into the LongTable ONCE (inserting them from every range
+// put ~1000 concurrent inserts of a hot word on one LongTable slot: 1.4 ms).
+#ifndef MRG_LREC_GRID
+#define MRG_LREC_GRID 512
+#endif
+#ifndef MRG_LREC_BATCH
+#define MRG_LREC_BATCH 2
+#endif
+constexpr uint32_t kLrecGrid = MRG_LREC_GRID, kLrecBatch = MRG_LREC_BATCH;
+static_assert(kLrecGrid <= 512 && kLrecSlots <= 4096, "the partials buffer (kLrecPartBytes) holds 512 x 4096");
+static_assert(sizeof(LrecLds) <= 160 * 1024, "LDS");
+__global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t, uint32_t nwg) {
     __shared__ LrecLds A;
-    const uint32_t g = blockIdx.x;
-    const uint32_t cap = t.lrec_cap;
-    uint32_t n = 0;
-    for (int r = 0; r < kWavesPerWG; r++) n += t.lrec_cnt[g * kWavesPerWG + r];
-    if (n == 0) return;
+    const uint64_t T = t.lrec_off[(uint64_t)kLrecBuckets * nwg];  // all records
+    const uint32_t s0 = (uint32_t)(T * blockIdx.x / kLrecGrid), s1 = (uint32_t)(T * (blockIdx.x + 1) / kLrecGrid);
+    if (s0 == s1) {  // (fewer records than ranges: an empty range still says so to lrec_merge_kernel)
+        if (threadIdx.x == 0) t.lrec_pcnt[blockIdx.x] = 0;
+        return;
+    }
     uint32_t direct = 0;
     for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
         A.h[i] = 0;
-        A.rep[i] = kRepUnpub;
+        A.rep[i] = 0;
         A.cnt[i] = 0;
     }
     __syncthreads();
-    for (int r = 0; r < kWavesPerWG; r++)
-    for (uint32_t i = threadIdx.x, nr = min(t.lrec_cnt[g * kWavesPerWG + r], cap); i < nr; i += kLongWG) {
-        // (nr: overflowed regions are flagged and the map repeated)
-        const uint4* recs = t.lrec + ((uint64_t)g * kWavesPerWG + r) * cap * 2;
-        const uint4 a = recs[2 * i], b = recs[2 * i + 1];
-        const uint32_t w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-        uint64_t h = kFnv64Off;
-        uint32_t len = 0;
+    const uint32_t per = (s1 - s0 + kLongWG - 1) / kLongWG;
+    const uint32_t k0 = min(s0 + threadIdx.x * per, s1), k1 = min(k0 + per, s1);
+    // two cached keys per thread (the most recent first): a hot word (~half of
+    // its bucket's records) stays cached between the other words, so it reaches
+    // the LDS counter once per thread, not once per run (its runs average ~2)
+    LrecKey c0 = {}, c1 = {};
+    for (uint32_t kb = k0; kb < k1; kb += kLrecBatch) {
+        uint32_t ix[kLrecBatch];
+        uint4 ra[kLrecBatch], rb[kLrecBatch];
 #pragma unroll
-        for (int q = 0; q < 32; q++) {
-            const uint32_t c = (w[q >> 2] >> (8 * (q & 3))) & 0xFFu;
-            if (c == 0) break;
-            h = fnv1a64_step(h, c);
-            len++;
+        for (uint32_t q = 0; q < kLrecBatch; q++) ix[q] = kb + q < k1 ? t.lrec_idx[kb + q] : 0u;
+#pragma unroll
+        for (uint32_t q = 0; q < kLrecBatch; q++) {
+            const uint4* rec = t.lrec + 2ull * ix[q];
+            ra[q] = kb + q < k1 ? rec[0] : make_uint4(0, 0, 0, 0);
+            rb[q] = kb + q < k1 ? rec[1] : make_uint4(0, 0, 0, 0);
         }
-        const unsigned long long hk = h | 1ull;
-        const unsigned long long me = (unsigned long long)(uintptr_t)(recs + 2 * i);
-        bool done = false;
-        uint32_t slot = (uint32_t)(hk >> 20) & (kLrecSlots - 1);
-        for (int probe = 0; probe < 16 && !done; probe++, slot = (slot + 1) & (kLrecSlots - 1)) {
-            unsigned long long cur = __hip_atomic_load(&A.h[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            if (cur == 0) {
-                cur = atomicCAS(&A.h[slot], 0ull, hk);
-                if (cur == 0) {  // claimed: publish the representative, then count
-                    A.len[slot] = len;
-                    __hip_atomic_store(&A.rep[slot], me, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    atomicAdd(&A.cnt[slot], 1u);
-                    done = true;
-                    break;
-                }
+        // (fully unrolled: a runtime trip count indexed ra/rb dynamically and put
+        // them in scratch, 288 B per lane)
+#pragma unroll
+        for (uint32_t q = 0; q < kLrecBatch; q++) {
+            const uint4 a = ra[q], b = rb[q];
+            if (kb + q >= k1) {
+            } else if (c0.run && c0.same(a, b)) {
+                c0.run++;
+            } else if (c1.run && c1.same(a, b)) {
+                const LrecKey x = c1;
+                c1 = c0;
+                c0 = x;
+                c0.run++;
+            } else {
+                if (c1.run) lrec_count(A, t, c1.a, c1.b, c1.h, 0, c1.rep, c1.run, direct);
+                c1 = c0;
+                c0.a = a;
+                c0.b = b;
+                c0.h = lrec_mix(a, b);
+                c0.rep = (unsigned long long)(uintptr_t)(t.lrec + 2ull * ix[q]);
+                c0.run = 1;
             }
-            if (cur == hk) {
-                const unsigned long long r = __hip_atomic_load(&A.rep[slot], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
-                if (r == kRepUnpub) break;  // being published: never wait here, insert directly
-                const uint4* rr = (const uint4*)(uintptr_t)r;
-                const uint4 ra = rr[0], rb = rr[1];
-                if (ra.x == a.x && ra.y == a.y && ra.z == a.z && ra.w == a.w && rb.x == b.x && rb.y == b.y &&
-                    rb.z == b.z && rb.w == b.w) {
-                    atomicAdd(&A.cnt[slot], 1u);
-                    done = true;
-                }
-            }
-        }
-        if (!done) {
-            long_insert(t, h, (const uint8_t*)(uintptr_t)me, len, 1);
-            direct++;
         }
     }
+    if (c0.run) lrec_count(A, t, c0.a, c0.b, c0.h, 0, c0.rep, c0.run, direct);
+    if (c1.run) lrec_count(A, t, c1.a, c1.b, c1.h, 0, c1.rep, c1.run, direct);
     if (t.dbg) {  // (MRG_DEBUG_TIMES diagnostics: records that missed the LDS table)
         const uint64_t d = wave_sum(direct);
         if ((threadIdx.x & 63) == 0 && d) atomicAdd(&t.ctr->lds_miss, (unsigned long long)d);
+    }
+    __syncthreads();
+    // this range's distinct keys -> partials [range][i], their count at pcount[range]
+    LrecPart* part = t.lrec_part + (uint64_t)blockIdx.x * kLrecSlots;
+    __shared__ uint32_t np;
+    if (threadIdx.x == 0) np = 0;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
+        const uint32_t c = A.cnt[i];
+        if (c) {  // the key's FNV-1a-64 and length from its bytes
+            const uint4 a = from_v4(A.key[i][0]), b = from_v4(A.key[i][1]);
+            uint32_t len;
+            const uint64_t h = lrec_fnv(a, b, len);
+            const uint32_t o = atomicAdd(&np, 1u);
+            part[o] = LrecPart{A.rep[i], h, len, c, lrec_bucket(a, b), 0};
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) t.lrec_pcnt[blockIdx.x] = np;
+}
+
+// First record index of range r (wc_lrec_kernel's split of the T records).
+__device__ __forceinline__ uint64_t lrec_range_start(uint64_t T, uint32_t r) { return T * r / kLrecGrid; }
+
+// One workgroup per bucket: the partials of every range its records span (a
+// wave per range), those of this bucket counted in an LDS table, then one
+// LongTable insert per distinct key.
+__global__ void __launch_bounds__(kLongWG) lrec_merge_kernel(Tables t, uint32_t nwg) {
+    __shared__ LrecLds A;
+    const uint32_t bk = blockIdx.x;
+    const uint64_t T = t.lrec_off[(uint64_t)kLrecBuckets * nwg];
+    const uint64_t bs = t.lrec_off[(uint64_t)bk * nwg], be = t.lrec_off[(uint64_t)(bk + 1) * nwg];
+    if (bs == be) return;
+    // ranges holding records bs and be - 1
+    uint32_t r0 = (uint32_t)min<uint64_t>(bs * kLrecGrid / T, kLrecGrid - 1), r1 = (uint32_t)min<uint64_t>((be - 1) * kLrecGrid / T, kLrecGrid - 1);
+    while (r0 + 1 < kLrecGrid && lrec_range_start(T, r0 + 1) <= bs) r0++;
+    while (r0 > 0 && lrec_range_start(T, r0) > bs) r0--;
+    while (r1 + 1 < kLrecGrid && lrec_range_start(T, r1 + 1) <= be - 1) r1++;
+    while (r1 > 0 && lrec_range_start(T, r1) > be - 1) r1--;
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
+        A.h[i] = 0;
+        A.rep[i] = 0;
+        A.cnt[i] = 0;
+    }
+    __syncthreads();
+    uint32_t direct = 0;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    for (uint32_t r = r0 + wv; r <= r1; r += kLongWG / 64) {
+        const LrecPart* part = t.lrec_part + (uint64_t)r * kLrecSlots;
+        for (uint32_t i = lane, n = t.lrec_pcnt[r]; i < n; i += 64) {
+            const LrecPart p = part[i];
+            if (p.bucket != bk) continue;
+            const uint4* rr = (const uint4*)(uintptr_t)p.rep;
+            lrec_count(A, t, rr[0], rr[1], p.h, p.len, p.rep, p.cnt, direct);
+        }
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < (uint32_t)kLrecSlots; i += kLongWG) {
@@ -230,7 +505,12 @@ __global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t) {
 }
 
 void launch_wc_lrec(const Tables& t, uint32_t nwg, hipStream_t s) {
-    if (t.lrec && nwg) wc_lrec_kernel<<<nwg, kLongWG, 0, s>>>(t);
+    if (!t.lrec || !nwg) return;
+    lrec_hist_kernel<<<nwg, kLongWG, 0, s>>>(t, nwg);
+    lrec_scan_kernel<<<1, 1024, 0, s>>>(t.lrec_off, nwg);
+    lrec_scatter_kernel<<<nwg, kLongWG, 0, s>>>(t, nwg);
+    wc_lrec_kernel<<<kLrecGrid, kLongWG, 0, s>>>(t, nwg);
+    lrec_merge_kernel<<<kLrecBuckets, kLongWG, 0, s>>>(t, nwg);
 }
 
 // ------------------------------------------------------------ grep kernels
@@ -444,13 +724,14 @@ __device__ __forceinline__ int64_t block_start(const uint8_t* in, int64_t q) {
 
 // long_insert (mrgpu_device.h) without its fill counters: returns whether this
 // lane claimed a new slot, and the caller counts claims once per wave.
-__device__ __forceinline__ bool long_try_insert_counted(const Tables& t, uint64_t h, const uint8_t* rep, uint64_t len) {
+__device__ __forceinline__ bool long_try_insert_counted(const Tables& t, uint64_t h, const uint8_t* rep, uint64_t len,
+                                                        uint64_t* slot = nullptr) {
     h |= 1ull;
     bool pending = true, claimed = false;
     uint32_t tries = 0;
     while (__ballot(pending)) {  // wave-uniform: reconverges between attempts
         if (pending) {
-            const int r = long_try(t, h, rep, len, 1);
+            const int r = long_try(t, h, rep, len, 1, slot);
             if (r == kFull) set_status(t.ctr, kStLongFull);
             claimed = r == kClaimed;
             pending = r == kRetry;
@@ -531,9 +812,15 @@ __device__ __forceinline__ void put_line(const Tables& t, uint64_t cap, bool kee
 }
 
 // One lane per hit.  plen == 0: the hits are line starts (empty pattern).
+// sorted: the hits are in position order, and a hit whose line has an earlier
+// hit (no '\n' since it) is dropped; unsorted (the map kernel's order, no sort
+// pass: C3 ~0.13 ms of radix passes), every hit resolves its own line, and the
+// LongTable's insert merges the rare repeats (a line with hits in two chunks).
 __global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
-                                                               Tables t, uint64_t nhits) {
+                                                               Tables t, uint64_t nhits, bool sorted) {
     __shared__ unsigned long long scratch[kLineWaves + 1];
+    __shared__ unsigned long long wg_bytes;
+    if (threadIdx.x == 0) wg_bytes = 0;  // (put_line's barriers order this before the adds below)
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool keep = false, defer = false;
     int64_t s = 0, e = 0;
@@ -543,11 +830,11 @@ __global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __
             s = p;
             keep = true;
         } else {
-            const int64_t lo = i == 0 ? 0 : (int64_t)t.hits[i - 1] + 1;
+            const int64_t lo = i == 0 || !sorted ? 0 : (int64_t)t.hits[i - 1] + 1;
             const int64_t q = last_nl_before(in, lo, p);
             if (q == -2) defer = true;
             else if (q >= 0) { s = q + 1; keep = true; }
-            else if (i == 0) { s = 0; keep = true; }  // no '\n' before the split's first hit
+            else if (lo == 0) { s = 0; keep = true; }  // no '\n' before the hit: the split's first line
             // else: no '\n' since the previous hit, which named this line already
         }
         if (keep) {
@@ -556,12 +843,17 @@ __global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __
         }
     }
     put_line(t, nhits, keep, (uint64_t)s, (uint64_t)e, defer, i, scratch);
+    // the lines' bytes (the record arena's bound), one device atomic per workgroup
+    const uint64_t lb = wave_sum(keep ? (uint64_t)(e - s) : 0ull);
+    if ((threadIdx.x & 63) == 0 && lb) atomicAdd(&wg_bytes, (unsigned long long)lb);
+    __syncthreads();
+    if (threadIdx.x == 0 && wg_bytes) atomicAdd(&t.ctr->line_bytes, wg_bytes);
 }
 
 // Deferred hits: one 256-thread workgroup each, 16 bytes per lane per step
 // (4 KiB steps of aligned blocks), block-wide max / min of the newline found.
 __global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
-                                                                Tables t, uint64_t ndefer, uint64_t cap) {
+                                                                Tables t, uint64_t ndefer, uint64_t cap, bool sorted) {
     __shared__ long long red[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uintptr_t base = (uintptr_t)in;
@@ -580,7 +872,7 @@ __global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* _
         int64_t s = p;
         bool keep = true;
         if (plen != 0) {
-            const int64_t lo = i == 0 ? 0 : (int64_t)t.hits[i - 1] + 1;
+            const int64_t lo = i == 0 || !sorted ? 0 : (int64_t)t.hits[i - 1] + 1;
             // aligned blocks from the one holding p - 1 downwards: block k starts at
             // input offset top - 16 k
             const int64_t top = (int64_t)(((base + (uint64_t)p - 1) & ~(uintptr_t)15) - base);
@@ -599,7 +891,7 @@ __global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* _
                 found = block_max(mine);
             }
             if (found >= 0) s = found + 1;
-            else if (i == 0) s = 0;
+            else if (lo == 0) s = 0;
             else keep = false;
         }
         int64_t e = (int64_t)n;
@@ -621,6 +913,7 @@ __global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* _
             }
         }
         if (tid == 0 && keep) {
+            atomicAdd(&t.ctr->line_bytes, (unsigned long long)(e - s));
             const unsigned long long o = atomicAdd(&t.ctr->nlines, 1ull);
             if (o < cap) {
                 t.lines[2 * o] = (uint64_t)s;
@@ -660,43 +953,159 @@ __device__ uint64_t hash_bytes(const uint8_t* in, int64_t s, int64_t e, uint64_t
     return h;
 }
 
-__global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __restrict__ in, Tables t, uint64_t nlines) {
-    __shared__ unsigned long long scratch[2 * kLineWaves];
+// hash_bytes plus, in the same pass, FNV-1a-32 of every byte (the partition
+// hash, worker.go:76).
+__device__ __forceinline__ uint64_t hash_line(const uint8_t* in, int64_t s, int64_t e, uint32_t& h32) {
+    uint64_t h = kFnv64Off;
+    uint32_t g = 2166136261u;
+    for (int64_t q = s; q < e;) {
+        const int64_t bi = block_start(in, q);
+        const uint8_t* ab = in + bi;
+        uint4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) v[k] = bi + 16 * k < e ? *(const uint4*)(ab + 16 * k) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                const int64_t p = bi + 16 * k + j;
+                if (p < q || p >= e) continue;
+                const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+                h = fnv1a64_step(h, c);
+                g = fnv1a32_step(g, c);
+            }
+        }
+        q = bi + 64;
+    }
+    h32 = g;
+    return h;
+}
+
+// The first 16 bytes of a line (zero-padded past len) as little-endian k0 / k1:
+// the aligned 16-byte blocks holding them (a block is read only if it holds a
+// byte of the line) funnel-shifted by the start's byte offset.
+__device__ __forceinline__ void line_prefix16(const uint8_t* in, int64_t s, uint64_t len, uint64_t& k0, uint64_t& k1) {
+    k0 = k1 = 0;
+    if (len == 0) return;
+    const uintptr_t a = (uintptr_t)(in + s), ab = a & ~(uintptr_t)15;
+    const uint32_t sh = (uint32_t)(a - ab);
+    const uint64_t want = len < 16 ? len : 16;
+    const uint4 v0 = *(const uint4*)ab;
+    const uint4 v1 = ab + 16 < a + want ? *(const uint4*)(ab + 16) : make_uint4(0, 0, 0, 0);
+    const uint64_t q0 = (uint64_t)v0.y << 32 | v0.x, q1 = (uint64_t)v0.w << 32 | v0.z;
+    const uint64_t q2 = (uint64_t)v1.y << 32 | v1.x, q3 = (uint64_t)v1.w << 32 | v1.z;
+    const bool hi = sh >= 8;
+    const uint32_t r = 8 * (sh & 7);
+    const uint64_t a0 = hi ? q1 : q0, a1 = hi ? q2 : q1, a2 = hi ? q3 : q2;
+    k0 = r ? (a0 >> r) | (a1 << (64 - r)) : a0;
+    k1 = r ? (a1 >> r) | (a2 << (64 - r)) : a1;
+    if (len < 8) {
+        k0 &= (1ull << (8 * len)) - 1;
+        k1 = 0;
+    } else if (len < 16) {
+        k1 &= (1ull << (8 * (len - 8))) - 1;
+    }
+}
+
+// One lane per resolved line: hash, insert into the LongTable (the first
+// occurrence claims the slot).  emit: the claiming lane also writes the line's
+// record at a workgroup's share of ctr->nrec / ctr->arena (one cursor pair per
+// workgroup) and the wave copies the claimed lines' bytes into the arena, one
+// line at a time with coalesced stores — the collect pass over the table
+// (C3: 0.26 ms + two host round trips) is not needed.  The record's count
+// (the line's occurrences: mr-X-r holds one KV per occurrence, worker.go:80-92)
+// is the slot's, read by grep_counts_kernel once every insert is in.
+__global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __restrict__ in, Tables t, uint64_t nlines,
+                                                              bool emit) {
+    __shared__ unsigned long long scratch[2 * kLineWaves + 2];
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool claimed = false;
-    uint64_t len = 0;
+    uint64_t len = 0, k0 = 0, k1 = 0;
+    uint32_t h32 = 0;
+    int64_t s = 0;
+    uint64_t slot = 0;
     if (i < nlines) {
-        const int64_t s = (int64_t)t.lines[2 * i], e = (int64_t)t.lines[2 * i + 1];
+        s = (int64_t)t.lines[2 * i];
+        const int64_t e = (int64_t)t.lines[2 * i + 1];
         len = (uint64_t)(e - s);
         uint64_t h;
         if (len <= kHashAll) {
-            h = hash_bytes(in, s, e, kFnv64Off);
+            h = hash_line(in, s, e, h32);
         } else {
             h = hash_bytes(in, s, s + (int64_t)kHashEdge, kFnv64Off);
             h = hash_bytes(in, e - (int64_t)kHashEdge, e, h);
             h = fnv1a64_step(h ^ len, 0xA5u);
         }
-        claimed = long_try_insert_counted(t, h, in + s, len);
+        claimed = long_try_insert_counted(t, h, in + s, len, &slot);
+        if (emit && claimed) {
+            line_prefix16(in, s, len, k0, k1);
+            if (len > kHashAll) {  // (rare: a very long line's partition hash)
+                h32 = 2166136261u;
+                for (uint64_t x = 0; x < len; x++) h32 = fnv1a32_step(h32, in[s + x]);
+            }
+        }
     }
     // fill counters once per workgroup (same-address device atomics serialize)
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint64_t k = wave_sum(claimed ? 1u : 0u), bytes = wave_sum(claimed ? len : 0);
-    if (lane == 0) {
-        scratch[wv] = k;
-        scratch[kLineWaves + wv] = bytes;
+    uint64_t ik = claimed ? 1u : 0u, ib = claimed ? len : 0;  // inclusive wave scans
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint64_t yk = __shfl_up(ik, off), yb = __shfl_up(ib, off);
+        if (lane >= (uint32_t)off) { ik += yk; ib += yb; }
+    }
+    if (lane == 63) {
+        scratch[wv] = ik;
+        scratch[kLineWaves + wv] = ib;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long kk = 0, bb = 0;
-        for (int w = 0; w < kLineWaves; w++) {
-            kk += scratch[w];
-            bb += scratch[kLineWaves + w];
+        for (int w = 0; w < kLineWaves; w++) {  // -> exclusive prefixes per wave
+            const unsigned long long xk = scratch[w], xb = scratch[kLineWaves + w];
+            scratch[w] = kk;
+            scratch[kLineWaves + w] = bb;
+            kk += xk;
+            bb += xb;
         }
+        unsigned long long rb = 0, ab = 0;
         if (kk) {
             atomicAdd(&t.ctr->long_bytes, bb);
             const unsigned long long used = atomicAdd(&t.ctr->long_used, kk) + kk;
             if (used * 10 > (t.lo_mask + 1) * 7) set_status(t.ctr, kStLongFull);
+            if (emit) {
+                rb = atomicAdd(&t.ctr->nrec, kk);
+                ab = atomicAdd(&t.ctr->arena, bb);
+            }
         }
+        scratch[2 * kLineWaves] = rb;
+        scratch[2 * kLineWaves + 1] = ab;
+    }
+    __syncthreads();
+    if (!emit) return;
+    const uint64_t o = scratch[2 * kLineWaves] + scratch[wv] + ik - (claimed ? 1u : 0u);
+    const uint64_t off = scratch[2 * kLineWaves + 1] + scratch[kLineWaves + wv] + ib - (claimed ? len : 0);
+    bool ok = false;
+    if (claimed) {
+        if (o < t.out_cap && off + len <= t.out.arena_n) {
+            ok = true;
+            t.out.k0[o] = k0;
+            t.out.k1[o] = k1;
+            t.out.len[o] = (uint32_t)len;
+            t.out.cnt[o] = slot;  // the slot's index until grep_counts_kernel reads its final count
+            t.out.part[o] = (h32 & 0x7fffffffu) % t.nreduce;
+            t.out.koff[o] = off;
+        } else {
+            set_status(t.ctr, kStRecFull);
+        }
+    }
+    uint64_t m = __ballot(ok);
+    while (m) {  // the claimed lines' bytes, a line at a time by the whole wave
+        const uint32_t j = (uint32_t)__builtin_ctzll(m);
+        m &= m - 1;
+        const uint64_t src = readlane64((uint64_t)s, j), dst = readlane64(off, j);
+        const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((uint32_t)len, j);
+        for (uint32_t x = lane; x < l; x += 64) t.out.arena[dst + x] = in[src + x];
     }
 }
 
@@ -919,6 +1328,8 @@ __global__ void clear_long_kernel(Tables t) {
         t.ctr->status = 0;
         t.ctr->long_used = 0;
         t.ctr->long_bytes = 0;
+        t.ctr->nrec = 0;
+        t.ctr->arena = 0;
     }
 }
 
@@ -955,21 +1366,33 @@ void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int g
     grep_all_lines_kernel<<<grid * 4, 256, 0, s>>>(in, n, t);
 }
 
-void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, hipStream_t s) {
+void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, bool sorted,
+                         hipStream_t s) {
     if (nhits == 0) return;
-    grep_resolve_kernel<<<(unsigned)((nhits + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, n, plen, t, nhits);
+    grep_resolve_kernel<<<(unsigned)((nhits + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, n, plen, t, nhits, sorted);
 }
 
 void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t ndefer,
-                              uint64_t nhits, hipStream_t s) {
+                              uint64_t nhits, bool sorted, hipStream_t s) {
     if (ndefer == 0) return;
     const uint64_t g = ndefer < 4096 ? ndefer : 4096;
-    grep_resolve_long_kernel<<<(unsigned)g, 256, 0, s>>>(in, n, plen, t, ndefer, nhits);
+    grep_resolve_long_kernel<<<(unsigned)g, 256, 0, s>>>(in, n, plen, t, ndefer, nhits, sorted);
 }
 
-void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, hipStream_t s) {
+// The emitted records' counts: cnt held the claimed slot's index.
+__global__ void grep_counts_kernel(Tables t) {
+    const uint64_t n = t.ctr->nrec < t.out_cap ? t.ctr->nrec : t.out_cap;
+    for (uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (uint64_t)gridDim.x * blockDim.x)
+        t.out.cnt[o] = t.lo[t.out.cnt[o] & t.lo_mask].count;
+}
+
+void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, bool emit, hipStream_t s) {
     if (nlines == 0) return;
-    grep_insert_kernel<<<(unsigned)((nlines + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, t, nlines);
+    grep_insert_kernel<<<(unsigned)((nlines + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, t, nlines, emit);
+    if (emit) {
+        const uint64_t g = (nlines + 255) / 256;
+        grep_counts_kernel<<<(unsigned)(g < 2048 ? g : 2048), 256, 0, s>>>(t);
+    }
 }
 
 __global__ void collect_mark_kernel(Counters* ctr) { ctr->nrec_base = ctr->nrec; }

@@ -613,15 +613,21 @@ __global__ void __launch_bounds__(kScanThreads) line_offsets_kernel(Recs r, cons
 // into LDS, then the block copies the range out with 16-byte stores (byte stores
 // only at the range's two ends, which neighbouring blocks share).  A range longer
 // than the LDS buffer (very long keys) is written directly, byte by byte.
-constexpr uint32_t kWlLines = 256;
+constexpr uint32_t kWlLines = 256;  // threads per workgroup
+// lines per workgroup step: grep's output lines (the line twice, ~160 B at C3)
+// overflowed 256 lines' staging, and an unstaged block stores byte by byte
+// (slow into device memory, slower into pinned host memory)
+template <int kApp>
+constexpr uint32_t wl_lines() { return kApp == 1 ? 256u : 128u; }
 template <int kApp>
 __global__ void __launch_bounds__(kWlLines) write_lines_staged_kernel(Recs r, const uint32_t* perm, uint64_t n,
                                                                         const uint64_t* off, uint8_t* out) {
     constexpr uint32_t kWlBytes = kApp == 1 ? 16384 : 49152;  // C2 lines ~14 B, C3 lines ~120 B
     __shared__ __attribute__((aligned(16))) uint8_t buf[kWlBytes];
     const uint32_t tid = threadIdx.x;
-    for (uint64_t i0 = (uint64_t)blockIdx.x * kWlLines; i0 < n; i0 += (uint64_t)gridDim.x * kWlLines) {
-        const uint64_t iend = i0 + kWlLines < n ? i0 + kWlLines : n;
+    constexpr uint32_t L = wl_lines<kApp>();
+    for (uint64_t i0 = (uint64_t)blockIdx.x * L; i0 < n; i0 += (uint64_t)gridDim.x * L) {
+        const uint64_t iend = i0 + L < n ? i0 + L : n;
         const uint64_t start = off[i0], end = off[iend];  // off[n] = the total
         const uint64_t a0 = start & ~15ull;
         const bool staged = end - a0 <= kWlBytes;  // block-uniform
@@ -1529,9 +1535,13 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         RCHK(ws->scan.prepare(ntiles, s, &st));
         if (app != 1) line_offsets_kernel<2><<<(unsigned)ntiles, kScanThreads, 0, s>>>(r, pa, n, off, st);
         else line_offsets_kernel<1><<<(unsigned)ntiles, kScanThreads, 0, s>>>(r, pa, n, off, st);
-        const unsigned wl_grid = (unsigned)std::min<uint64_t>((n + kWlLines - 1) / kWlLines, 8192);
-        if (app != 1) write_lines_staged_kernel<2><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, out);
-        else write_lines_staged_kernel<1><<<wl_grid, kWlLines, 0, s>>>(r, pa, n, off, out);
+        if (app != 1) {
+            const unsigned g = (unsigned)std::min<uint64_t>((n + wl_lines<2>() - 1) / wl_lines<2>(), 8192);
+            write_lines_staged_kernel<2><<<g, kWlLines, 0, s>>>(r, pa, n, off, out);
+        } else {
+            const unsigned g = (unsigned)std::min<uint64_t>((n + wl_lines<1>() - 1) / wl_lines<1>(), 8192);
+            write_lines_staged_kernel<1><<<g, kWlLines, 0, s>>>(r, pa, n, off, out);
+        }
         part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, nparts, !all, ws->offs.as<uint64_t>());
         RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
         return 0;

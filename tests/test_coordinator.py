@@ -164,15 +164,17 @@ def test_coordinator_forked_worker_crash_still_succeeds(tmp_path):
     """-w 2 with forked worker 0 dying while it holds its second task: the task
     is re-issued to worker 1 (coordinator.go:70-77); the job's status follows
     Done(), so it exits 0 and reports the crash as information."""
-    files = cases.synthetic(C.KIND_ASCII, 5000, [200_000, 150_000, 100_000, 120_000], 64)
+    # (16 map and 8 reduce tasks: with 4 + 4, worker 1 sometimes finished every
+    # task before worker 0 asked for its second, and nothing crashed)
+    files = cases.synthetic(C.KIND_ASCII, 5000, [200_000, 150_000, 100_000, 120_000] * 4, 64)
     paths = _write(tmp_path, files)
     env = dict(os.environ, MRG_WORKER_CRASH_AFTER="1", MRG_WORKER_CRASH_INDEX="0")
-    r = subprocess.run([COORD, "-n", "4", "-w", "2", "--sock", str(tmp_path / "s"), "--task-timeout", "2", "wc"]
+    r = subprocess.run([COORD, "-n", "8", "-w", "2", "--sock", str(tmp_path / "s"), "--task-timeout", "2", "wc"]
                        + paths, cwd=tmp_path, env=env, capture_output=True, timeout=240)
     assert r.returncode == 0, r.stderr.decode()[-2000:]
     info = json.loads(r.stdout.decode().strip().splitlines()[-1])
     assert info["done"] and info["workers_failed"] == 1 and info["reissued"] >= 1
-    assert [(tmp_path / f"mr-out-{k}").read_bytes() for k in range(4)] == O.c_partitioned("wc", files, 4)
+    assert [(tmp_path / f"mr-out-{k}").read_bytes() for k in range(8)] == O.c_partitioned("wc", files, 8)
     assert not list(tmp_path.glob("mr-*.tmp-*"))  # unique temp files, all renamed
 
 

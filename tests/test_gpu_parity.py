@@ -138,9 +138,37 @@ def test_wc_long_words_many(wctx, list_cap, lrec):
         wctx.set_option("long_records", 0)
 
 
-def test_grep_synthetic(ctx):
-    files = cases.synthetic_grep(50000, [3_000_000, 1_000_001], 5)
-    check(ctx, "grep:distributed", files, nreduces=(1, 10))
+def test_wc_long_records_fewer_than_ranges(wctx):
+    """Splits with fewer 17-32-byte records than wc_lrec_kernel has ranges (512)
+    after a split with millions of them on the same context: the empty ranges'
+    partial counts must not be the previous split's (mrcoord's small files
+    caught that)."""
+    files = [cases.long_words(3_000_000, 1), cases.long_words(2_000, 5)] + \
+        cases.synthetic(C.KIND_UTF8, 20000, [1_000, 90_000, 7], 61, 0.001) + [cases.long_words(40, 6)]
+    for f in files:
+        assert gpu_partitioned(wctx, "wc", [f], 10) == O.c_partitioned("wc", [f], 10)
+    check(wctx, "wc", files, nreduces=(10,))
+
+
+@pytest.mark.parametrize("sort_hits,emit", [(0, 1), (1, 1), (0, 0)])
+def test_grep_synthetic(ctx, sort_hits, emit):
+    """grep over synthetic lines; the hits resolved in the map kernel's order
+    (default) or sorted by position first (option grep_sort_hits = 1); the
+    records written by the LongTable insert as it claims a line (default) or by
+    a collect pass over the table afterwards (option grep_emit = 0); the edge
+    cases (lines across chunks, long lines, no final newline) for the
+    non-default paths too."""
+    ctx.set_option("grep_sort_hits", sort_hits)
+    ctx.set_option("grep_emit", emit)
+    try:
+        files = cases.synthetic_grep(50000, [3_000_000, 1_000_001], 5)
+        check(ctx, "grep:distributed", files, nreduces=(1, 10))
+        if sort_hits or not emit:
+            for name, (gf, pat) in sorted(cases.grep_edge_cases().items()):
+                check(ctx, "grep:" + pat.decode("utf-8", "surrogateescape"), gf, nreduces=(4,))
+    finally:
+        ctx.set_option("grep_sort_hits", 0)
+        ctx.set_option("grep_emit", 1)
 
 
 def test_wc_lds_overflow_and_table_growth(ctx):
@@ -905,12 +933,12 @@ def test_host_input_streamed_in_pieces(ctx, app):
         ctx.set_option("dict_min_bytes", 0)
 
 
-@pytest.mark.parametrize("direct", [0, -1])
+@pytest.mark.parametrize("direct", [0, -1, 1])
 def test_run_job_output_to_host(ctx, direct):
-    """mrg_run_job's wc output lines written straight into pinned host memory by
-    the formatting kernel (option out_direct, default) or through a device buffer
-    and a copy (-1): the same bytes as the oracle on wc edge cases (long words,
-    an empty output); grep (which always takes the copy) alongside."""
+    """mrg_run_job's output lines written straight into pinned host memory by
+    the formatting kernel (option out_direct, default), through a device buffer
+    and a copy (-1), or directly for wc only (1): the same bytes as the oracle
+    on wc edge cases (long words, an empty output) and grep edge cases."""
     ctx.set_option("out_direct", direct)
     try:
         edge = cases.edge_cases()
