@@ -1154,9 +1154,11 @@ static bool go_valid_utf8(const uint8_t* p, size_t n) {
 }
 
 // grep map (mrapps/dgrep.go:18-36) with a literal pattern:
-//   grep_map_kernel -> occurrence positions (one per line per chunk) -> sort ->
+//   grep_map_kernel -> occurrence positions (one per line per chunk) ->
 //   grep_resolve_kernel (+ _long) -> one (start, end) per matching line
-//   occurrence -> the LongTable sized for them -> collect.
+//   occurrence -> the LongTable sized for them, whose insert writes each
+//   distinct line's record (option grep_emit = 0: a collect pass instead;
+//   option grep_sort_hits = 1: the hits sorted by position first).
 // The pattern is a literal (regexp.QuoteMeta semantics).  dgrep.go:20-23 returns
 // no lines when regexp.Compile fails, which for a quoted literal happens exactly
 // when it is not valid UTF-8; a pattern holding '\n' matches no line of
@@ -1198,15 +1200,23 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
         }
         HCHK(c, hipGetLastError());
         HCHK(c, hipEventRecord(c->ev[1], c->s));
-        if ((rc = read_counters(c))) return rc;
-        if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
-        const uint64_t nhits = c->h_ctr->nlist;
-        // sort the hits by position, resolve their lines
-        HCHK(c, c->ghits.ensure_grow(nhits * 8 + 64));
+        // Unsorted hits (default): the line resolution follows the map kernel with
+        // no host read in between (it reads the hit counts on the device, over
+        // buffers sized for the list's capacity); the one counter read after it
+        // also tells whether the map's list overflowed (then everything repeats
+        // with a larger list).  Sorted (option grep_sort_hits): the sort needs the
+        // count on the host first.
+        const bool sorted = c->grep_sort_hits, dev = !sorted;
+        if (sorted) {
+            if ((rc = read_counters(c))) return rc;
+            if (grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
+        }
+        const uint64_t nhits = dev ? c->list_cap : c->h_ctr->nlist;
+        if (sorted) HCHK(c, c->ghits.ensure_grow(nhits * 8 + 64));
         HCHK(c, c->glines.ensure_grow(nhits * 16 + 64));
         HCHK(c, c->gdefer.ensure_grow(nhits * 8 + 64));
         t = make_tables(c);
-        if (c->grep_sort_hits) {
+        if (sorted) {
             unsigned bits = 1;
             while (bits < 64 && (len >> bits) != 0) bits++;
             if (nhits && sort_u64_keys(c->rws, t.list, (uint64_t*)c->ghits.p, nhits, bits, c->s))
@@ -1214,11 +1224,13 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
         } else {
             t.hits = t.list;  // the map kernel's order (grep_resolve_kernel: unsorted)
         }
-        launch_grep_resolve(in, len, (uint32_t)plen, t, nhits, c->grep_sort_hits, c->s);
+        launch_grep_resolve(in, len, (uint32_t)plen, t, nhits, dev, sorted, c->s);
+        if (dev) launch_grep_resolve_long(in, len, (uint32_t)plen, t, 0, nhits, true, false, c->s);
         HCHK(c, hipGetLastError());
         if ((rc = read_counters(c))) return rc;
-        if (c->h_ctr->ndefer) {
-            launch_grep_resolve_long(in, len, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, c->grep_sort_hits, c->s);
+        if (dev && grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
+        if (sorted && c->h_ctr->ndefer) {
+            launch_grep_resolve_long(in, len, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, false, true, c->s);
             HCHK(c, hipGetLastError());
             if ((rc = read_counters(c))) return rc;
         }

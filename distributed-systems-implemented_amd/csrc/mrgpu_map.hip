@@ -817,43 +817,53 @@ __device__ __forceinline__ void put_line(const Tables& t, uint64_t cap, bool kee
 // pass: C3 ~0.13 ms of radix passes), every hit resolves its own line, and the
 // LongTable's insert merges the rare repeats (a line with hits in two chunks).
 __global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
-                                                               Tables t, uint64_t nhits, bool sorted) {
+                                                               Tables t, uint64_t cap, const unsigned long long* dn,
+                                                               bool sorted) {
     __shared__ unsigned long long scratch[kLineWaves + 1];
     __shared__ unsigned long long wg_bytes;
     if (threadIdx.x == 0) wg_bytes = 0;  // (put_line's barriers order this before the adds below)
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool keep = false, defer = false;
-    int64_t s = 0, e = 0;
-    if (i < nhits) {
-        const int64_t p = (int64_t)t.hits[i];
-        if (plen == 0) {
-            s = p;
-            keep = true;
-        } else {
-            const int64_t lo = i == 0 || !sorted ? 0 : (int64_t)t.hits[i - 1] + 1;
-            const int64_t q = last_nl_before(in, lo, p);
-            if (q == -2) defer = true;
-            else if (q >= 0) { s = q + 1; keep = true; }
-            else if (lo == 0) { s = 0; keep = true; }  // no '\n' before the hit: the split's first line
-            // else: no '\n' since the previous hit, which named this line already
+    // dn: the hit count read here (the map kernel's cursor, no host round trip);
+    // the workgroups stride over it in whole-workgroup steps (put_line's barriers)
+    const uint64_t nhits = dn ? (*dn < cap ? *dn : cap) : cap;
+    for (uint64_t base = (uint64_t)blockIdx.x * kLineWG; base < nhits; base += (uint64_t)gridDim.x * kLineWG) {
+        const uint64_t i = base + threadIdx.x;
+        bool keep = false, defer = false;
+        int64_t s = 0, e = 0;
+        if (i < nhits) {
+            const int64_t p = (int64_t)t.hits[i];
+            if (plen == 0) {
+                s = p;
+                keep = true;
+            } else {
+                const int64_t lo = i == 0 || !sorted ? 0 : (int64_t)t.hits[i - 1] + 1;
+                const int64_t q = last_nl_before(in, lo, p);
+                if (q == -2) defer = true;
+                else if (q >= 0) { s = q + 1; keep = true; }
+                else if (lo == 0) { s = 0; keep = true; }  // no '\n' before the hit: the split's first line
+                // else: no '\n' since the previous hit, which named this line already
+            }
+            if (keep) {
+                e = first_nl_from(in, (int64_t)n, p + plen);
+                if (e == -2) { keep = false; defer = true; }
+            }
         }
-        if (keep) {
-            e = first_nl_from(in, (int64_t)n, p + plen);
-            if (e == -2) { keep = false; defer = true; }
-        }
+        put_line(t, cap, keep, (uint64_t)s, (uint64_t)e, defer, i, scratch);
+        // the lines' bytes (the record arena's bound)
+        const uint64_t lb = wave_sum(keep ? (uint64_t)(e - s) : 0ull);
+        if ((threadIdx.x & 63) == 0 && lb) atomicAdd(&wg_bytes, (unsigned long long)lb);
     }
-    put_line(t, nhits, keep, (uint64_t)s, (uint64_t)e, defer, i, scratch);
-    // the lines' bytes (the record arena's bound), one device atomic per workgroup
-    const uint64_t lb = wave_sum(keep ? (uint64_t)(e - s) : 0ull);
-    if ((threadIdx.x & 63) == 0 && lb) atomicAdd(&wg_bytes, (unsigned long long)lb);
     __syncthreads();
-    if (threadIdx.x == 0 && wg_bytes) atomicAdd(&t.ctr->line_bytes, wg_bytes);
+    if (threadIdx.x == 0 && wg_bytes) atomicAdd(&t.ctr->line_bytes, wg_bytes);  // one device atomic per workgroup
 }
 
 // Deferred hits: one 256-thread workgroup each, 16 bytes per lane per step
 // (4 KiB steps of aligned blocks), block-wide max / min of the newline found.
 __global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
-                                                                Tables t, uint64_t ndefer, uint64_t cap, bool sorted) {
+                                                                Tables t, uint64_t ndefer_h, uint64_t cap, bool sorted,
+                                                                bool dev_count) {
+    // dev_count: the deferred count read here (no host round trip; none: every
+    // workgroup returns at once)
+    const uint64_t ndefer = dev_count ? (t.ctr->ndefer < cap ? t.ctr->ndefer : cap) : ndefer_h;
     __shared__ long long red[4];
     const uint32_t tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const uintptr_t base = (uintptr_t)in;
@@ -1099,13 +1109,37 @@ __global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __r
             set_status(t.ctr, kStRecFull);
         }
     }
+    // The claimed lines' bytes by the whole wave, four lines per step with all
+    // four lines' loads issued before their stores (a line at a time left one
+    // load round trip per line on each wave's critical path: insert 0.28 ->
+    // 0.45 ms on C3).
+    constexpr int kCopyLines = 4;
     uint64_t m = __ballot(ok);
-    while (m) {  // the claimed lines' bytes, a line at a time by the whole wave
-        const uint32_t j = (uint32_t)__builtin_ctzll(m);
-        m &= m - 1;
-        const uint64_t src = readlane64((uint64_t)s, j), dst = readlane64(off, j);
-        const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((uint32_t)len, j);
-        for (uint32_t x = lane; x < l; x += 64) t.out.arena[dst + x] = in[src + x];
+    while (m) {
+        uint64_t src[kCopyLines], dst[kCopyLines];
+        uint32_t l[kCopyLines], lmax = 0;
+#pragma unroll
+        for (int k = 0; k < kCopyLines; k++) {
+            src[k] = dst[k] = 0;
+            l[k] = 0;
+            if (m) {
+                const uint32_t j = (uint32_t)__builtin_ctzll(m);
+                m &= m - 1;
+                src[k] = readlane64((uint64_t)s, j);
+                dst[k] = readlane64(off, j);
+                l[k] = (uint32_t)__builtin_amdgcn_readlane((uint32_t)len, j);
+                lmax = l[k] > lmax ? l[k] : lmax;
+            }
+        }
+        for (uint32_t x0 = 0; x0 < lmax; x0 += 64) {
+            const uint32_t x = x0 + lane;
+            uint8_t b[kCopyLines];
+#pragma unroll
+            for (int k = 0; k < kCopyLines; k++) b[k] = x < l[k] ? in[src[k] + x] : (uint8_t)0;
+#pragma unroll
+            for (int k = 0; k < kCopyLines; k++)
+                if (x < l[k]) t.out.arena[dst[k] + x] = b[k];
+        }
     }
 }
 
@@ -1366,17 +1400,20 @@ void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int g
     grep_all_lines_kernel<<<grid * 4, 256, 0, s>>>(in, n, t);
 }
 
-void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, bool sorted,
-                         hipStream_t s) {
+void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, bool dev_count,
+                         bool sorted, hipStream_t s) {
     if (nhits == 0) return;
-    grep_resolve_kernel<<<(unsigned)((nhits + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, n, plen, t, nhits, sorted);
+    uint64_t g = (nhits + kLineWG - 1) / kLineWG;
+    if (dev_count && g > 1024) g = 1024;  // (nhits = the list's capacity: the workgroups stride)
+    grep_resolve_kernel<<<(unsigned)g, kLineWG, 0, s>>>(in, n, plen, t, nhits, dev_count ? &t.ctr->nlist : nullptr,
+                                                        sorted);
 }
 
 void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t ndefer,
-                              uint64_t nhits, bool sorted, hipStream_t s) {
-    if (ndefer == 0) return;
-    const uint64_t g = ndefer < 4096 ? ndefer : 4096;
-    grep_resolve_long_kernel<<<(unsigned)g, 256, 0, s>>>(in, n, plen, t, ndefer, nhits, sorted);
+                              uint64_t nhits, bool dev_count, bool sorted, hipStream_t s) {
+    if (!dev_count && ndefer == 0) return;
+    const uint64_t g = dev_count ? 1024 : ndefer < 4096 ? ndefer : 4096;
+    grep_resolve_long_kernel<<<(unsigned)g, 256, 0, s>>>(in, n, plen, t, ndefer, nhits, sorted, dev_count);
 }
 
 // The emitted records' counts: cnt held the claimed slot's index.

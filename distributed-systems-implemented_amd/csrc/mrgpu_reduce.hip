@@ -1102,6 +1102,12 @@ static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
     RCHK(hipStreamSynchronize(s));
     const uint32_t m = (uint32_t)(ws->h_pinned[8] & 0xFFFFFFFFu);
     if (m == 0) return 0;
+    static const bool dbg = getenv("MRG_DEBUG_TIES") != nullptr;
+    hipEvent_t ev[2];
+    if (dbg) {
+        for (auto& e : ev) (void)hipEventCreate(&e);
+        (void)hipEventRecord(ev[0], s);
+    }
     uint32_t* va = ws->key_b.as<uint32_t>();
     uint32_t* vb = va + n;
     const unsigned g = (unsigned)((m + 255) / 256 < 4096 ? (m + 255) / 256 : 4096);
@@ -1120,10 +1126,13 @@ static int sort_long_runs(ReduceWs* ws, const Recs& r, uint32_t* perm, uint64_t 
         sorted = merge_sort_u32(va, vb, m, FullLess{r, ext}, s);
     }
     scatter_perm_kernel<<<g, 256, 0, s>>>(perm, pos, d_m, sorted);
-    static const bool dbg = getenv("MRG_DEBUG_TIES") != nullptr;
-    if (dbg) {
+    if (dbg) {  // (MRG_DEBUG_TIES: the long runs' sort, gather to scatter, by HIP events)
+        (void)hipEventRecord(ev[1], s);
         RCHK(hipStreamSynchronize(s));
-        fprintf(stderr, "[ties] long runs: %u members merge-sorted\n", m);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ev[0], ev[1]);
+        fprintf(stderr, "[ties] long runs: %u members merge-sorted in %.1f us\n", m, 1e3 * ms);
+        for (auto& e : ev) (void)hipEventDestroy(e);
     }
     return 0;
 }

@@ -171,6 +171,19 @@ def test_grep_synthetic(ctx, sort_hits, emit):
         ctx.set_option("grep_emit", 1)
 
 
+def test_grep_list_overflow_rerun(ctx):
+    """A hit list far smaller than the split's hits (option list_cap): the line
+    resolution, which reads the hit count on the device, runs over a truncated
+    list; the counter read after it sees the overflow, and the map repeats with
+    a larger list — exact output either way."""
+    files = cases.synthetic_grep(50000, [2_000_000], 8, match_rate=0.05)
+    ctx.set_option("list_cap", 500)
+    try:
+        check(ctx, "grep:distributed", files, nreduces=(10,))
+    finally:
+        ctx.set_option("list_cap", 0)
+
+
 def test_wc_lds_overflow_and_table_growth(ctx):
     """Force the HBM paths: tiny HBM table (growth + re-run) and a corpus whose
     distinct keys overflow every workgroup's LDS table."""
