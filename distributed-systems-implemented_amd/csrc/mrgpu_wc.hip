@@ -1113,20 +1113,26 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
 // sets = 4096 short keys + 1024 mid keys: a C2 bucket holds ~2 K distinct
 // keys); later rounds of high-cardinality splits use one 1024-thread workgroup
 // per CU with twice the keys, so a bucket settles in fewer rounds.
-template <int NS, int NM, int NW>
+// (SW: ways per short set, 4 or 2 — A/B option MRG_AGG_WAYS: a 2-way set is one
+// 16-byte read instead of two, with twice the sets for the same keys)
+#ifndef MRG_AGG_WAYS
+#define MRG_AGG_WAYS 4
+#endif
+template <int NS, int NM, int NW, int SW = 4>
 struct alignas(16) AggLdsT {
-    static constexpr int kShortSets = NS, kMidSets = NM;
+    static constexpr int kShortSets = NS, kMidSets = NM, kShortWays = SW;
+    static_assert(SW == 4 || SW == 2, "short set ways");
     static constexpr uint32_t kWaves = NW;
     static constexpr uint32_t kParts = NW / kAggSegs;  // waves per miss segment
-    unsigned long long sk[NS * 4];
+    unsigned long long sk[NS * SW];
     unsigned long long mk[NM * 4 * 2];  // way w of set s: mk[2(4s+w)] = k0, mk[2(4s+w)+1] = k1
-    uint32_t sc[NS * 4 + kWave];        // counts (+ per-lane dummies for branch-free adds)
+    uint32_t sc[NS * SW + kWave];       // counts (+ per-lane dummies for branch-free adds)
     uint32_t mc[NM * 4 + kWave];
     unsigned long long red[4 * NW + 4];  // block_add4 / block_alloc scratch
     uint32_t ncur8[kAggSegs], ncur16[kAggSegs];  // misses appended to each segment
 };
-using AggLds = AggLdsT<1024, 256, kAggThreads / kWave>;
-using AggLdsBig = AggLdsT<2048, 512, 2 * kAggThreads / kWave>;
+using AggLds = AggLdsT<1024 * 4 / MRG_AGG_WAYS, 256, kAggThreads / kWave, MRG_AGG_WAYS>;
+using AggLdsBig = AggLdsT<2048 * 4 / MRG_AGG_WAYS, 512, 2 * kAggThreads / kWave, MRG_AGG_WAYS>;
 static_assert(AggLds::kWaves == kAggSegs && AggLdsBig::kWaves == 2 * kAggSegs, "waves per miss segment");
 static_assert(2 * sizeof(AggLds) <= 160 * 1024, "two aggregator workgroups per CU");
 static_assert(sizeof(AggLdsBig) <= 160 * 1024, "one big aggregator workgroup per CU");
@@ -1135,16 +1141,24 @@ static_assert(sizeof(AggLdsBig) <= 160 * 1024, "one big aggregator workgroup per
 // and retries: the winner, often the same key, published its way with its CAS).
 constexpr int kClaimAttempts = 4;
 __device__ __forceinline__ uint32_t second_hash(uint32_t h) { return __builtin_amdgcn_alignbit(h, h, 16) * 0xC2B2AE3Du; }
-template <int NSETS>
-__device__ __forceinline__ uint32_t set_base(uint32_t h) { return __umulhi(h, NSETS) * 4; }
+template <int NSETS, int WAYS = 4>
+__device__ __forceinline__ uint32_t set_base(uint32_t h) { return __umulhi(h, NSETS) * WAYS; }
+// the first way of a short key's set (first or second choice)
+template <class AL>
+__device__ __forceinline__ uint32_t sbase(uint32_t h) { return set_base<AL::kShortSets, AL::kShortWays>(h); }
 
-// 4-bit masks of the ways of a short set holding k / holding 0
+// way masks (4 or 2 bits) of a short set holding k / holding 0
 template <class AL>
 __device__ __forceinline__ void short_set_masks(const AL& A, uint32_t base, uint64_t k, uint32_t& m, uint32_t& z) {
     const u64x2 a = *(const lds_u64x2*)(&A.sk[base]);
-    const u64x2 b = *(const lds_u64x2*)(&A.sk[base + 2]);
-    m = (a.x == k ? 1u : 0u) | (a.y == k ? 2u : 0u) | (b.x == k ? 4u : 0u) | (b.y == k ? 8u : 0u);
-    z = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u) | (b.x == 0 ? 4u : 0u) | (b.y == 0 ? 8u : 0u);
+    if constexpr (AL::kShortWays == 2) {
+        m = (a.x == k ? 1u : 0u) | (a.y == k ? 2u : 0u);
+        z = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u);
+    } else {
+        const u64x2 b = *(const lds_u64x2*)(&A.sk[base + 2]);
+        m = (a.x == k ? 1u : 0u) | (a.y == k ? 2u : 0u) | (b.x == k ? 4u : 0u) | (b.y == k ? 8u : 0u);
+        z = (a.x == 0 ? 1u : 0u) | (a.y == 0 ? 2u : 0u) | (b.x == 0 ? 4u : 0u) | (b.y == 0 ? 8u : 0u);
+    }
 }
 
 // Slow path of a short key absent from the first read of its first set:
@@ -1159,7 +1173,7 @@ __device__ bool short_insert_slow(AL& A, uint64_t k, uint32_t h, uint32_t add) {
     for (int attempt = 0; attempt < kClaimAttempts; attempt++) {
         bool raced = false;
         for (int c = 0; c < 2 && !raced; c++) {
-            const uint32_t base = set_base<AL::kShortSets>(c == 0 ? h : second_hash(h));
+            const uint32_t base = sbase<AL>(c == 0 ? h : second_hash(h));
             uint32_t m, z;
             short_set_masks(A, base, k, m, z);
             if (m) {
@@ -1231,8 +1245,8 @@ __device__ bool mid_insert(AL& A, uint64_t k0, uint64_t k1, uint32_t h, uint32_t
 template <class AL>
 __device__ __forceinline__ int short_find_exact(const AL& A, uint64_t k, uint32_t h) {
     for (int c = 0; c < 2; c++) {
-        const uint32_t base = set_base<AL::kShortSets>(c == 0 ? h : second_hash(h));
-        for (uint32_t w = 0; w < 4; w++)
+        const uint32_t base = sbase<AL>(c == 0 ? h : second_hash(h));
+        for (uint32_t w = 0; w < (uint32_t)AL::kShortWays; w++)
             if (A.sk[base + w] == k) return (int)(base + w);
     }
     return -1;
@@ -1423,7 +1437,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                 uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
-                    base[u] = set_base<AL::kShortSets>(h[u]);
+                    base[u] = sbase<AL>(h[u]);
                     short_set_masks(A, base[u], ((uint64_t)cur[u].y << 32) | cur[u].x, m[u], z[u]);
                 }
                 bool slow[kAggUnroll];
@@ -1432,7 +1446,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
                     const bool hit = valid && m[u] != 0;
                     slow[u] = valid && m[u] == 0;
-                    const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)AL::kShortSets * 4 + lane;
+                    const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)(AL::kShortSets * AL::kShortWays) + lane;
                     if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
                     else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
@@ -1455,14 +1469,14 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     uint32_t m, z;
-                    short_set_masks(A, set_base<AL::kShortSets>(h[u]), ((uint64_t)cur[u].y << 32) | cur[u].x, m, z);
+                    short_set_masks(A, sbase<AL>(h[u]), ((uint64_t)cur[u].y << 32) | cur[u].x, m, z);
                     mz[u] = m | z << 4;
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     if ((cur[u].x | cur[u].y) != 0 && mz[u] == 0) {
                         uint32_t m2, z2;
-                        short_set_masks(A, set_base<AL::kShortSets>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
+                        short_set_masks(A, sbase<AL>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
                                         m2, z2);
                         mz[u] = m2 << 8 | z2 << 12 | 1u << 16;  // bit 16: second set read
                     }
@@ -1475,10 +1489,10 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     // both sets read, full, without the key: final for this round (ways are
                     // never freed), so the key is deferred without the claim path
                     if (valid && (mz[u] >> 8) == (1u << 8)) full |= 1u << u;
-                    const uint32_t ci = !valid   ? (uint32_t)AL::kShortSets * 4 + lane
-                                        : m != 0  ? set_base<AL::kShortSets>(h[u]) + __builtin_ctz(m)
-                                        : m2 != 0 ? set_base<AL::kShortSets>(second_hash(h[u])) + __builtin_ctz(m2)
-                                                  : (uint32_t)AL::kShortSets * 4 + lane;
+                    const uint32_t ci = !valid   ? (uint32_t)(AL::kShortSets * AL::kShortWays) + lane
+                                        : m != 0  ? sbase<AL>(h[u]) + __builtin_ctz(m)
+                                        : m2 != 0 ? sbase<AL>(second_hash(h[u])) + __builtin_ctz(m2)
+                                                  : (uint32_t)(AL::kShortSets * AL::kShortWays) + lane;
                     if (valid && (m | m2) == 0 && !((full >> u) & 1u)) slow |= 1u << u;
                     if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
                     else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1641,7 +1655,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                 uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
-                    base[u] = set_base<AL::kShortSets>(h[u]);
+                    base[u] = sbase<AL>(h[u]);
                     short_set_masks(A, base[u], ((uint64_t)cur[u].y << 32) | cur[u].x, m[u], z[u]);
                 }
                 bool slow[kAggUnroll];
@@ -1650,7 +1664,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     const bool valid = (cur[u].x | cur[u].y) != 0;  // keys have k0 != 0
                     const bool hit = valid && m[u] != 0;
                     slow[u] = valid && m[u] == 0;
-                    const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)AL::kShortSets * 4 + lane;
+                    const uint32_t ci = hit ? base[u] + __builtin_ctz(m[u]) : (uint32_t)(AL::kShortSets * AL::kShortWays) + lane;
                     if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
                     else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
@@ -1673,14 +1687,14 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     uint32_t m, z;
-                    short_set_masks(A, set_base<AL::kShortSets>(h[u]), ((uint64_t)cur[u].y << 32) | cur[u].x, m, z);
+                    short_set_masks(A, sbase<AL>(h[u]), ((uint64_t)cur[u].y << 32) | cur[u].x, m, z);
                     mz[u] = m | z << 4;
                 }
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     if ((cur[u].x | cur[u].y) != 0 && mz[u] == 0) {
                         uint32_t m2, z2;
-                        short_set_masks(A, set_base<AL::kShortSets>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
+                        short_set_masks(A, sbase<AL>(second_hash(h[u])), ((uint64_t)cur[u].y << 32) | cur[u].x,
                                         m2, z2);
                         mz[u] = m2 << 8 | z2 << 12 | 1u << 16;  // bit 16: second set read
                     }
@@ -1693,10 +1707,10 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     // both sets read, full, without the key: final for this round (ways are
                     // never freed), so the key is deferred without the claim path
                     if (valid && (mz[u] >> 8) == (1u << 8)) full |= 1u << u;
-                    const uint32_t ci = !valid   ? (uint32_t)AL::kShortSets * 4 + lane
-                                        : m != 0  ? set_base<AL::kShortSets>(h[u]) + __builtin_ctz(m)
-                                        : m2 != 0 ? set_base<AL::kShortSets>(second_hash(h[u])) + __builtin_ctz(m2)
-                                                  : (uint32_t)AL::kShortSets * 4 + lane;
+                    const uint32_t ci = !valid   ? (uint32_t)(AL::kShortSets * AL::kShortWays) + lane
+                                        : m != 0  ? sbase<AL>(h[u]) + __builtin_ctz(m)
+                                        : m2 != 0 ? sbase<AL>(second_hash(h[u])) + __builtin_ctz(m2)
+                                                  : (uint32_t)(AL::kShortSets * AL::kShortWays) + lane;
                     if (valid && (m | m2) == 0 && !((full >> u) & 1u)) slow |= 1u << u;
                     if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
                     else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1811,8 +1825,8 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
         }
     }
     if (t.dbg && tid == 0) t.dbg[2 * blockIdx.x] = __builtin_amdgcn_s_memrealtime();
-    for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4 + kWave; i += kNT) A.sc[i] = 0;
-    for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kNT) A.sk[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)(kAggShortSets * AL::kShortWays) + kWave; i += kNT) A.sc[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)(kAggShortSets * AL::kShortWays); i += kNT) A.sk[i] = 0;
     for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kNT) {
         A.mk[2 * i] = 0;
         A.mk[2 * i + 1] = kUnwritten;
@@ -1858,7 +1872,7 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
     // bucket (tables and misses) through the HBM table.
     const bool merge = emit == 0 || (emit == 1 && t.bflag[b] != 0);
     if (merge) {
-        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kNT) {
+        for (uint32_t i = tid; i < (uint32_t)(kAggShortSets * AL::kShortWays); i += kNT) {
             const uint64_t k0 = A.sk[i];
             if (k0 != 0) short_insert(t, k0, 0, A.sc[i]);
         }
@@ -1922,10 +1936,10 @@ __global__ void __launch_bounds__(AL::kWaves * 64) wc_agg_kernel(Tables t, int e
         __syncthreads();
         // one cursor allocation per workgroup, then each thread writes its keys
         uint32_t mine = 0;
-        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kNT) mine += A.sk[i] != 0;
+        for (uint32_t i = tid; i < (uint32_t)(kAggShortSets * AL::kShortWays); i += kNT) mine += A.sk[i] != 0;
         for (uint32_t i = tid; i < (uint32_t)kAggMidSets * 4; i += kNT) mine += A.mk[2 * i] != 0;
         unsigned long long o = block_alloc<kAggWaves>(&t.ctr->nrec, mine, A.red);
-        for (uint32_t i = tid; i < (uint32_t)kAggShortSets * 4; i += kNT) {
+        for (uint32_t i = tid; i < (uint32_t)(kAggShortSets * AL::kShortWays); i += kNT) {
             const uint64_t k0 = A.sk[i];
             if (k0 != 0) put_short(t, o++, k0, 0, A.sc[i], emit == 1);
         }
