@@ -1406,7 +1406,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         if (v != 0 && v != kSpillBuckets && v != kSpillBucketsHi && v != kSpillBucketsLo)
             return fail(c, MRG_EINVAL, "spill_buckets: 0, 256, 512 or 2048");
         c->spill_buckets_opt = (int)v;
-    } else if (!strcmp(name, "sort_digit_bits")) {  // 64-bit radix passes: 8 or 10 bits per digit (0: by app)
+    } else if (!strcmp(name, "sort_digit_bits")) {  // radix passes: 8 (0) or 10 bits per digit
         reduce_ws_set(c->rws, (int)v, -1, -1);
     } else if (!strcmp(name, "sort_fold_part")) {  // partition folded into the k0 sort key (-1: off)
         reduce_ws_set(c->rws, 0, v >= 0 ? 1 : 0, -1);

@@ -286,8 +286,10 @@ int map_grid_size(int device);
 struct RadixWs;
 RadixWs* radix_ws_new();
 void radix_ws_free(RadixWs*);
-// Stable sort by the low `bits` key bits (8-bit digits, one launch per pass);
-// k_in / v_in are not modified.  Returns 0 or a hipError_t.
+// Stable sort by the low `bits` key bits (8- or 10-bit digits, one launch per
+// pass); k_in / v_in are not modified.  Returns 0 or a hipError_t.
+// digit bits: 10, or 8 (0 = 8).
+void radix_ws_set_digit_bits(RadixWs*, int bits);
 int radix_sort_pairs_u32(RadixWs*, const uint32_t* k_in, uint32_t* k_out, const uint32_t* v_in, uint32_t* v_out,
                          uint64_t n, unsigned bits, hipStream_t s);
 int radix_sort_pairs_u64(RadixWs*, const uint64_t* k_in, uint64_t* k_out, const uint32_t* v_in, uint32_t* v_out,

@@ -47,7 +47,7 @@ struct DBuf {
 struct ReduceWs {
     DBuf perm_a, perm_b, key_a, key_b, lineoff, out, flags, sel, offs, ext, tiek, bins, runs;
     uint64_t* h_pinned = nullptr;  // small pinned staging
-    int digit_bits = 0;            // radix digit of the 64-bit key passes: 8, 10, 0 = by app (grep 10, wc 8)
+    int digit_bits = 0;            // radix digit of the key passes: 10, or 8 (0 = 8; mrgpu_sort.hip)
     bool fold_part = true;         // wc: partition folded into the top bits of the k0 sort key
     bool grep_k1 = true;           // grep: radix passes over the first 16 key bytes (else 8, more ties)
     bool compact_ties = true;      // tied runs merge-sorted on compact key copies (TieKey)
@@ -972,6 +972,7 @@ int sort_u64_keys(ReduceWs* ws, uint64_t* k_in, uint64_t* k_out, uint64_t n, uns
 int sort_in_place(ReduceWs* ws, int key_bytes, void* keys, uint32_t* vals, uint64_t n, unsigned bits, hipStream_t s) {
     if (n == 0) return 0;
     if ((key_bytes != 4 && key_bytes != 8) || (!vals && key_bytes != 8)) return (int)hipErrorInvalidValue;
+    radix_ws_set_digit_bits(ws->rx, ws->digit_bits);
     void* ko = nullptr;
     uint32_t* vo = nullptr;
     RCHK(hipMalloc(&ko, n * key_bytes));
@@ -1411,15 +1412,9 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     // launches, than the larger merge sort they save)
     const bool grep = app != 1;
     const bool k1_first = grep && ws->grep_k1;
-    // 10-bit digits: C3 reduce 1.50 -> 1.44 ms (15 passes instead of 17); C2's
-    // packed 60-bit key: 6 passes instead of 8
-    const int saved_bits = ws->digit_bits;
-    if (saved_bits == 0) ws->digit_bits = 10;
-    struct Restore {
-        ReduceWs* w;
-        int b;
-        ~Restore() { w->digit_bits = b; }
-    } restore{ws, saved_bits};
+    // radix digits (mrgpu_sort.hip): 8 bits; option sort_digit_bits = 10 for
+    // 10-bit ones (fewer, wider passes: measured no faster)
+    radix_ws_set_digit_bits(ws->rx, ws->digit_bits);
     const uint64_t* ext = nullptr;
     if (grep) {
         RCHK(ws->ext.ensure(n * 8 * kExtWords));

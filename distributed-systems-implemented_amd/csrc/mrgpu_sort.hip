@@ -45,15 +45,24 @@ namespace mrg {
 
 namespace {
 
-constexpr int kRadixBits = 8;
-constexpr uint32_t kBins = 1u << kRadixBits;
+// Digit width RB: 8 bits (default), or 10 (option sort_digit_bits = 10: 64-bit
+// keys in 7 passes instead of 8, C2's 60-bit key in 6; 1024 per-wave digit
+// counters, 64 KB of LDS, 1024 look-back threads per tile).  Measured on C2 /
+// C3 (`profiles/ab_r05_radix_digits.txt`): the wider passes cost what the
+// saved passes save (C2 reduce 0.410 vs 0.415 ms) or more (C3 +0.05-0.1 ms).
+constexpr int kRadixBitsMax = 10;
+constexpr uint32_t kBinsMax = 1u << kRadixBitsMax;
+template <int RB>
+constexpr uint32_t bins_of() { return 1u << RB; }
+template <int RB>
+constexpr int max_passes() { return (64 + RB - 1) / RB; }
 constexpr int kSortWaves = MRG_SORT_WAVES;  // waves per pass workgroup
 constexpr int kSortThreads = 64 * kSortWaves;
 constexpr int kHistThreads = 256;
 constexpr int kRowsPerWave = MRG_SORT_ROWS;
 constexpr uint32_t kWaveKeys = 64 * kRowsPerWave;           // 1024
 constexpr uint32_t kTileKeys = kWaveKeys * kSortWaves;      // 4096
-constexpr int kMaxPasses = 8;                               // 64-bit keys
+constexpr int kMaxPasses = 8;                               // 64-bit keys (8-bit digits: the most passes)
 constexpr uint32_t kFlagAgg = 1, kFlagInc = 2;
 constexpr int kLookWin = 16;  // look-back words loaded per round trip
 
@@ -84,11 +93,13 @@ __device__ __forceinline__ uint32_t digit_of(K key, uint32_t shift, uint32_t mas
 
 // hist: npasses * 256 u32, zero on entry (left zero on exit); starts: the
 // passes' exclusive digit starts; ticket: zero on entry (left zero).
-template <class K>
+template <class K, int RB>
 __global__ void __launch_bounds__(kHistThreads) radix_hist_kernel(const K* __restrict__ keys, uint64_t n, uint32_t bits,
                                                                   uint32_t npasses, uint32_t* hist, uint32_t* starts,
                                                                   uint32_t* ticket) {
-    __shared__ uint32_t h[kMaxPasses * kBins];
+    constexpr uint32_t kBins = bins_of<RB>(), kPer = kBins / kHistThreads;  // digits per thread in the scan
+    constexpr int kRadixBits = RB;
+    __shared__ uint32_t h[max_passes<RB>() * kBins];
     __shared__ uint32_t red[kHistThreads / 64];
     __shared__ uint32_t last;
     for (uint32_t i = threadIdx.x; i < npasses * kBins; i += kHistThreads) h[i] = 0;
@@ -113,25 +124,35 @@ __global__ void __launch_bounds__(kHistThreads) radix_hist_kernel(const K* __res
     __threadfence();
     for (uint32_t p = 0; p < npasses; p++) {
         uint32_t* hp = hist + p * kBins;
-        const uint32_t v = __hip_atomic_load(hp + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint32_t v[kPer], sum = 0;  // digits kPer * tid .. + kPer - 1
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++) {
+            v[q] = __hip_atomic_load(hp + kPer * threadIdx.x + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sum += v[q];
+        }
         uint32_t tot;
-        starts[p * kBins + threadIdx.x] = block_excl_scan<kHistThreads / 64>(v, red, &tot);
-        hp[threadIdx.x] = 0u;
+        uint32_t run = block_excl_scan<kHistThreads / 64>(sum, red, &tot);
+#pragma unroll
+        for (uint32_t q = 0; q < kPer; q++) {
+            starts[p * kBins + kPer * threadIdx.x + q] = run;
+            run += v[q];
+            hp[kPer * threadIdx.x + q] = 0u;
+        }
     }
     if (threadIdx.x == 0) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <class K, bool kVals>
+template <class K, bool kVals, int RB>
 struct PassLds {
     K k[kTileKeys];
     uint32_t v[kVals ? kTileKeys : 1];
-    uint32_t wcnt[kSortWaves][kBins];  // per-wave digit counters, then the wave's exclusive offsets
-    uint32_t dst[kBins];               // global position of the tile's digit-d run minus its tile-local start
+    uint32_t wcnt[kSortWaves][bins_of<RB>()];  // per-wave digit counters, then the wave's exclusive offsets
+    uint32_t dst[bins_of<RB>()];               // global position of the tile's digit-d run minus its tile-local start
     uint32_t red[kSortWaves];
     uint32_t tile;
 };
 
-template <class K, bool kVals>
+template <class K, bool kVals, int RB>
 __global__ void __launch_bounds__(kSortThreads) radix_pass_kernel(const K* __restrict__ kin, K* __restrict__ kout,
                                                                   const uint32_t* __restrict__ vin,
                                                                   uint32_t* __restrict__ vout, uint64_t n,
@@ -139,7 +160,10 @@ __global__ void __launch_bounds__(kSortThreads) radix_pass_kernel(const K* __res
                                                                   const uint32_t* __restrict__ starts,
                                                                   unsigned long long* state, uint32_t* tile_ctr,
                                                                   uint32_t epoch, uint32_t ntiles) {
-    __shared__ PassLds<K, kVals> L;
+    constexpr uint32_t kBins = bins_of<RB>();
+    constexpr int kRadixBits = RB;
+    static_assert(kBins <= (uint32_t)kSortThreads, "one digit per thread");
+    __shared__ PassLds<K, kVals, RB> L;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (tid == 0) {
         const uint32_t t = atomicAdd(tile_ctr, 1u);
@@ -200,7 +224,7 @@ __global__ void __launch_bounds__(kSortThreads) radix_pass_kernel(const K* __res
     if (dig) {
     // decoupled look-back for digit tid: publish this tile's count, sum the
     // earlier tiles' counts back to the first inclusive prefix
-    unsigned long long* st = state + (uint64_t)t * kBins + tid;
+    unsigned long long* st = state + (uint64_t)t * kBins + tid;  // (the state array holds kBinsMax words per tile)
     const uint64_t hi_agg = (uint64_t)((epoch << 2) | kFlagAgg) << 32;
     const uint64_t hi_inc = (uint64_t)((epoch << 2) | kFlagInc) << 32;
     uint32_t prefix = 0;
@@ -269,13 +293,16 @@ __global__ void __launch_bounds__(kSortThreads) radix_pass_kernel(const K* __res
 }  // namespace
 
 struct RadixWs {
-    uint32_t* small = nullptr;         // hist [kMaxPasses*256] | starts [kMaxPasses*256] | ticket | tile counter
+    uint32_t* small = nullptr;         // hist [kMaxPasses*kBinsMax] | starts [same] | ticket | tile counter
     unsigned long long* state = nullptr;
     uint64_t state_tiles = 0;
     void* buf = nullptr;               // ping-pong keys + values
     size_t buf_cap = 0;
     uint32_t epoch = 0;
+    int digit_bits = 0;  // 10: 10-bit digits; 0 or 8: 8-bit
 };
+
+void radix_ws_set_digit_bits(RadixWs* w, int bits) { w->digit_bits = bits; }
 
 RadixWs* radix_ws_new() { return new RadixWs(); }
 
@@ -293,36 +320,63 @@ void radix_ws_free(RadixWs* w) {
         if (_e != hipSuccess) return (int)_e; \
     } while (0)
 
+template <class K, bool kVals, int RB>
+static void radix_launch(RadixWs* w, const K* k_in, K* k_out, const uint32_t* v_in, uint32_t* v_out, uint64_t n,
+                         unsigned bits, uint64_t ntiles, hipStream_t s) {
+    constexpr uint32_t kBins = bins_of<RB>();
+    const uint32_t npasses = (bits + RB - 1) / RB;
+    uint32_t* hist = w->small;
+    uint32_t* starts = hist + kMaxPasses * kBinsMax;
+    uint32_t* ticket = starts + kMaxPasses * kBinsMax;
+    uint32_t* tile_ctr = ticket + 16;
+    K* k_tmp = (K*)w->buf;
+    uint32_t* v_tmp = (uint32_t*)((char*)w->buf + ((n * sizeof(K) + 255) & ~(size_t)255));
+    const unsigned hgrid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + 8191) / 8192, 1), 512);
+    radix_hist_kernel<K, RB><<<hgrid, kHistThreads, 0, s>>>(k_in, n, bits, npasses, hist, starts, ticket);
+    const K* src_k = k_in;
+    const uint32_t* src_v = v_in;
+    for (uint32_t p = 0; p < npasses; p++) {  // ping-pong: the last pass writes k_out / v_out
+        const bool to_out = ((npasses - 1 - p) & 1u) == 0;
+        K* dk = to_out ? k_out : k_tmp;
+        uint32_t* dv = to_out ? v_out : v_tmp;
+        const uint32_t shift = p * RB;
+        const uint32_t wbits = std::min<uint32_t>(RB, bits - shift);
+        radix_pass_kernel<K, kVals, RB><<<(unsigned)ntiles, kSortThreads, 0, s>>>(
+            src_k, dk, src_v, dv, n, shift, (1u << wbits) - 1u, starts + p * kBins, w->state, tile_ctr, ++w->epoch,
+            (uint32_t)ntiles);
+        src_k = dk;
+        src_v = dv;
+    }
+}
+
 template <class K, bool kVals>
 static int radix_sort_impl(RadixWs* w, const K* k_in, K* k_out, const uint32_t* v_in, uint32_t* v_out, uint64_t n,
                            unsigned bits, hipStream_t s) {
     if (n == 0) return 0;
     if (n > 0xFFFFFFFFull) return (int)hipErrorInvalidValue;  // 32-bit counts in the look-back words
     if (bits == 0 || bits > 8 * sizeof(K)) bits = 8 * sizeof(K);
-    const uint32_t npasses = (bits + kRadixBits - 1) / kRadixBits;
-    const uint32_t small_words = 2 * kMaxPasses * kBins + 64;
+    const uint64_t ntiles = (n + kTileKeys - 1) / kTileKeys;
+    // 10-bit digits only when asked for (option sort_digit_bits = 10) and they
+    // save a pass
+    const bool wide = w->digit_bits == 10 && (bits + 9) / 10 < (bits + 7) / 8;
+    const uint32_t npasses = wide ? (bits + 9) / 10 : (bits + 7) / 8;
+    const uint32_t small_words = 2 * kMaxPasses * kBinsMax + 64;
     if (!w->small) {
         SCHK(hipMalloc(&w->small, small_words * 4));
         SCHK(hipMemsetAsync(w->small, 0, small_words * 4, s));
     }
-    uint32_t* hist = w->small;
-    uint32_t* starts = hist + kMaxPasses * kBins;
-    uint32_t* ticket = starts + kMaxPasses * kBins;
-    uint32_t* tile_ctr = ticket + 16;
-    const uint64_t ntiles = (n + kTileKeys - 1) / kTileKeys;
     if (ntiles > w->state_tiles || w->epoch >= (1u << 29)) {
         if (ntiles > w->state_tiles) {
             if (w->state) SCHK(hipFree(w->state));
             w->state = nullptr;
             w->state_tiles = 0;
             const uint64_t nt = ntiles + ntiles / 4 + 16;
-            SCHK(hipMalloc(&w->state, nt * kBins * 8));
+            SCHK(hipMalloc(&w->state, nt * kBinsMax * 8));
             w->state_tiles = nt;
         }
-        SCHK(hipMemsetAsync(w->state, 0, w->state_tiles * kBins * 8, s));
+        SCHK(hipMemsetAsync(w->state, 0, w->state_tiles * kBinsMax * 8, s));
         w->epoch = 0;
     }
-    // ping-pong: the last pass writes k_out / v_out
     const size_t need = n * sizeof(K) + (kVals ? n * 4 : 0) + 256;
     if (npasses > 1 && need > w->buf_cap) {
         if (w->buf) SCHK(hipFree(w->buf));
@@ -332,24 +386,8 @@ static int radix_sort_impl(RadixWs* w, const K* k_in, K* k_out, const uint32_t* 
         SCHK(hipMalloc(&w->buf, c));
         w->buf_cap = c;
     }
-    K* k_tmp = (K*)w->buf;
-    uint32_t* v_tmp = (uint32_t*)((char*)w->buf + ((n * sizeof(K) + 255) & ~(size_t)255));
-    const unsigned hgrid = (unsigned)std::min<uint64_t>(std::max<uint64_t>((n + 8191) / 8192, 1), 512);
-    radix_hist_kernel<K><<<hgrid, kHistThreads, 0, s>>>(k_in, n, bits, npasses, hist, starts, ticket);
-    const K* src_k = k_in;
-    const uint32_t* src_v = v_in;
-    for (uint32_t p = 0; p < npasses; p++) {
-        const bool to_out = ((npasses - 1 - p) & 1u) == 0;
-        K* dk = to_out ? k_out : k_tmp;
-        uint32_t* dv = to_out ? v_out : v_tmp;
-        const uint32_t shift = p * kRadixBits;
-        const uint32_t wbits = std::min<uint32_t>(kRadixBits, bits - shift);
-        radix_pass_kernel<K, kVals><<<(unsigned)ntiles, kSortThreads, 0, s>>>(
-            src_k, dk, src_v, dv, n, shift, (1u << wbits) - 1u, starts + p * kBins, w->state, tile_ctr, ++w->epoch,
-            (uint32_t)ntiles);
-        src_k = dk;
-        src_v = dv;
-    }
+    if (wide) radix_launch<K, kVals, 10>(w, k_in, k_out, v_in, v_out, n, bits, ntiles, s);
+    else radix_launch<K, kVals, 8>(w, k_in, k_out, v_in, v_out, n, bits, ntiles, s);
     return (int)hipGetLastError();
 }
 

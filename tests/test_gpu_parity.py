@@ -332,7 +332,8 @@ def test_wc_staged_spill(ctx_dict, case):
                           (10, -1, 0, 0, 1)])
 def test_reduce_sort_variants(ctx, digit_bits, fold, grep_k1, compact, own):
     """The reduce's sort variants give the same bytes: the hand-written radix
-    passes (default) or rocPRIM onesweep (own_sort=0) with 8- or 10-bit digits,
+    passes with 8-bit (default) or 10-bit digits (own_sort=0 is kept as an
+    alias: the same passes since rocPRIM left),
     the partition folded into the first key pass (default) or sorted on its own,
     grep lines radix-sorted on 16 key bytes (default) or 8 (more tied runs), tied
     runs merge-sorted on compact key copies (default) or on the records.
@@ -428,13 +429,16 @@ def test_radix_sort_hook(ctx, own, kind, bits):
     sizes around the 4096-key tile (0, 1, 4095, 4096, 4097), 1e5 keys, and 3e6
     (733 tiles: more than can be resident at once, so the look-back waits on
     tiles started later); uniform keys, keys from 5 values (ties: stability),
-    all keys equal, high bits set past `bits` (ignored by the sort)."""
+    all keys equal, high bits set past `bits` (ignored by the sort); 8-bit
+    radix digits (default) and 10-bit ones (option sort_digit_bits = 10)."""
     rng = np.random.default_rng(bits * 7 + own)
     dt = np.uint32 if kind == "u32" else np.uint64
     width = 32 if kind == "u32" else 64
     mask = (1 << bits) - 1 if bits < width else (1 << width) - 1
     ctx.set_option("own_sort", own)
     try:
+      for digit_bits in (0, 10):
+        ctx.set_option("sort_digit_bits", digit_bits)
         for n in (0, 1, 4095, 4096, 4097, 100_000, 3_000_000):
             for dist in ("uniform", "few", "equal"):
                 if n >= 3_000_000 and dist != "uniform":
@@ -458,6 +462,7 @@ def test_radix_sort_hook(ctx, own, kind, bits):
                     assert np.array_equal(ko, keys[order]), (n, dist)
     finally:
         ctx.set_option("own_sort", 1)
+        ctx.set_option("sort_digit_bits", 0)
 
 
 @pytest.mark.parametrize("bins,prefix32", [(1, 1), (0, 1), (0, 0)])
