@@ -225,6 +225,7 @@ struct mrg_ctx {
     bool out_direct_grep = true;        // ... for grep too (out_direct = 1: wc only)
     bool grep_sort_hits = false;        // grep: hits sorted by position before line resolution (option grep_sort_hits)
     bool grep_emit = true;              // grep: records written by the table insert (option grep_emit; 0: collect pass)
+    uint64_t grep_hint_lines = 0, grep_hint_bytes = 0;  // grep: the previous split's resolved lines and their bytes
     bool grep_literal = false;          // grep: regexp metacharacters taken literally (QuoteMeta) instead of refused
     DevBuf lrec, lrec_cnt;              // wc: 32-byte long-word records [map wave][lrec_cap], their counts
     DevBuf lrec_aux;                    // wc: their bucket offsets and bucket-ordered indices (launch_wc_lrec)
@@ -1227,50 +1228,87 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
         launch_grep_resolve(in, len, (uint32_t)plen, t, nhits, dev, sorted, c->s);
         if (dev) launch_grep_resolve_long(in, len, (uint32_t)plen, t, 0, nhits, true, false, c->s);
         HCHK(c, hipGetLastError());
-        if ((rc = read_counters(c))) return rc;
-        if (dev && grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
-        if (sorted && c->h_ctr->ndefer) {
-            launch_grep_resolve_long(in, len, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, false, true, c->s);
-            HCHK(c, hipGetLastError());
+        // emit (default): the insert writes each distinct line's record as it
+        // claims the line's slot, into parts sized for every occurrence (records
+        // <= lines, arena <= the lines' bytes); option grep_emit = 0: insert,
+        // then collect the table (round 4).
+        const bool emit = c->grep_emit;
+        // Speculative sizes (unsorted hits, emit, a previous split mapped on this
+        // context): the parts (records for the list's capacity, arena for the
+        // previous split's line bytes + 25 %) and the LongTable (for its lines +
+        // 25 %) are set up with no host read after the resolution, whose line
+        // count the insert reads on the device; the one read after the insert
+        // checks every bound, and an overflow repeats with the exact sizes.
+        bool spec = dev && emit && c->grep_hint_lines > 0;
+        uint64_t cap_lines, cap_bytes, want_lines;
+        if (spec) {
+            cap_lines = nhits;  // (the list's capacity: lines <= hits)
+            cap_bytes = c->grep_hint_bytes + c->grep_hint_bytes / 4 + (1u << 20);
+            want_lines = c->grep_hint_lines + c->grep_hint_lines / 4;
+        } else {
             if ((rc = read_counters(c))) return rc;
+            if (dev && grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
+            if (sorted && c->h_ctr->ndefer) {
+                launch_grep_resolve_long(in, len, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, false, true, c->s);
+                HCHK(c, hipGetLastError());
+                if ((rc = read_counters(c))) return rc;
+            }
+            if (c->h_ctr->status & kStListFull) return fail(c, MRG_EDEVICE, "grep: line list overflow");
+            cap_lines = want_lines = c->h_ctr->nlines;
+            cap_bytes = c->h_ctr->line_bytes;
         }
-        if (c->h_ctr->status & kStListFull) return fail(c, MRG_EDEVICE, "grep: line list overflow");
-        const uint64_t nlines = c->h_ctr->nlines;
         HCHK(c, hipEventRecord(c->ev[8], c->s));
         // The LongTable holds at most nlines distinct lines: size it for them
         // (capped; a table that still fills up grows, and only the inserts re-run).
         int need = 14;
-        while (need < 24 && (1ull << need) * 7 < nlines * 10) need++;
+        while (need < 24 && (1ull << need) * 7 < want_lines * 10) need++;
         c->lo_log2_cur = need;
-        // emit (default): the insert writes each distinct line's record as it
-        // claims the line's slot, into parts sized for every occurrence (records
-        // <= nlines, arena <= the lines' bytes); option grep_emit = 0: insert,
-        // then collect the table (round 4).
-        const bool emit = c->grep_emit;
         mrg_parts* p = nullptr;
-        if (emit && (rc = parts_alloc(c, nlines, c->h_ctr->line_bytes, MRG_APP_GREP, nreduce, &p))) return rc;
-        bool ok = false;
+        if (emit && (rc = parts_alloc(c, cap_lines, cap_bytes, MRG_APP_GREP, nreduce, &p))) return rc;
+        bool ok = false, again = false;
         for (int grow = 0; grow < 8 && !ok; grow++) {
             if ((rc = ensure_tables(c))) { if (p) mrg_parts_free(p); return rc; }
             t = make_tables(c);
             if (emit) {
                 t.out = p->r;
-                t.out_cap = nlines;
+                t.out_cap = cap_lines;
                 t.nreduce = nreduce;
             }
             clear_long_table(t, c->s);
-            launch_grep_insert(in, t, nlines, emit, c->s);
+            launch_grep_insert(in, t, cap_lines, spec, emit, c->s);
             HCHK(c, hipGetLastError());
             if ((rc = read_counters(c))) { if (p) mrg_parts_free(p); return rc; }
             const uint32_t st = c->h_ctr->status;
-            if (st & (kStSpin | kStRecFull)) {
+            if (spec && (st & kStListFull)) {  // the map's hit list overflowed: the whole attempt again
+                if (p) mrg_parts_free(p);
+                grow_on_overflow(c, kStListFull);
+                again = true;
+                break;
+            }
+            if (st & kStSpin) {
                 if (p) mrg_parts_free(p);
                 return fail(c, MRG_EDEVICE, "grep: line table insert failed (status %#x)", st);
+            }
+            if (st & kStRecFull) {
+                if (!spec || c->h_ctr->line_bytes <= cap_bytes) {
+                    if (p) mrg_parts_free(p);
+                    return fail(c, MRG_EDEVICE, "grep: line records overflow (status %#x)", st);
+                }
+                // the speculative arena was short: parts for the exact line bytes, insert again
+                mrg_parts_free(p);
+                p = nullptr;
+                cap_bytes = c->h_ctr->line_bytes;
+                if ((rc = parts_alloc(c, cap_lines, cap_bytes, MRG_APP_GREP, nreduce, &p))) return rc;
+                continue;
             }
             if (st & kStLongFull) c->lo_log2_cur += 2;
             else ok = true;
         }
+        if (again) continue;
         if (!ok) { if (p) mrg_parts_free(p); return fail(c, MRG_ENOMEM, "grep: line table kept overflowing"); }
+        const uint64_t nlines = c->h_ctr->nlines;
+        c->grep_hint_lines = nlines;
+        c->grep_hint_bytes = c->h_ctr->line_bytes;
         HCHK(c, hipEventRecord(c->ev[2], c->s));
         c->stats.map_kernel_ms = ev_ms(c->ev[0], c->ev[1]);
         if (emit) {

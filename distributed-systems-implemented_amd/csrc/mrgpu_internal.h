@@ -261,8 +261,9 @@ void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, cons
 // t.lines -> the LongTable (one distinct line = one slot).
 // emit: each line that claims its slot also writes its record (t.out: key
 // prefix, length, partition, its bytes copied to the arena at ctr->arena) —
-// no collect pass over the table afterwards.
-void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, bool emit, hipStream_t s);
+// no collect pass over the table afterwards.  dev_count: nlines is a bound and
+// the kernel reads the resolved line count on the device.
+void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, bool dev_count, bool emit, hipStream_t s);
 // Clear the LongTable and its fill counters, and the record / arena cursors (a
 // re-run of launch_grep_insert after growth).
 void clear_long_table(const Tables& t, hipStream_t s);

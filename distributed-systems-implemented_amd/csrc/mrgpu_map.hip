@@ -1026,10 +1026,8 @@ __device__ __forceinline__ void line_prefix16(const uint8_t* in, int64_t s, uint
 // (C3: 0.26 ms + two host round trips) is not needed.  The record's count
 // (the line's occurrences: mr-X-r holds one KV per occurrence, worker.go:80-92)
 // is the slot's, read by grep_counts_kernel once every insert is in.
-__global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __restrict__ in, Tables t, uint64_t nlines,
-                                                              bool emit) {
-    __shared__ unsigned long long scratch[2 * kLineWaves + 2];
-    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void grep_insert_line(const uint8_t* __restrict__ in, const Tables& t, uint64_t i,
+                                                 uint64_t nlines, bool emit, unsigned long long* scratch) {
     bool claimed = false;
     uint64_t len = 0, k0 = 0, k1 = 0;
     uint32_t h32 = 0;
@@ -1092,7 +1090,7 @@ __global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __r
         scratch[2 * kLineWaves + 1] = ab;
     }
     __syncthreads();
-    if (!emit) return;
+    if (!emit) return;  // (workgroup-uniform)
     const uint64_t o = scratch[2 * kLineWaves] + scratch[wv] + ik - (claimed ? 1u : 0u);
     const uint64_t off = scratch[2 * kLineWaves + 1] + scratch[kLineWaves + wv] + ib - (claimed ? len : 0);
     bool ok = false;
@@ -1140,6 +1138,18 @@ __global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __r
             for (int k = 0; k < kCopyLines; k++)
                 if (x < l[k]) t.out.arena[dst[k] + x] = b[k];
         }
+    }
+}
+
+// nlines, or with dn the line count read here (the resolution's cursor, no
+// host round trip): the workgroups stride over it in whole-workgroup steps.
+__global__ void __launch_bounds__(kLineWG) grep_insert_kernel(const uint8_t* __restrict__ in, Tables t, uint64_t nlines,
+                                                              const unsigned long long* dn, bool emit) {
+    __shared__ unsigned long long scratch[2 * kLineWaves + 2];
+    const uint64_t n = dn ? (*dn < nlines ? *dn : nlines) : nlines;
+    for (uint64_t base = (uint64_t)blockIdx.x * kLineWG; base < n; base += (uint64_t)gridDim.x * kLineWG) {
+        grep_insert_line(in, t, base + threadIdx.x, n, emit, scratch);
+        __syncthreads();  // scratch reused by the next step
     }
 }
 
@@ -1359,7 +1369,10 @@ __global__ void clear_long_kernel(Tables t) {
     const uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t i = i0; i <= t.lo_mask; i += stride) t.lo[i] = LongSlot{0, nullptr, 0, 0};
     if (i0 == 0) {
-        t.ctr->status = 0;
+        // the insert's own status bits only: a hit-list overflow flagged by the
+        // map kernel must survive to the counter read after the insert (grep's
+        // speculative sizes read nothing in between)
+        t.ctr->status &= ~(uint32_t)(kStLongFull | kStRecFull | kStSpin);
         t.ctr->long_used = 0;
         t.ctr->long_bytes = 0;
         t.ctr->nrec = 0;
@@ -1423,9 +1436,11 @@ __global__ void grep_counts_kernel(Tables t) {
         t.out.cnt[o] = t.lo[t.out.cnt[o] & t.lo_mask].count;
 }
 
-void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, bool emit, hipStream_t s) {
+void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, bool dev_count, bool emit, hipStream_t s) {
     if (nlines == 0) return;
-    grep_insert_kernel<<<(unsigned)((nlines + kLineWG - 1) / kLineWG), kLineWG, 0, s>>>(in, t, nlines, emit);
+    uint64_t g = (nlines + kLineWG - 1) / kLineWG;
+    if (dev_count && g > 1024) g = 1024;  // (nlines = the capacity: the workgroups stride)
+    grep_insert_kernel<<<(unsigned)g, kLineWG, 0, s>>>(in, t, nlines, dev_count ? &t.ctr->nlines : nullptr, emit);
     if (emit) {
         const uint64_t g = (nlines + 255) / 256;
         grep_counts_kernel<<<(unsigned)(g < 2048 ? g : 2048), 256, 0, s>>>(t);

@@ -174,12 +174,22 @@ def test_grep_synthetic(ctx, sort_hits, emit):
 def test_grep_list_overflow_rerun(ctx):
     """A hit list far smaller than the split's hits (option list_cap): the line
     resolution, which reads the hit count on the device, runs over a truncated
-    list; the counter read after it sees the overflow, and the map repeats with
-    a larger list — exact output either way."""
+    list; the counter read after it (or, once an earlier split has set the
+    speculative sizes, the one after the insert) sees the overflow, and the map
+    repeats with a larger list.  Then a split with far more line bytes than the
+    previous one (the speculative record arena overflows and the insert runs
+    again with the exact size) — exact output every time."""
     files = cases.synthetic_grep(50000, [2_000_000], 8, match_rate=0.05)
+    small = cases.synthetic_grep(5000, [20_000], 9, match_rate=0.02)
+    big = cases.synthetic_grep(50000, [6_000_000], 10, match_rate=0.6)
     ctx.set_option("list_cap", 500)
     try:
         check(ctx, "grep:distributed", files, nreduces=(10,))
+        assert gpu_partitioned(ctx, "grep:distributed", small, 10) == O.c_partitioned("grep:distributed", small, 10)
+        ctx.set_option("list_cap", 500)  # (the sizes of `small` are now the speculative ones)
+        assert gpu_partitioned(ctx, "grep:distributed", files, 10) == O.c_partitioned("grep:distributed", files, 10)
+        assert gpu_partitioned(ctx, "grep:distributed", small, 10) == O.c_partitioned("grep:distributed", small, 10)
+        assert gpu_partitioned(ctx, "grep:distributed", big, 10) == O.c_partitioned("grep:distributed", big, 10)
     finally:
         ctx.set_option("list_cap", 0)
 
