@@ -227,24 +227,31 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *   exchange_timeout_ms                  deadline of a collective phase (mrg_exchange;
  *                                        mrg_comm_init gets 4x; default 120000): past it the
  *                                        process prints the phase and exits with status 124
- *   sort_digit_bits (8, 10), sort_fold_part (-1: off), grep_sort_k1 (-1: 8-byte
- *                                        prefix passes only), sort_compact_ties (-1:
- *                                        off), sort_bins (1: sample sort), sort_prefix32
- *                                        (0: the wc key pass over all 60/64 bits instead
- *                                        of the top 32), own_sort (0: rocPRIM onesweep
- *                                        radix passes instead of the hand-written LSD
- *                                        sort), tie_rank (0: grep's tied runs merge-sorted
- *                                        together instead of ranked per run)   reduce sort
- *                                        variants
+ *   sort_digit_bits (10: 10-bit radix digits; default 8), sort_fold_part (-1: off),
+ *                                        grep_sort_k1 (-1: 8-byte prefix passes only),
+ *                                        sort_compact_ties (-1: off), sort_bins (1: sample
+ *                                        sort), sort_prefix32 (0: the wc key pass over all
+ *                                        60/64 bits instead of the top 32), own_sort (kept
+ *                                        for compatibility: every value runs the hand-written
+ *                                        LSD passes), tie_rank (0: grep's tied runs
+ *                                        merge-sorted together instead of ranked per run)
+ *                                        reduce sort variants
  *   grep_literal (1: on)                 grep patterns with regexp metacharacters matched as
  *                                        literals (QuoteMeta) instead of refused with MRG_EINVAL
  *   async_direct_max (bytes; -1: none)   mrg_run_job_async: wc outputs up to this bound (default
  *                                        64 MB) are written straight into the pinned buffer,
  *                                        larger ones copied on the output stream
  *   map_lean (-1: off)                   wc: the all-ASCII map variant after an all-ASCII split
- *   out_direct (-1: off)                 mrg_run_job (wc) writes the output lines straight into
- *                                        its pinned host buffer (default) instead of a
- *                                        device buffer + copy */
+ *   out_direct (-1: off, 1: wc only)     mrg_run_job writes the output lines straight into its
+ *                                        pinned host buffer (default: wc and grep) instead of
+ *                                        a device buffer + copy
+ *   grep_sort_hits (1: on)               grep: the hits sorted by position before the line
+ *                                        resolution (default: the map kernel's order, counts
+ *                                        read on the device, sizes speculated from the
+ *                                        previous split and checked once after the insert)
+ *   grep_emit (0: off)                   grep: each distinct line's record written by the
+ *                                        LongTable insert that claims it (default) instead
+ *                                        of a collect pass over the table */
 int mrg_set_option(mrg_ctx* ctx, const char* name, int64_t value);
 
 uint32_t mrg_ihash(const uint8_t* key, size_t n);
