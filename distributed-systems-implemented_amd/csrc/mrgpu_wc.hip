@@ -714,19 +714,19 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                 const __amdgpu_buffer_rsrc_t rsr = __builtin_amdgcn_make_buffer_rsrc(
                                     (void*)(tr.lrec + (uint64_t)(blockIdx.x * kWavesPerWG + wv) * rcap * 2u), (short)0, (int)(rcap * 32u), 0x00020000);
                                 const uint32_t ro = __builtin_amdgcn_inverse_ballot_w64(mR) && idx < rcap ? idx * 32u : kOutOfRange;
-                                // the key's 32 bytes from the slot, zero past its length, 16 at a time
+                                // the key's 32 bytes from the slot, zero past its length, 16 at a
+                                // time; the byte masks from the length table (kmask4[len]: the first
+                                // min(len, 16) bytes), not per-dword clamps (~50 VALU fewer per turn)
+                                const u32x4 mk[2] = {kmask4[wl < 31u ? wl : 31u], kmask4[wl > 16u ? wl - 16u : 0u]};
         #pragma unroll
                                 for (int hf = 0; hf < 2; hf++) {
                                     const lds_u32* q4 = (const lds_u32*)(uintptr_t)(bufa + (p & ~3u) + 16u * hf);
                                     uint32_t d[5], k[4];
         #pragma unroll
                                     for (int i = 0; i < 5; i++) d[i] = q4[i];
+                                    const uint32_t mw[4] = {mk[hf].x, mk[hf].y, mk[hf].z, mk[hf].w};
         #pragma unroll
-                                    for (int i = 0; i < 4; i++) {
-                                        const int nb = min(max((int)wl - 4 * (4 * hf + i), 0), 4);
-                                        k[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], p) &
-                                               (nb >= 4 ? 0xFFFFFFFFu : (1u << (8 * nb)) - 1u);
-                                    }
+                                    for (int i = 0; i < 4; i++) k[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], p) & mw[i];
                                     __builtin_amdgcn_raw_buffer_store_b128((u32x4){k[0], k[1], k[2], k[3]}, rsr,
                                                                            ro == kOutOfRange ? kOutOfRange : ro + 16u * hf, 0, 0);
                                 }
