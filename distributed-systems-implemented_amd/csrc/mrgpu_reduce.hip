@@ -210,25 +210,30 @@ __global__ void ext_words_kernel(Recs r, uint64_t* ext) {
         const uint32_t len = r.len[j];
         uint64_t wd[kExtWords] = {};
         if (len > 16) {
-            // key bytes [16, min(len, 64)) by aligned 16-byte blocks of the arena
-            // (one load per block; an aligned block never crosses a page)
+            // key bytes [16, min(len, 64)) by the (at most four) aligned 16-byte
+            // blocks of the arena holding them, all loads issued before any is used
+            // (one memory round trip per record, not one per block; an aligned
+            // block never crosses a page, and only blocks holding key bytes are read)
             const uint8_t* p = r.arena + r.koff[j];
             const int64_t end = len < 16 + 8 * kExtWords ? (int64_t)len : 16 + 8 * kExtWords;
-            for (int64_t q = 16; q < end;) {
-                const uintptr_t a = (uintptr_t)(p + q), ab = a & ~(uintptr_t)15;
-                const int64_t bi = q - (int64_t)(a - ab);
-                const uint4 v = *(const uint4*)ab;
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+            const uintptr_t a = (uintptr_t)(p + 16), ab = a & ~(uintptr_t)15;
+            const int64_t bi0 = 16 - (int64_t)(a - ab);  // key index of block 0's first byte
+            uint4 v[4];
+#pragma unroll
+            for (int blk = 0; blk < 4; blk++)
+                v[blk] = bi0 + 16 * blk < end ? *(const uint4*)(ab + 16 * blk) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+            for (int blk = 0; blk < 4; blk++) {
+                const uint32_t w4[4] = {v[blk].x, v[blk].y, v[blk].z, v[blk].w};
 #pragma unroll
                 for (int b = 0; b < 16; b++) {
-                    const int64_t k = bi + b;
-                    if (k < q || k >= end) continue;
+                    const int64_t k = bi0 + 16 * blk + b;
+                    if (k < 16 || k >= end) continue;
                     const uint64_t byte = (w4[b >> 2] >> (8 * (b & 3))) & 0xFFu;
 #pragma unroll
                     for (int w = 0; w < kExtWords; w++)  // register-indexed: select, no scratch
                         if ((k - 16) >> 3 == w) wd[w] |= byte << (56 - 8 * ((k - 16) & 7));
                 }
-                q = bi + 16;
             }
         }
 #pragma unroll
