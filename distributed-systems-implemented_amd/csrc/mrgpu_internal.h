@@ -217,7 +217,7 @@ void launch_wc_lrec(const Tables& t, uint32_t nwg, hipStream_t s);
 // bytes of the bucket offsets ahead of the record indices in the lrec aux buffer
 constexpr uint64_t kLrecAuxOff = (256ull * kMaxMapWGs + 64) * 4;
 // the per-range partials of the long-word records (after the indices)
-constexpr uint64_t kLrecPartBytes = 512ull * 4096 * sizeof(LrecPart) + 512 * 4 + 256;
+constexpr uint64_t kLrecPartBytes = 512ull * 4096 * sizeof(LrecPart) + 1024 * 4 + 256;  // partials, then <= 1024 range counts
 // ---- wc pipeline (mrgpu_wc.hip) ----
 uint32_t wc_map_grid(uint64_t n, int grid);
 // Chunks [cbeg, cend) of the split (kOwn = 992 input bytes each; default: all);

@@ -165,7 +165,7 @@ __global__ void __launch_bounds__(kLongWG) wc_long_kernel(const uint8_t* __restr
 //      ranges the bucket spans and inserts each distinct key once.
 constexpr uint32_t kLrecBuckets = 256;
 #ifndef MRG_LREC_SLOTS
-#define MRG_LREC_SLOTS 2048
+#define MRG_LREC_SLOTS 1024
 #endif
 constexpr int kLrecSlots = MRG_LREC_SLOTS;
 struct alignas(16) LrecLds {
@@ -371,14 +371,16 @@ struct LrecKey {
 // merges each bucket's partials (from the ranges its records span) and inserts
 // every distinct key into the LongTable ONCE (inserting them from every range
 // put ~1000 concurrent inserts of a hot word on one LongTable slot: 1.4 ms).
+// (1024 ranges of a 1024-slot table: C2u wc_lrec 0.786 -> 0.751 ms, merge
+// unchanged, against 512 x 2048; profiles/ab_r05_lrec_grid.txt)
 #ifndef MRG_LREC_GRID
-#define MRG_LREC_GRID 512
+#define MRG_LREC_GRID 1024
 #endif
 #ifndef MRG_LREC_BATCH
 #define MRG_LREC_BATCH 2
 #endif
 constexpr uint32_t kLrecGrid = MRG_LREC_GRID, kLrecBatch = MRG_LREC_BATCH;
-static_assert(kLrecGrid <= 512 && kLrecSlots <= 4096, "the partials buffer (kLrecPartBytes) holds 512 x 4096");
+static_assert(kLrecGrid <= 1024 && (uint64_t)kLrecGrid * kLrecSlots <= 512ull * 4096, "the partials buffer (kLrecPartBytes)");
 static_assert(sizeof(LrecLds) <= 160 * 1024, "LDS");
 __global__ void __launch_bounds__(kLongWG) wc_lrec_kernel(Tables t, uint32_t nwg) {
     __shared__ LrecLds A;

@@ -1,7 +1,7 @@
 # Round-5 final set, part A: GPU suite, smoke, bench lines C2 (default: CPU
 # baseline, PCIe-inclusive, oracle), C3, C2u.  Each step under its own limit.
 set -e
-out=gpurun_out/final5
+out=gpurun_out/final5d
 mkdir -p $out
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $out/gpu_tests.log 2>&1
 tail -2 $out/gpu_tests.log
