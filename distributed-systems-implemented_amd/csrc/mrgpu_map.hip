@@ -539,14 +539,29 @@ __device__ __forceinline__ uint32_t eq_mask16(uint4 v, uint32_t rep) {
 // wait for a chunk is a counted vmcnt(1) — a compiler-visible load or a global
 // pattern read in the loop would make hipcc wait vmcnt(0) and serialize the
 // prefetch (measured: 7.0 ms per 10 GB that way).  The pattern sits in LDS.
-// Candidates: positions whose byte and next byte equal the pattern's first two
-// (exact SWAR compares), verified in LDS for patterns of <= 65 bytes (longer
+// Candidates: positions whose next four bytes equal the pattern's first four
+// (patterns of 1-3 bytes: the first two, per-byte SWAR compares), verified in
+// LDS for patterns of <= 65 bytes (longer
 // ones read HBM and drain with vmcnt(0)).  Matches are buffered per wave in LDS
 // and flushed to the list with ONE cursor atomic per flush: a same-address
 // device atomic per match serializes at the memory side (~12 ns each; C3's
 // ~600 K matches cost 7 ms that way, the whole kernel time).
 constexpr uint32_t kGrepOwn = 960;  // own bytes per chunk (lanes 0-59)
-constexpr uint32_t kGrepBuf = 256;  // buffered matches per wave
+// LDS ring slots per wave: kGrepSlots - 1 chunk DMAs in flight while one chunk
+// is scanned.  3 slots and a 128-entry match buffer keep two workgroups per CU
+// (64 KiB of LDS each); C3 map 2.09 -> 2.05 ms against 2 slots and 256 entries,
+// 3 slots with 256 entries (one workgroup per CU) 2.31 ms
+// (profiles/ab_r05_grep_ring.txt)
+#ifndef MRG_GREP_SLOTS
+#define MRG_GREP_SLOTS 3
+#endif
+constexpr uint32_t kGrepSlots = MRG_GREP_SLOTS;
+#ifndef MRG_GREP_BUF
+#define MRG_GREP_BUF 128
+#endif
+constexpr uint32_t kGrepBuf = MRG_GREP_BUF;  // buffered matches per wave
+// flushed once fewer than this many entries are free (a chunk rarely adds more)
+constexpr uint32_t kGrepFlushRoom = kGrepBuf / 2 < 64 ? kGrepBuf / 2 : 64;
 typedef int gi32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ void grep_dma(const uint8_t* in, uint64_t n, uint64_t cs, uint32_t lane, uint32_t lds_base) {
@@ -598,7 +613,7 @@ __device__ __attribute__((noinline)) uint32_t first_hit_per_line(uint32_t hit, u
 __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __restrict__ in, uint64_t n, uint64_t cbeg,
                                                             uint64_t nchunks, const uint8_t* __restrict__ pat,
                                                             uint32_t plen, Tables t) {
-    __shared__ uint4 ring[kWavesPerWG][2][kChunk / 16];
+    __shared__ uint4 ring[kWavesPerWG][kGrepSlots][kChunk / 16];
     __shared__ uint8_t P[kAhead + 16];
     __shared__ unsigned long long mbuf[kWavesPerWG][kGrepBuf];  // buffered match positions
     __shared__ uint32_t mcnt[kWavesPerWG];
@@ -624,18 +639,21 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
         wave_sync();
     };
     const bool in_lds = plen <= (uint32_t)kAhead + 1;
-    const uint32_t p0 = P[0], p1 = plen > 1 ? P[1] : 0u;
-    const uint32_t rep0 = p0 * 0x01010101u, rep1 = p1 * 0x01010101u;
+    const uint32_t p0 = P[0], p1 = plen > 1 ? P[1] : 0u, p2 = plen > 2 ? P[2] : 0u, p3 = plen > 3 ? P[3] : 0u;
+    const uint32_t rep0 = p0 * 0x01010101u, rep1 = p1 * 0x01010101u, rep2 = p2 * 0x01010101u, rep3 = p3 * 0x01010101u;
     const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
     const uint64_t c0 = cbeg + (uint64_t)blockIdx.x * kWavesPerWG + wv;
     const uint32_t slot0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ring[wv][0];
     const uint64_t cstep = stride * kGrepOwn;
-    grep_dma(in, n, c0 * kGrepOwn, lane, slot0);
+#pragma unroll
+    for (uint32_t q = 0; q + 1 < kGrepSlots; q++) grep_dma(in, n, (c0 + q * stride) * kGrepOwn, lane, slot0 + q * kChunk);
     uint32_t k = 0;
     uint64_t cs = c0 * kGrepOwn;
-    for (uint64_t c = c0; c < nchunks; c += stride, cs += cstep, k ^= 1u) {
-        grep_dma(in, n, cs + cstep, lane, slot0 + (k ^ 1u) * kChunk);  // next chunk into the other slot
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");              // this chunk's DMA has landed
+    for (uint64_t c = c0; c < nchunks; c += stride, cs += cstep, k = k == kGrepSlots - 1 ? 0u : k + 1u) {
+        // the chunk kGrepSlots - 1 strides ahead into the slot the previous one left
+        const uint32_t kn = k == 0 ? kGrepSlots - 1 : k - 1u;
+        grep_dma(in, n, cs + (kGrepSlots - 1) * cstep, lane, slot0 + kn * kChunk);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGrepSlots - 1) : "memory");  // this chunk's DMA has landed
         const uint64_t n4 = n & ~3ull;
         if ((n & 3) && n4 >= cs && n4 < cs + kChunk) {
             // the split's last n % 4 bytes sit in a dword the range check zero-filled
@@ -646,11 +664,41 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
         const lds_uint4* b4 = (const lds_uint4*)ring[wv][k];
         const lds_u8* bb = (const lds_u8*)b4;
         const uint4 v = from_v4(b4[lane]);
-        uint32_t m = lane < kGrepOwn / 16 ? eq_mask16(v, rep0) : 0u;
-        if (plen > 1) {
-            const uint32_t m1 = eq_mask16(v, rep1);
-            const uint32_t nb = (uint32_t)__shfl_down((int)(m1 & 1u), 1);  // next lane's byte 0 (lane 59 -> 60: look-ahead)
-            m &= (m1 >> 1) | (nb << 15);
+        uint32_t m, q0;  // candidate starts of this lane's bytes; pattern bytes they already match
+        if (plen >= 4) {
+            // 4-byte prefix filter, one zero-byte test per dword: y = OR over k < 4
+            // of (the stream shifted by k) ^ (pattern byte k) is zero in byte i
+            // exactly when bytes i..i+3 equal the pattern's first four (~10 VALU a
+            // dword; the per-byte masks of a two-byte filter cost ~70 a lane and
+            // left a candidate loop running in most chunks).  The exact mask only
+            // for lanes with a candidate.
+            const uint32_t nx = (uint32_t)__shfl_down((int)v.x, 1);  // the next lane's first dword
+            const uint32_t w[5] = {v.x, v.y, v.z, v.w, nx};
+            uint32_t y[4];
+#pragma unroll
+            for (int j = 0; j < 4; j++) {
+                const uint32_t s1 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], 1);
+                const uint32_t s2 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], 2);
+                const uint32_t s3 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], 3);
+                // (a ^ b) | c as v_bitop3_b32 (truth table 0xBE)
+                const uint32_t u = __builtin_amdgcn_bitop3_b32(w[j], rep0, s1 ^ rep1, 0xBE);
+                y[j] = u | __builtin_amdgcn_bitop3_b32(s2, rep2, s3 ^ rep3, 0xBE);
+            }
+            // any zero byte (the borrow's false positives sit above a true zero only)
+            uint32_t zany = 0;
+#pragma unroll
+            for (int j = 0; j < 4; j++) zany |= (y[j] - 0x01010101u) & ~y[j];
+            m = 0;
+            if ((zany & 0x80808080u) != 0 && lane < kGrepOwn / 16) m = eq_mask16((uint4){y[0], y[1], y[2], y[3]}, 0u);
+            q0 = 4;
+        } else {
+            m = lane < kGrepOwn / 16 ? eq_mask16(v, rep0) : 0u;
+            if (plen > 1) {
+                const uint32_t m1 = eq_mask16(v, rep1);
+                const uint32_t nb = (uint32_t)__shfl_down((int)(m1 & 1u), 1);  // next lane's byte 0 (lane 59 -> 60: look-ahead)
+                m &= (m1 >> 1) | (nb << 15);
+            }
+            q0 = 2;
         }
         bool any = false;  // a rare path issued other VMEM instructions: drain before the next DMA wait
         uint32_t vm = 0;   // verified occurrences starting in this lane's bytes
@@ -662,10 +710,10 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
             if (pos + plen > n) continue;
             bool ok = true;
             if (in_lds) {
-                for (uint32_t q = 2; q < plen; q++)
+                for (uint32_t q = q0; q < plen; q++)
                     if (bb[at + q] != P[q]) { ok = false; break; }
             } else {
-                for (uint32_t q = 2; q < plen; q++)
+                for (uint32_t q = q0; q < plen; q++)
                     if (in[pos + q] != pat[q]) { ok = false; break; }
                 any = true;
             }
@@ -693,7 +741,7 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
         if (__ballot(any)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rare paths: drain
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's LDS reads are done before it is refilled
-        if (*wcnt >= (uint32_t)kGrepBuf - 64) flush();
+        if (*wcnt >= kGrepBuf - kGrepFlushRoom) flush();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last prefetch lands before the workgroup exits
     flush();

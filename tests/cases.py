@@ -150,6 +150,16 @@ def grep_edge_cases() -> dict[str, tuple[list[bytes], bytes]]:
         "long_lines_many_hits": ([_long_line(21000, 1) + b"\nshort e line\n" + _long_line(21000, 1) + b"\n"
                                   + _long_line(9000, 2) + b"\neee\ne\n" + _long_line(5000, 3)], b"e"),
         "overlapping": ([b"aaaaaa\nxaax\naaa\naa\na\n"], b"aa"),
+        # the grep map's 4-byte prefix filter: a 4-byte pattern at every offset
+        # mod 16 (across dwords, lanes and chunk seams) with 3-byte decoys,
+        # overlapping occurrences, lines shorter than the pattern, the pattern
+        # at the split's end; a 5-byte UTF-8 pattern with its first 4 bytes as
+        # decoys
+        "prefix4_offsets": ([b"".join(b"x" * k + b"dis dist\n" for k in range(40)) + _seams(b"dist", 30) + b"aaaa",
+                             b"aaaaaaa\naaa\nxaaaax\naaaa"], b"dist"),
+        "prefix4_overlap": ([b"aaaaaaa\naaa\nxaaaax\n" * 70 + b"aaaa"], b"aaaa"),
+        "prefix5_utf8": (["".join("y" * k + "aκ aκc\n" for k in range(33)).encode() + _seams("aκc".encode(), 12)],
+                         "aκc".encode()),
         # > 64 distinct matching lines sharing a 70-byte prefix that differ later,
         # strict prefixes of one another, NUL bytes past byte 64 (the reduce's
         # arena-compare fallback past the 64 bytes its sort words cover)
