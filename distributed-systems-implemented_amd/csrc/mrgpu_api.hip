@@ -585,6 +585,31 @@ static int ensure_recbuf(mrg_ctx* c) {
     return MRG_OK;
 }
 
+// Diagnostics: grep_insert_kernel's per-workgroup phase stamps (ins_stamp), as
+// percentiles of each phase's end relative to the earliest start, in us.  (The
+// stamps of a workgroup's last grid-stride step.)
+static void print_insert_stamps(mrg_ctx* c) {
+    constexpr uint32_t kMaxWg = 1024;
+    std::vector<unsigned long long> h(4 * kMaxWg);
+    hipStreamSynchronize(c->s);
+    hipMemcpy(h.data(), c->dbg.p, h.size() * 8, hipMemcpyDeviceToHost);
+    unsigned long long t0 = ~0ull;
+    uint32_t nb = 0;
+    for (uint32_t b = 0; b < kMaxWg; b++)
+        if (h[4 * b + 3] > h[4 * b] && h[4 * b]) { t0 = std::min(t0, h[4 * b]); nb++; }
+    if (!nb) return;
+    fprintf(stderr, "[mrg stamps] grep insert, %u workgroups:", nb);
+    for (int k = 0; k < 4; k++) {
+        std::vector<double> v;
+        for (uint32_t b = 0; b < kMaxWg; b++)
+            if (h[4 * b + 3] > h[4 * b] && h[4 * b]) v.push_back((h[4 * b + k] - t0) / 100.0);
+        std::sort(v.begin(), v.end());
+        fprintf(stderr, " phase%d p0 %.1f p50 %.1f p100 %.1f;", k, v[0], v[v.size() / 2], v.back());
+    }
+    fprintf(stderr, "\n");
+    hipMemset(c->dbg.p, 0, h.size() * 8);
+}
+
 // Total bytes the map's long-word record regions may take: the
 // split's size, at least 256 MiB.
 static uint64_t lrec_bytes_cap(uint64_t len) { return std::max<uint64_t>(len, 256ull << 20); }
@@ -1277,6 +1302,7 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
             clear_long_table(t, c->s);
             launch_grep_insert(in, t, cap_lines, spec, emit, c->s);
             HCHK(c, hipGetLastError());
+            if (c->debug_times && t.dbg) print_insert_stamps(c);
             if ((rc = read_counters(c))) { if (p) mrg_parts_free(p); return rc; }
             const uint32_t st = c->h_ctr->status;
             if (spec && (st & kStListFull)) {  // the map's hit list overflowed: the whole attempt again

@@ -1013,10 +1013,14 @@ __device__ uint64_t hash_bytes(const uint8_t* in, int64_t s, int64_t e, uint64_t
     return h;
 }
 
-// hash_bytes plus, in the same pass, FNV-1a-32 of every byte (the partition
-// hash, worker.go:76).
+// A line's FNV-1a-32 (the partition hash, worker.go:76) in one pass over its
+// bytes, and from it and the length the line's LongTable hash.  The table
+// confirms every hash match bytewise, so the hash only has to be a function of
+// the bytes; it is used by grep_insert_kernel's table alone (records merged
+// later are re-inserted into clean tables with hash_bytes).  An FNV-1a-64 chain
+// beside the 32-bit one doubled the kernel's multiplies (C3 insert 0.45 ms).
+// 32-bit position arithmetic within each 64-byte block.
 __device__ __forceinline__ uint64_t hash_line(const uint8_t* in, int64_t s, int64_t e, uint32_t& h32) {
-    uint64_t h = kFnv64Off;
     uint32_t g = 2166136261u;
     for (int64_t q = s; q < e;) {
         const int64_t bi = block_start(in, q);
@@ -1024,22 +1028,26 @@ __device__ __forceinline__ uint64_t hash_line(const uint8_t* in, int64_t s, int6
         uint4 v[4];
 #pragma unroll
         for (int k = 0; k < 4; k++) v[k] = bi + 16 * k < e ? *(const uint4*)(ab + 16 * k) : make_uint4(0, 0, 0, 0);
+        const uint32_t lo = (uint32_t)(q - bi);                      // 0..15
+        const uint32_t span = (uint32_t)((e - bi < 64 ? e - bi : 64) - (int64_t)lo);  // block positions [lo, lo + span)
 #pragma unroll
         for (int k = 0; k < 4; k++) {
             const uint32_t w[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
 #pragma unroll
             for (int j = 0; j < 16; j++) {
-                const int64_t p = bi + 16 * k + j;
-                if (p < q || p >= e) continue;
                 const uint32_t c = (w[j >> 2] >> (8 * (j & 3))) & 0xFFu;
-                h = fnv1a64_step(h, c);
-                g = fnv1a32_step(g, c);
+                if ((uint32_t)(16 * k + j) - lo < span) g = fnv1a32_step(g, c);
             }
         }
         q = bi + 64;
     }
     h32 = g;
-    return h;
+    uint64_t x = ((uint64_t)g << 32) | (uint32_t)(e - s);
+    x ^= x >> 33;
+    x *= 0xFF51AFD7ED558CCDull;
+    x ^= x >> 33;
+    x *= 0xC4CEB9FE1A85EC53ull;
+    return x ^ (x >> 33);
 }
 
 // The first 16 bytes of a line (zero-padded past len) as little-endian k0 / k1:
@@ -1076,8 +1084,14 @@ __device__ __forceinline__ void line_prefix16(const uint8_t* in, int64_t s, uint
 // (C3: 0.26 ms + two host round trips) is not needed.  The record's count
 // (the line's occurrences: mr-X-r holds one KV per occurrence, worker.go:80-92)
 // is the slot's, read by grep_counts_kernel once every insert is in.
+// (t.dbg, MRG_DEBUG_TIMES: per workgroup 4 stamps: start, table inserts done,
+// cursors reserved, lines copied)
+__device__ __forceinline__ void ins_stamp(const Tables& t, int k) {
+    if (t.dbg && threadIdx.x == 0) t.dbg[4 * blockIdx.x + k] = __builtin_amdgcn_s_memrealtime();
+}
 __device__ __forceinline__ void grep_insert_line(const uint8_t* __restrict__ in, const Tables& t, uint64_t i,
                                                  uint64_t nlines, bool emit, unsigned long long* scratch) {
+    ins_stamp(t, 0);
     bool claimed = false;
     uint64_t len = 0, k0 = 0, k1 = 0;
     uint32_t h32 = 0;
@@ -1117,6 +1131,7 @@ __device__ __forceinline__ void grep_insert_line(const uint8_t* __restrict__ in,
         scratch[kLineWaves + wv] = ib;
     }
     __syncthreads();
+    ins_stamp(t, 1);
     if (threadIdx.x == 0) {
         unsigned long long kk = 0, bb = 0;
         for (int w = 0; w < kLineWaves; w++) {  // -> exclusive prefixes per wave
@@ -1128,18 +1143,25 @@ __device__ __forceinline__ void grep_insert_line(const uint8_t* __restrict__ in,
         }
         unsigned long long rb = 0, ab = 0;
         if (kk) {
-            atomicAdd(&t.ctr->long_bytes, bb);
-            const unsigned long long used = atomicAdd(&t.ctr->long_used, kk) + kk;
-            if (used * 10 > (t.lo_mask + 1) * 7) set_status(t.ctr, kStLongFull);
+            // emit: the record cursors count exactly the claims and their bytes,
+            // so they stand in for long_used / long_bytes (grep_counts_kernel
+            // copies them over): two same-address atomics per workgroup step, not four
+            unsigned long long used;
             if (emit) {
                 rb = atomicAdd(&t.ctr->nrec, kk);
                 ab = atomicAdd(&t.ctr->arena, bb);
+                used = rb + kk;
+            } else {
+                atomicAdd(&t.ctr->long_bytes, bb);
+                used = atomicAdd(&t.ctr->long_used, kk) + kk;
             }
+            if (used * 10 > (t.lo_mask + 1) * 7) set_status(t.ctr, kStLongFull);
         }
         scratch[2 * kLineWaves] = rb;
         scratch[2 * kLineWaves + 1] = ab;
     }
     __syncthreads();
+    ins_stamp(t, 2);
     if (!emit) return;  // (workgroup-uniform)
     const uint64_t o = scratch[2 * kLineWaves] + scratch[wv] + ik - (claimed ? 1u : 0u);
     const uint64_t off = scratch[2 * kLineWaves + 1] + scratch[kLineWaves + wv] + ib - (claimed ? len : 0);
@@ -1188,6 +1210,10 @@ __device__ __forceinline__ void grep_insert_line(const uint8_t* __restrict__ in,
             for (int k = 0; k < kCopyLines; k++)
                 if (x < l[k]) t.out.arena[dst[k] + x] = b[k];
         }
+    }
+    if (t.dbg) {
+        __syncthreads();
+        ins_stamp(t, 3);
     }
 }
 
@@ -1482,6 +1508,10 @@ void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, cons
 // The emitted records' counts: cnt held the claimed slot's index.
 __global__ void grep_counts_kernel(Tables t) {
     const uint64_t n = t.ctr->nrec < t.out_cap ? t.ctr->nrec : t.out_cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) {  // (the insert counted its claims in the record cursors only)
+        t.ctr->long_used = t.ctr->nrec;
+        t.ctr->long_bytes = t.ctr->arena;
+    }
     for (uint64_t o = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; o < n; o += (uint64_t)gridDim.x * blockDim.x)
         t.out.cnt[o] = t.lo[t.out.cnt[o] & t.lo_mask].count;
 }
@@ -1489,7 +1519,10 @@ __global__ void grep_counts_kernel(Tables t) {
 void launch_grep_insert(const uint8_t* in, const Tables& t, uint64_t nlines, bool dev_count, bool emit, hipStream_t s) {
     if (nlines == 0) return;
     uint64_t g = (nlines + kLineWG - 1) / kLineWG;
-    if (dev_count && g > 1024) g = 1024;  // (nlines = the capacity: the workgroups stride)
+#ifndef MRG_GREP_INS_GRID
+#define MRG_GREP_INS_GRID 1024
+#endif
+    if (dev_count && g > MRG_GREP_INS_GRID) g = MRG_GREP_INS_GRID;  // (nlines = the capacity: the workgroups stride)
     grep_insert_kernel<<<(unsigned)g, kLineWG, 0, s>>>(in, t, nlines, dev_count ? &t.ctr->nlines : nullptr, emit);
     if (emit) {
         const uint64_t g = (nlines + 255) / 256;
