@@ -1202,6 +1202,9 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
     HCHK(c, c->pat.ensure(plen + 16));
     if (plen) HCHK(c, hipMemcpyAsync(c->pat.p, pat, plen, hipMemcpyHostToDevice, c->s));
     c->lo_log2_cur = 14;
+    // grep_map_kernel's 32-bit chunk indices (with the grid's stride on top)
+    if (len / kGrepChunkBytes + 2 * (uint64_t)c->grid * 16 + 16 >= (1ull << 32))
+        return fail(c, MRG_EINVAL, "split too large for 32-bit chunk indices (%llu bytes)", (unsigned long long)len);
     Ingest ing;
     if (host && plen && (rc = ingest_start(c, ing, host, (uint8_t*)in, len))) return rc;
     if (host && !plen) HCHK(c, hipMemcpyAsync((void*)in, host, len, hipMemcpyHostToDevice, c->s));

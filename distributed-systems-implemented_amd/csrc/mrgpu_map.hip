@@ -580,6 +580,31 @@ __device__ __forceinline__ void grep_dma(const uint8_t* in, uint64_t n, uint64_t
                  : "memory", "m0");
 }
 
+// grep_dma as a stream: the descriptor (base = the window start rounded down
+// to 1 GiB, range = bytes to the split's end) is recomputed only when the
+// offset passes 3 GiB; a chunk's DMA is one 32-bit add.
+struct GrepStream {
+    uint32_t base_lo, base_hi, nrec, voff;
+    __device__ __forceinline__ void set(const uint8_t* in, uint64_t n, uint64_t cs) {
+        const uint64_t base = cs & ~((1ull << 30) - 1);
+        const uint64_t r = n - base;  // wraps if base >= n
+        const uint32_t rhi = (uint32_t)(r >> 32), rlo = (uint32_t)r;
+        nrec = (int32_t)rhi < 0 ? 0u : (rhi != 0 || rlo > 0xFFFFFF00u) ? 0xFFFFFF00u : rlo;
+        const uint64_t b = (uint64_t)(in + base);
+        base_lo = (uint32_t)b;
+        base_hi = (uint32_t)(b >> 32) & 0xFFFFu;
+        voff = (uint32_t)(cs - base);
+    }
+    __device__ __forceinline__ void issue(uint32_t lane, uint32_t lds_base) const {
+        const gi32x4 rs = {(int)__builtin_amdgcn_readfirstlane(base_lo), (int)__builtin_amdgcn_readfirstlane(base_hi),
+                           (int)__builtin_amdgcn_readfirstlane(nrec), 0x00020000};
+        lds_base = __builtin_amdgcn_readfirstlane(lds_base);
+        asm volatile("s_mov_b32 m0, %2\n\tbuffer_load_dwordx4 %0, %1, 0 offen lds" ::"v"(voff + 16u * lane), "s"(rs),
+                     "s"(lds_base)
+                     : "memory", "m0");
+    }
+};
+
 // Of a chunk's occurrences (lane l: 16-bit masks `hit` and `nl` ('\n') of its
 // 16 bytes), keep the first of each line: an occurrence is dropped when an
 // earlier one of the chunk has no '\n' between them (the pattern holds no
@@ -641,21 +666,34 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
     const bool in_lds = plen <= (uint32_t)kAhead + 1;
     const uint32_t p0 = P[0], p1 = plen > 1 ? P[1] : 0u, p2 = plen > 2 ? P[2] : 0u, p3 = plen > 3 ? P[3] : 0u;
     const uint32_t rep0 = p0 * 0x01010101u, rep1 = p1 * 0x01010101u, rep2 = p2 * 0x01010101u, rep3 = p3 * 0x01010101u;
-    const uint64_t stride = (uint64_t)gridDim.x * kWavesPerWG;
-    const uint64_t c0 = cbeg + (uint64_t)blockIdx.x * kWavesPerWG + wv;
+    // Chunk indices are 32-bit (the launcher checks) and the DMA offsets advance
+    // by one 32-bit add per chunk (GrepStream): scalar work the loop no longer
+    // redoes per chunk in 64 bits.
+    const uint32_t stride = gridDim.x * kWavesPerWG;
+    const uint32_t c0 = (uint32_t)cbeg + blockIdx.x * kWavesPerWG + wv, nch = (uint32_t)nchunks;
     const uint32_t slot0 = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)ring[wv][0];
-    const uint64_t cstep = stride * kGrepOwn;
+    const uint64_t cstep = (uint64_t)stride * kGrepOwn;
+    const uint32_t cstep32 = (uint32_t)cstep;  // < 2^24
 #pragma unroll
-    for (uint32_t q = 0; q + 1 < kGrepSlots; q++) grep_dma(in, n, (c0 + q * stride) * kGrepOwn, lane, slot0 + q * kChunk);
+    for (uint32_t q = 0; q + 1 < kGrepSlots; q++)
+        grep_dma(in, n, (uint64_t)(c0 + q * stride) * kGrepOwn, lane, slot0 + q * kChunk);
+    GrepStream ds;
+    ds.set(in, n, (uint64_t)c0 * kGrepOwn + (kGrepSlots - 1) * cstep);
+    // the chunks whose window [cs, cs + kChunk) holds the dword with the split's
+    // last n % 4 bytes (none when n % 4 == 0)
+    const uint64_t n4 = n & ~3ull;
+    const uint32_t tail_lo = (n & 3) == 0 ? ~0u : n4 < kChunk ? 0u : (uint32_t)((n4 - kChunk) / kGrepOwn + 1);
+    const uint32_t tail_hi = (n & 3) == 0 ? 0u : (uint32_t)(n4 / kGrepOwn);
     uint32_t k = 0;
-    uint64_t cs = c0 * kGrepOwn;
-    for (uint64_t c = c0; c < nchunks; c += stride, cs += cstep, k = k == kGrepSlots - 1 ? 0u : k + 1u) {
+    uint64_t cs = (uint64_t)c0 * kGrepOwn;
+    for (uint32_t c = c0; c < nch; c += stride, cs += cstep, k = k == kGrepSlots - 1 ? 0u : k + 1u) {
         // the chunk kGrepSlots - 1 strides ahead into the slot the previous one left
         const uint32_t kn = k == 0 ? kGrepSlots - 1 : k - 1u;
-        grep_dma(in, n, cs + (kGrepSlots - 1) * cstep, lane, slot0 + kn * kChunk);
+        ds.issue(lane, slot0 + kn * kChunk);
+        ds.voff += cstep32;
+        if (ds.voff >= (3u << 30)) ds.set(in, n, cs + kGrepSlots * cstep);  // rare: the window moved 2 GiB past the base
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGrepSlots - 1) : "memory");  // this chunk's DMA has landed
-        const uint64_t n4 = n & ~3ull;
-        if ((n & 3) && n4 >= cs && n4 < cs + kChunk) {
+        if (c >= tail_lo && c <= tail_hi) {
             // the split's last n % 4 bytes sit in a dword the range check zero-filled
             if (lane < (uint32_t)(n & 3)) ((lds_u8*)ring[wv][k])[n4 - cs + lane] = in[n4 + lane];
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1482,6 +1520,7 @@ void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32
     uint64_t g = (nchunks - cbeg + kWavesPerWG - 1) / kWavesPerWG;
     const uint64_t gmax = (uint64_t)grid * 2;
     if (g > gmax) g = gmax;
+    // (32-bit chunk indices in the kernel: mrg_map refuses splits past them)
     grep_map_kernel<<<(unsigned)g, kThreads, 0, s>>>(in, n, cbeg, nchunks, d_pat, plen, t);
 }
 
