@@ -665,7 +665,7 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
     };
     const bool in_lds = plen <= (uint32_t)kAhead + 1;
     const uint32_t p0 = P[0], p1 = plen > 1 ? P[1] : 0u, p2 = plen > 2 ? P[2] : 0u, p3 = plen > 3 ? P[3] : 0u;
-    const uint32_t rep0 = p0 * 0x01010101u, rep1 = p1 * 0x01010101u, rep2 = p2 * 0x01010101u, rep3 = p3 * 0x01010101u;
+    const uint32_t rep0 = p0 * 0x01010101u, rep1 = p1 * 0x01010101u;
     // Chunk indices are 32-bit (the launcher checks) and the DMA offsets advance
     // by one 32-bit add per chunk (GrepStream): scalar work the loop no longer
     // redoes per chunk in 64 bits.
@@ -704,30 +704,32 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
         const uint4 v = from_v4(b4[lane]);
         uint32_t m, q0;  // candidate starts of this lane's bytes; pattern bytes they already match
         if (plen >= 4) {
-            // 4-byte prefix filter, one zero-byte test per dword: y = OR over k < 4
-            // of (the stream shifted by k) ^ (pattern byte k) is zero in byte i
-            // exactly when bytes i..i+3 equal the pattern's first four (~10 VALU a
-            // dword; the per-byte masks of a two-byte filter cost ~70 a lane and
-            // left a candidate loop running in most chunks).  The exact mask only
-            // for lanes with a candidate.
+            // 4-byte prefix filter as 32-bit compares: the word at each of the 16
+            // start offsets (v_alignbyte of the lane's dwords and the next lane's
+            // first) against the pattern's first four bytes, the compare results
+            // straight into lane masks OR-ed by the scalar unit (7 VALU a dword);
+            // the exact per-offset mask only for lanes with a candidate.  (A
+            // zero-byte test of OR-ed shifted XORs per dword, ~10 VALU a dword,
+            // measured 0.08 ms slower per 10 GB; per-byte masks of the first two
+            // bytes ~70 VALU a lane and a candidate loop in most chunks: 0.19 ms.)
+            const uint32_t p4 = p0 | p1 << 8 | p2 << 16 | p3 << 24;
             const uint32_t nx = (uint32_t)__shfl_down((int)v.x, 1);  // the next lane's first dword
             const uint32_t w[5] = {v.x, v.y, v.z, v.w, nx};
-            uint32_t y[4];
+            uint64_t cand = 0;
 #pragma unroll
             for (int j = 0; j < 4; j++) {
-                const uint32_t s1 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], 1);
-                const uint32_t s2 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], 2);
-                const uint32_t s3 = __builtin_amdgcn_alignbyte(w[j + 1], w[j], 3);
-                // (a ^ b) | c as v_bitop3_b32 (truth table 0xBE)
-                const uint32_t u = __builtin_amdgcn_bitop3_b32(w[j], rep0, s1 ^ rep1, 0xBE);
-                y[j] = u | __builtin_amdgcn_bitop3_b32(s2, rep2, s3 ^ rep3, 0xBE);
-            }
-            // any zero byte (the borrow's false positives sit above a true zero only)
-            uint32_t zany = 0;
+                cand |= __ballot(w[j] == p4);
 #pragma unroll
-            for (int j = 0; j < 4; j++) zany |= (y[j] - 0x01010101u) & ~y[j];
+                for (int b = 1; b < 4; b++) cand |= __ballot(__builtin_amdgcn_alignbyte(w[j + 1], w[j], b) == p4);
+            }
             m = 0;
-            if ((zany & 0x80808080u) != 0 && lane < kGrepOwn / 16) m = eq_mask16((uint4){y[0], y[1], y[2], y[3]}, 0u);
+            if (lane < kGrepOwn / 16 && __builtin_amdgcn_inverse_ballot_w64(cand)) {
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+#pragma unroll
+                    for (int b = 0; b < 4; b++)
+                        if ((b == 0 ? w[j] : __builtin_amdgcn_alignbyte(w[j + 1], w[j], b)) == p4) m |= 1u << (4 * j + b);
+            }
             q0 = 4;
         } else {
             m = lane < kGrepOwn / 16 ? eq_mask16(v, rep0) : 0u;
