@@ -684,6 +684,7 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
     const uint64_t n4 = n & ~3ull;
     const uint32_t tail_lo = (n & 3) == 0 ? ~0u : n4 < kChunk ? 0u : (uint32_t)((n4 - kChunk) / kGrepOwn + 1);
     const uint32_t tail_hi = (n & 3) == 0 ? 0u : (uint32_t)(n4 / kGrepOwn);
+    const uint32_t tail_span = (n & 3) == 0 ? 0u : tail_hi - tail_lo;  // (n % 4 == 0: c - ~0u <= 0 only for c = ~0u: never)
     uint32_t k = 0;
     uint64_t cs = (uint64_t)c0 * kGrepOwn;
     for (uint32_t c = c0; c < nch; c += stride, cs += cstep, k = k == kGrepSlots - 1 ? 0u : k + 1u) {
@@ -693,7 +694,7 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
         ds.voff += cstep32;
         if (ds.voff >= (3u << 30)) ds.set(in, n, cs + kGrepSlots * cstep);  // rare: the window moved 2 GiB past the base
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kGrepSlots - 1) : "memory");  // this chunk's DMA has landed
-        if (c >= tail_lo && c <= tail_hi) {
+        if (c - tail_lo <= tail_span) {  // c in [tail_lo, tail_hi]: one unsigned compare
             // the split's last n % 4 bytes sit in a dword the range check zero-filled
             if (lane < (uint32_t)(n & 3)) ((lds_u8*)ring[wv][k])[n4 - cs + lane] = in[n4 + lane];
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -781,7 +782,9 @@ __global__ void __launch_bounds__(kThreads) grep_map_kernel(const uint8_t* __res
         if (__ballot(any)) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // rare paths: drain
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // this slot's LDS reads are done before it is refilled
-        if (*wcnt >= kGrepBuf - kGrepFlushRoom) flush();
+        // (the buffer only grows in chunks with a match: no LDS read of the count
+        // in the others)
+        if (lanes_hit != 0 && *wcnt >= kGrepBuf - kGrepFlushRoom) flush();
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last prefetch lands before the workgroup exits
     flush();

@@ -1,0 +1,8 @@
+# grep map: the match-count read only in chunks with a match (f1) vs HEAD (f0):
+# grep GPU tests, then C3 lines alternating.
+set -e
+out=gpurun_out/r5av
+mkdir -p $out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "grep or smoke or run_job" > $out/tests.log 2>&1
+tail -1 $out/tests.log
+timeout -k 10 900 bash distributed-systems-implemented_amd/tools/ab_libs.sh r5av c3 f0 f1
