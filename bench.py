@@ -22,6 +22,11 @@ Other §8d workloads (evidence runs; the default is C2):
 Run:  python bench.py [--gpus N --steps K --warmup W]
       N > 1: python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
              --master-addr 127.0.0.1 --master-port P bench.py --gpus N ...
+      or plain `python bench.py --gpus N`: with no WORLD_SIZE in the environment
+      it starts those N ranks itself, as a child torch.distributed.run (before
+      any GPU call; the parent forwards rank 0's line and the child's exit code).
+      N > 1 defaults to C4 (12.5 GB per GPU, nReduce = 64, the 8-GPU 100 GB
+      config) with the C5 weak-scaling sub-run (E(P) at 25 GB per GPU).
 Prints ONE JSON line on rank 0.
 """
 from __future__ import annotations
@@ -68,6 +73,46 @@ PATTERN = b"distributed"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 HBM_COPY_GBS = 6290.0  # measured copy bandwidth (secondary reference)
 XGMI_LINK_GBS = 153.0  # per xGMI link (7 links x ~153 GB/s per GPU)
+
+
+def host_threads() -> int:
+    """Host threads per rank for generation and the oracle checks: the box's
+    cores split over the ranks of this node (8 ranks x 16 threads would
+    oversubscribe a node whose ranks all generate and check at once)."""
+    per_node = int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1")))
+    return max(1, min(16, (os.cpu_count() or 1) // max(1, per_node)))
+
+
+def self_launch(argv: list[str], n: int) -> int:
+    """`bench.py --gpus N` (N > 1) with no launcher around it: run the N ranks
+    as a child `torch.distributed.run` on 127.0.0.1 and return its exit code.
+    A child, never an exec: this process must not replace itself (nothing here
+    has touched the GPU yet, but the rule is kept everywhere).  The ranks inherit
+    stdout, so rank 0's JSON line is this command's line."""
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + argv
+    log(f"--gpus {n} without WORLD_SIZE: starting {n} ranks ({' '.join(cmd[1:6])} ...)")
+    return subprocess.call(cmd, env=dict(os.environ, MASTER_ADDR="127.0.0.1"))
+
+
+class Wall:
+    """Wall seconds of the run's host-side phases (generation, upload, timed
+    steps, checks, sub-runs), reported in the line: the N = 8 run must fit the
+    driver's time limit (DESIGN.md §7 budget)."""
+
+    def __init__(self):
+        self.t0 = time.time()
+        self.phases: dict[str, float] = {}
+
+    def add(self, name: str, t_start: float):
+        self.phases[name] = round(self.phases.get(name, 0.0) + time.time() - t_start, 1)
+
+    def as_dict(self):
+        return {**self.phases, "total": round(time.time() - self.t0, 1)}
 
 
 def log(msg):
@@ -121,14 +166,14 @@ def gen_corpus(w: dict, rank: int, file_mb: int, nfiles: int, split: int = 0):
     uniform = w["app"] == "grep" or w["V"] <= 10**6
     if uniform:
         seeds = [file_seed(w, rank, split, i) for i in range(nfiles)]
-        voc.fill_files([sz] * nfiles, seeds, file_params(w, 0, nfiles), threads=min(16, os.cpu_count() or 1), out=buf)
+        voc.fill_files([sz] * nfiles, seeds, file_params(w, 0, nfiles), threads=host_threads(), out=buf)
     else:
         from concurrent.futures import ThreadPoolExecutor  # the C generator releases the GIL
 
         def one(i):
             voc.fill_files([sz], [file_seed(w, rank, split, i)], file_params(w, i, nfiles), threads=1,
                            out=buf[i * sz:(i + 1) * sz])
-        with ThreadPoolExecutor(min(16, os.cpu_count() or 1)) as ex:
+        with ThreadPoolExecutor(host_threads()) as ex:
             list(ex.map(one, range(nfiles)))
     return buf
 
@@ -259,20 +304,24 @@ def _oracle():
     return O
 
 
-def oracle_exact_check(w: dict, host: np.ndarray, gpu_parts: list[bytes], nreduce: int, rank: int, world: int) -> dict:
+def oracle_exact_check(w: dict, host: np.ndarray, gpu_parts: list[bytes], nreduce: int, rank: int, world: int,
+                       local_reduce: bool = False) -> dict:
     """Byte equality of every mr-out-r of the full-size job with the C oracle's
     (oracle/mrcount.c: the reference's wc / grep job restated, counted by host
     threads over the same split; main/mrsequential.go:59-84, mrapps/wc.go:21-34,
     mrapps/dgrep.go:18-46).  N > 1: every rank counts its own split, the
     partitions travel to their owners (r % N) over gloo and are merged there
     (the reduce over all splits' intermediates, worker.go:123-146), and each
-    owner compares its partitions; non-owned partitions must be empty."""
+    owner compares its partitions; non-owned partitions must be empty.
+    local_reduce (a rehearsal: ranks share a device, no exchange, every rank
+    reduced all partitions of its own split): each rank against its own count."""
     O = _oracle()
     app = "wc" if w["app"] == "wc" else "grep:" + PATTERN.decode()
-    threads = min(16, os.cpu_count() or 1)
+    threads = host_threads()
     t0 = time.time()
     mine = O.c_count_mt(app, host, nreduce, threads)
-    if world > 1:
+    own = (lambda r: True) if local_reduce or world == 1 else (lambda r: r % world == rank)
+    if world > 1 and not local_reduce:
         from mrgpu import dist as D
         send = []
         for o in range(world):
@@ -291,10 +340,10 @@ def oracle_exact_check(w: dict, host: np.ndarray, gpu_parts: list[bytes], nreduc
         want = O.c_merge_parts(app, outs)
     else:
         want = mine
-    ok = all(gpu_parts[r] == (want[r] if r % world == rank else b"") for r in range(nreduce))
-    bad = [r for r in range(nreduce) if gpu_parts[r] != (want[r] if r % world == rank else b"")]
+    bad = [r for r in range(nreduce) if gpu_parts[r] != (want[r] if own(r) else b"")]
+    ok = not bad
     res = {"exact_vs_oracle": ok, "oracle_s": round(time.time() - t0, 1), "oracle_threads": threads,
-           "oracle_output_bytes": sum(len(want[r]) for r in range(nreduce) if r % world == rank)}
+           "oracle_output_bytes": sum(len(want[r]) for r in range(nreduce) if own(r))}
     if bad:
         res["mismatched_partitions"] = bad[:16]
     if world > 1:
@@ -420,10 +469,11 @@ def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: 
     nsplits = max(1, args.scaling_splits)
     devs = []
     t0 = time.time()
-    for sp in range(nsplits):
-        host = gen_corpus(w, rank, w["file_mb"], args.scaling_files or w["files"], sp)
-        devs.append(upload(host, local))
-        del host
+    with heartbeat(f"[{wname}] generating the splits"):
+        for sp in range(nsplits):
+            host = gen_corpus(w, rank, w["file_mb"], args.scaling_files or w["files"], sp)
+            devs.append(upload(host, local))
+            del host
     nbytes = int(devs[0].numel())
     log(f"[{wname}] generated {nsplits} x {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
     ctx = Context(local)
@@ -449,7 +499,10 @@ def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: 
     parts = [out[offs[i]:offs[i + 1]] for i in range(w["nreduce"])]
     chk = check_output(parts, w["nreduce"], "wc")
     owned_ok = all(not parts[r] for r in range(w["nreduce"]) if r % world != rank) or shared
-    tw = torch.tensor([chk["total_words"]], dtype=torch.int64)
+    # Σ counts over every owner's partitions = an independent count of every
+    # rank's split 0 (plain torch ops on the resident input)
+    indep = ascii_word_count(devs[0])
+    tw = torch.tensor([chk["total_words"], -(1 << 40) if indep is None else indep], dtype=torch.int64)
     dist.all_reduce(tw)
     t1 = no_shuffle_time(ctx, run_step, steps, shared, nsplits)
     res = {"workload": f"{w['desc']}; {nbytes / 1e9:.2f} GB per GPU", "nreduce": w["nreduce"],
@@ -458,7 +511,8 @@ def scaling_subrun(wname: str, args, rank: int, world: int, local: int, shared: 
            "ms_per_step": round(t_max / steps * 1e3, 3),
            **multi_fields(stats, t_max, t1, world, shared, ndev),
            "checks": {"sorted_unique": chk["sorted_unique"], "partition_ok": chk["partition_ok"],
-                      "non_owned_empty": owned_ok, "total_words": int(tw.item())}}
+                      "non_owned_empty": owned_ok, "total_words": int(tw[0]),
+                      "total_words_match": int(tw[0]) == int(tw[1])}}
     ctx.close()
     del devs
     torch.cuda.empty_cache()
@@ -516,7 +570,8 @@ def group_rehearsal(args) -> dict:
                 "distinct_keys_per_rank": [int(s["distinct_keys"]) for s in mst],
                 "map_kernel_ms": [round(s["map_kernel_ms"], 3) for s in mst],
                 "map_total_ms": [round(s["map_total_ms"], 3) for s in mst],
-                "records_per_owner_after_reaggregation": [int(x) for x in recv],
+                "keys_per_owner_after_reaggregation": [int(x) for x in recv],
+                "records_received_per_owner": [int(s["shuffle_recv_records"]) for s in est],
                 "exchange_unpack_ms": [round(s["exchange_unpack_ms"], 3) for s in est],
                 "shuffle_send_bytes": [int(s["shuffle_send_bytes"]) for s in est],
                 "owner_reduce_ms": [round(s["reduce_ms"], 3) for s in rst],
@@ -537,7 +592,8 @@ def group_rehearsal(args) -> dict:
            "exchange_unpack_ms_mean": round(sum(last["exchange_unpack_ms"]) / P, 3),
            "owner_reduce_ms_max": max(last["owner_reduce_ms"]),
            "owner_reduce_ms_mean": round(sum(last["owner_reduce_ms"]) / P, 3),
-           "records_received_per_owner": last["records_per_owner_after_reaggregation"],
+           "keys_per_owner_after_reaggregation": last["keys_per_owner_after_reaggregation"],
+           "records_received_per_owner": last["records_received_per_owner"],
            "per_step": steps,
            "checks": {"exact_vs_oracle": not bad, "mismatched": bad[:16],
                       "oracle_output_bytes": sum(len(x) for x in want)},
@@ -554,7 +610,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c2")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default=None,
+                    help="default: c2 (configs[1]) on one GPU, c4 (configs[3]: 12.5 GB per GPU, nReduce = 64) for N > 1")
     ap.add_argument("--file-mb", type=int, default=None, help="override the workload's file size (MB)")
     ap.add_argument("--files", type=int, default=None, help="override the workload's file count")
     ap.add_argument("--nreduce", type=int, default=None, help="override the workload's nReduce")
@@ -581,28 +638,48 @@ def main():
     ap.add_argument("--group-files", type=int, default=100, help="C5 files per rank (all of them: every word once)")
     ap.add_argument("--group-file-mb", type=int, default=10)
     ap.add_argument("--group-steps", type=int, default=2)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="resolve ranks, workload and sizes, print them from rank 0 and exit (no GPU call)")
     args = ap.parse_args()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ and not args.group_rehearsal:
+        sys.exit(self_launch(sys.argv[1:], args.gpus))
     if args.group_rehearsal:
         torch.zeros(1, device="cuda:0").add_(1)
         torch.cuda.synchronize()
         print(json.dumps(group_rehearsal(args)), flush=True)
         return
-    w = WORKLOADS[args.workload]
-    args.file_mb = args.file_mb or w["file_mb"]
-    args.files = args.files or w["files"]
-    args.nreduce = args.nreduce or w["nreduce"]
-    grep = w["app"] == "grep"
-
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"--gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    # N > 1: the headline is C4, the 8-GPU config (12.5 GB per GPU, R = 64:
+    # 64 partitions spread evenly over 2, 4 or 8 owners); E(P) comes from the
+    # C5 sub-run below
+    args.workload = args.workload or ("c4" if world > 1 else "c2")
+    w = WORKLOADS[args.workload]
+    args.file_mb = args.file_mb or w["file_mb"]
+    args.files = args.files or w["files"]
+    args.nreduce = args.nreduce or w["nreduce"]
+    grep = w["app"] == "grep"
+    wall = Wall()
     if world > 1:
         import datetime
         # control plane only (the shuffle is RCCL inside libmrgpu); a lost rank
         # ends the job in minutes rather than gloo's default half hour
         dist.init_process_group("gloo", timeout=datetime.timedelta(minutes=10))
+    if args.dry_run:
+        info = {"rank": rank, "n_gpus": world, "workload": args.workload, "nreduce": args.nreduce,
+                "input_bytes_per_gpu": args.files * args.file_mb * 1_000_000, "host_threads": host_threads(),
+                "scaling_workload": args.scaling_workload if world > 1 else None}
+        if world > 1:
+            allinfo = [None] * world
+            dist.all_gather_object(allinfo, info)
+            info = {**info, "ranks": [i["rank"] for i in allinfo]}
+            dist.destroy_process_group()
+        if rank == 0:
+            print(json.dumps({"dry_run": True, **info}), flush=True)
+        return
     # one GPU per rank; more ranks than devices only as an explicit rehearsal of
     # the N > 1 path on a smaller box (the driver's N-GPU runs have one each)
     ndev = max(1, torch.cuda.device_count())
@@ -626,8 +703,12 @@ def main():
     devs = []
     with heartbeat("generating the splits"):
         for sp in range(nsplits):
+            tg = time.time()
             host = gen_corpus(w, rank, args.file_mb, args.files, sp)
+            wall.add("generate", tg)
+            tg = time.time()
             devs.append(upload(host, local))
+            wall.add("upload", tg)
             del host
     nbytes = int(devs[0].numel())
     log(f"generated {nsplits} x {nbytes / 1e9:.2f} GB in {time.time() - t0:.1f} s")
@@ -652,7 +733,9 @@ def main():
                                nreduce=args.nreduce, copy_out=False)
         return ctx.run_job(MRG_APP_WC, device_ptr=dptrs[sp], nbytes=nbytes, nreduce=args.nreduce, copy_out=False)
 
+    tg = time.time()
     t_max, stats, cold_ms, cold_st = timed_steps(ctx, run_step, args.steps, args.warmup, world, nsplits)
+    wall.add("warmup_and_timed_steps", tg)
     kern_ms = [st["map_kernel_ms"] for st in stats]
     log("map kernel ms per timed step: " + " ".join(f"{k:.2f}" for k in kern_ms))
     log("aggregation ms per timed step: " + " ".join(f"{st['agg_ms']:.2f}" for st in stats))
@@ -717,6 +800,7 @@ def main():
     import ctypes
     checks = {}
     per_split = []
+    tchk = time.time()
     for sp in range(nsplits):
         p, n, offs = run_step(sp)
         out = ctypes.string_at(p, n) if n else b""
@@ -741,10 +825,10 @@ def main():
                 dist.all_reduce(ti)
                 ck["total_words_independent"] = int(ti.item())
                 ck["total_words_match"] = ck["total_words_independent"] == ck[key]
-        if not args.no_oracle and not shared:
+        if not args.no_oracle:
             with heartbeat(f"oracle check of split {sp}"):
                 host = download(devs[sp])
-                ck.update(oracle_exact_check(w, host, parts, args.nreduce, rank, world))
+                ck.update(oracle_exact_check(w, host, parts, args.nreduce, rank, world, local_reduce=shared))
             del host
         del out, parts
         per_split.append(ck)
@@ -755,13 +839,16 @@ def main():
             checks[k] = all(vals)
     if nsplits > 1:
         checks["per_split"] = per_split
+    wall.add("output_and_oracle_checks", tchk)
 
     # N > 1: the shuffle's share and the weak-scaling efficiency against the
     # same ranks running their splits with no shuffle (T(1) of the same per-GPU
     # work, measured in this process, every partition reduced locally)
     multi = None
     if world > 1:
+        tg = time.time()
         t1 = no_shuffle_time(ctx, run_step, args.steps, shared, nsplits)
+        wall.add("no_shuffle_steps", tg)
         multi = multi_fields(stats, t_max, t1, world, shared, ndev)
         multi["note"] = ("shuffle bytes = wire bytes a rank sends to the other ranks (max over ranks of the mean over "
                          "timed steps; 24-byte wire records + long-key bytes); xgmi_frac = those bytes / all-to-all time "
@@ -820,7 +907,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        tg = time.time()
         cpu = cpu_baseline(w, args.cpu_sample_files, args.cpu_sample_mb, args.cpu_seq_files, args.nreduce, ctx)
+        wall.add("cpu_baseline", tg)
 
     ctx.close()
     dev = host = None
@@ -828,7 +917,15 @@ def main():
     torch.cuda.empty_cache()
     scaling = None
     if world > 1 and args.scaling_workload not in ("", "none") and args.scaling_workload != args.workload:
+        tg = time.time()
         scaling = scaling_subrun(args.scaling_workload, args, rank, world, local, shared, ndev)
+        wall.add("scaling_subrun", tg)
+    # the slowest rank's phases (the run ends when it does)
+    wall_s = wall.as_dict()
+    if world > 1:
+        allw = [None] * world
+        dist.all_gather_object(allw, wall_s)
+        wall_s = {k: max(x.get(k, 0.0) for x in allw) for k in allw[0]}
 
     if rank == 0:
         line = {
@@ -891,6 +988,7 @@ def main():
             "multi_gpu": multi,
             "multi_gpu_scaling_workload": scaling,
             "cpu_baseline": cpu,
+            "wall_s": wall_s,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -1253,8 +1253,8 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
         } else {
             t.hits = t.list;  // the map kernel's order (grep_resolve_kernel: unsorted)
         }
-        launch_grep_resolve(in, len, (uint32_t)plen, t, nhits, dev, sorted, c->s);
-        if (dev) launch_grep_resolve_long(in, len, (uint32_t)plen, t, 0, nhits, true, false, c->s);
+        launch_grep_resolve(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, nhits, dev, sorted, c->s);
+        if (dev) launch_grep_resolve_long(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, 0, nhits, true, false, c->s);
         HCHK(c, hipGetLastError());
         // emit (default): the insert writes each distinct line's record as it
         // claims the line's slot, into parts sized for every occurrence (records
@@ -1277,7 +1277,8 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
             if ((rc = read_counters(c))) return rc;
             if (dev && grow_on_overflow(c, c->h_ctr->status & kStListFull)) continue;
             if (sorted && c->h_ctr->ndefer) {
-                launch_grep_resolve_long(in, len, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, false, true, c->s);
+                launch_grep_resolve_long(in, len, (const uint8_t*)c->pat.p, (uint32_t)plen, t, c->h_ctr->ndefer, nhits, false,
+                                         true, c->s);
                 HCHK(c, hipGetLastError());
                 if ((rc = read_counters(c))) return rc;
             }
@@ -1304,7 +1305,10 @@ static int grep_map(mrg_ctx* c, const uint8_t* in, uint64_t len, const uint8_t* 
             }
             clear_long_table(t, c->s);
             launch_grep_insert(in, t, cap_lines, spec, emit, c->s);
-            HCHK(c, hipGetLastError());
+            if (hipGetLastError() != hipSuccess) {
+                if (p) mrg_parts_free(p);
+                return fail(c, MRG_EDEVICE, "grep: line table insert launch");
+            }
             if (c->debug_times && t.dbg) print_insert_stamps(c);
             if ((rc = read_counters(c))) { if (p) mrg_parts_free(p); return rc; }
             const uint32_t st = c->h_ctr->status;
@@ -2287,6 +2291,7 @@ static void exch_bytes(const ExchPlan& pl, int P, int me, mrg_stats* st) {
     }
     st->shuffle_send_bytes = snd;
     st->shuffle_recv_bytes = rcv;
+    st->shuffle_recv_records = pl.rrec;  // every rank's segment, this rank's own included
 }
 
 static int exchange_rccl(mrg_ctx* c, const mrg_parts* local, int P, mrg_parts** owned);
@@ -2467,6 +2472,7 @@ int mrg_run_job(mrg_ctx* c, int app, const void* buf, size_t len, int kind, cons
         keep.rccl_rank = c->stats.rccl_rank;
         keep.shuffle_send_bytes = c->stats.shuffle_send_bytes;
         keep.shuffle_recv_bytes = c->stats.shuffle_recv_bytes;
+        keep.shuffle_recv_records = c->stats.shuffle_recv_records;
         mrg_parts_free(p);
         if (rc) return rc;
         use = o;
@@ -2554,6 +2560,7 @@ int mrg_run_job_async(mrg_ctx* c, int app, const void* buf, size_t len, int kind
         keep.rccl_rank = c->stats.rccl_rank;
         keep.shuffle_send_bytes = c->stats.shuffle_send_bytes;
         keep.shuffle_recv_bytes = c->stats.shuffle_recv_bytes;
+        keep.shuffle_recv_records = c->stats.shuffle_recv_records;
         mrg_parts_free(p);
         if (rc) return rc;
         use = o;

@@ -253,11 +253,10 @@ void launch_grep_map(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32
 // window to t.defer (ctr->ndefer).  dev_count: nhits is the list's capacity
 // and the kernels read the hit / deferred-hit counts on the device, so no host
 // round trip sits between the map kernel and the line resolution.
-void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, bool dev_count,
-                         bool sorted, hipStream_t s);
-// The deferred hits, one workgroup each (wide coalesced scans).
-void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t ndefer,
-                              uint64_t nhits, bool dev_count, bool sorted, hipStream_t s);
+void launch_grep_resolve(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t,
+                         uint64_t nhits, bool dev_count, bool sorted, hipStream_t s);
+void launch_grep_resolve_long(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t,
+                              uint64_t ndefer, uint64_t nhits, bool dev_count, bool sorted, hipStream_t s);
 // t.lines -> the LongTable (one distinct line = one slot).
 // emit: each line that claims its slot also writes its record (t.out: key
 // prefix, length, partition, its bytes copied to the arena at ctr->arena) —

@@ -864,6 +864,54 @@ __device__ int64_t last_nl_before(const uint8_t* in, int64_t lo, int64_t p) {
     return -1;
 }
 
+// Whether the pattern occurs at input offset x (x + plen <= n checked).
+__device__ __forceinline__ bool occurs_at(const uint8_t* in, int64_t n, int64_t x, const uint8_t* pat, uint32_t plen) {
+    if (x < 0 || x + (int64_t)plen > n) return false;
+    for (uint32_t q = 0; q < plen; q++)
+        if (in[x + q] != pat[q]) return false;
+    return true;
+}
+
+// Unsorted hits: the line start of hit p, found like last_nl_before(in, 0, p),
+// and whether the line has an occurrence of the pattern starting before the
+// hit's chunk [cs, cs + kGrepOwn).  Such an occurrence belongs to an earlier
+// chunk, which emitted this same line occurrence (grep_map_kernel keeps the
+// first hit of each line per chunk), so this hit is dropped: every line
+// occurrence is resolved exactly once, by the first chunk holding a hit in it
+// (its record count is then the number of times the line occurs, as
+// dgrep.go:30-33 emits one KeyValue per matching line).  The scan stops at the
+// first '\n' or earlier occurrence below p, so over a long line with hits in
+// many chunks the scans cover disjoint byte ranges (linear).
+// Returns the '\n' position, -1 (none: the split's first line), -2 (beyond
+// kLineScan) or -3 (an earlier chunk's occurrence: drop).
+__device__ int64_t line_start_first_chunk(const uint8_t* in, int64_t n, int64_t p, int64_t cs, const uint8_t* pat,
+                                          uint32_t plen) {
+    const uint32_t rep0 = (uint32_t)pat[0] * 0x01010101u;
+    int64_t q = p;
+    while (q > 0) {
+        if (p - q >= kLineScan) return -2;
+        int64_t bi;
+        const uint4 v = block16(in, q - 1, bi);
+        const uint32_t below = (2u << (uint32_t)(q - 1 - bi)) - 1u;  // bytes < q
+        const uint32_t valid = bi < 0 ? ~((1u << (uint32_t)(-bi)) - 1u) : ~0u;  // bytes >= 0
+        const uint32_t nl = eq_mask16(v, 0x0A0A0A0Au) & below & valid;
+        const int64_t top_nl = nl ? bi + 31 - __builtin_clz(nl) : -1;
+        if (bi < cs) {  // occurrences starting below the chunk, above the newline
+            uint32_t m = eq_mask16(v, rep0) & below & valid;
+            if (cs - bi < 16) m &= (1u << (uint32_t)(cs - bi)) - 1u;
+            if (top_nl >= 0) m &= ~((2u << (uint32_t)(top_nl - bi)) - 1u);
+            while (m) {
+                const uint32_t b = 31 - __builtin_clz(m);
+                m &= ~(1u << b);
+                if (occurs_at(in, n, bi + b, pat, plen)) return -3;
+            }
+        }
+        if (nl) return top_nl;
+        q = bi;
+    }
+    return -1;
+}
+
 // Position of the first '\n' in [q0, n): n if there is none, -2 if none within
 // kLineScan bytes.
 __device__ int64_t first_nl_from(const uint8_t* in, int64_t n, int64_t q0) {
@@ -909,7 +957,8 @@ __device__ __forceinline__ void put_line(const Tables& t, uint64_t cap, bool kee
 // hit (no '\n' since it) is dropped; unsorted (the map kernel's order, no sort
 // pass: C3 ~0.13 ms of radix passes), every hit resolves its own line, and the
 // LongTable's insert merges the rare repeats (a line with hits in two chunks).
-__global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
+__global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                               const uint8_t* __restrict__ pat, uint32_t plen,
                                                                Tables t, uint64_t cap, const unsigned long long* dn,
                                                                bool sorted) {
     __shared__ unsigned long long scratch[kLineWaves + 1];
@@ -929,11 +978,13 @@ __global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __
                 keep = true;
             } else {
                 const int64_t lo = i == 0 || !sorted ? 0 : (int64_t)t.hits[i - 1] + 1;
-                const int64_t q = last_nl_before(in, lo, p);
+                const int64_t q = sorted ? last_nl_before(in, lo, p)
+                                         : line_start_first_chunk(in, (int64_t)n, p, p - p % (int64_t)kGrepOwn, pat, plen);
                 if (q == -2) defer = true;
                 else if (q >= 0) { s = q + 1; keep = true; }
-                else if (lo == 0) { s = 0; keep = true; }  // no '\n' before the hit: the split's first line
-                // else: no '\n' since the previous hit, which named this line already
+                else if (q == -1 && lo == 0) { s = 0; keep = true; }  // no '\n' before the hit: the split's first line
+                // else: no '\n' since the previous hit (sorted), or an earlier chunk's
+                // occurrence in the line (unsorted): that hit names this line
             }
             if (keep) {
                 e = first_nl_from(in, (int64_t)n, p + plen);
@@ -951,7 +1002,8 @@ __global__ void __launch_bounds__(kLineWG) grep_resolve_kernel(const uint8_t* __
 
 // Deferred hits: one 256-thread workgroup each, 16 bytes per lane per step
 // (4 KiB steps of aligned blocks), block-wide max / min of the newline found.
-__global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* __restrict__ in, uint64_t n, uint32_t plen,
+__global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* __restrict__ in, uint64_t n,
+                                                                const uint8_t* __restrict__ pat, uint32_t plen,
                                                                 Tables t, uint64_t ndefer_h, uint64_t cap, bool sorted,
                                                                 bool dev_count) {
     // dev_count: the deferred count read here (no host round trip; none: every
@@ -976,8 +1028,12 @@ __global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* _
         bool keep = true;
         if (plen != 0) {
             const int64_t lo = i == 0 || !sorted ? 0 : (int64_t)t.hits[i - 1] + 1;
+            // unsorted: occurrences starting below the hit's chunk end the scan
+            // too (line_start_first_chunk: an earlier chunk resolves this line)
+            const int64_t cs = sorted ? 0 : p - p % (int64_t)kGrepOwn;
             // aligned blocks from the one holding p - 1 downwards: block k starts at
-            // input offset top - 16 k
+            // input offset top - 16 k.  Events: 2 x ('\n' position), 2 x (occurrence
+            // start) + 1; the highest event below p decides.
             const int64_t top = (int64_t)(((base + (uint64_t)p - 1) & ~(uintptr_t)15) - base);
             long long found = -1;
             for (int64_t step = 0; found < 0; step++) {
@@ -989,11 +1045,21 @@ __global__ void __launch_bounds__(256) grep_resolve_long_kernel(const uint8_t* _
                     const uint4 v = *(const uint4*)(in + bo);
                     uint32_t m = eq_mask16(v, 0x0A0A0A0Au);
                     for (int b = 15; b >= 0; b--)
-                        if (((m >> b) & 1u) && bo + b >= lo && bo + b < p) { mine = bo + b; break; }
+                        if (((m >> b) & 1u) && bo + b >= lo && bo + b < p) { mine = 2 * (bo + b); break; }
+                    if (bo < cs) {
+                        uint32_t c = eq_mask16(v, (uint32_t)pat[0] * 0x01010101u);
+                        for (int b = 15; b >= 0; b--)
+                            if (((c >> b) & 1u) && bo + b >= 0 && bo + b < cs && 2 * (bo + b) + 1 > mine &&
+                                occurs_at(in, (int64_t)n, bo + b, pat, plen)) {
+                                mine = 2 * (bo + b) + 1;
+                                break;
+                            }
+                    }
                 }
                 found = block_max(mine);
             }
-            if (found >= 0) s = found + 1;
+            if (found >= 0 && (found & 1)) keep = false;  // an earlier chunk's occurrence in this line
+            else if (found >= 0) s = found / 2 + 1;
             else if (lo == 0) s = 0;
             else keep = false;
         }
@@ -1533,20 +1599,20 @@ void launch_grep_all_lines(const uint8_t* in, uint64_t n, const Tables& t, int g
     grep_all_lines_kernel<<<grid * 4, 256, 0, s>>>(in, n, t);
 }
 
-void launch_grep_resolve(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t nhits, bool dev_count,
-                         bool sorted, hipStream_t s) {
+void launch_grep_resolve(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t,
+                         uint64_t nhits, bool dev_count, bool sorted, hipStream_t s) {
     if (nhits == 0) return;
     uint64_t g = (nhits + kLineWG - 1) / kLineWG;
     if (dev_count && g > 1024) g = 1024;  // (nhits = the list's capacity: the workgroups stride)
-    grep_resolve_kernel<<<(unsigned)g, kLineWG, 0, s>>>(in, n, plen, t, nhits, dev_count ? &t.ctr->nlist : nullptr,
-                                                        sorted);
+    grep_resolve_kernel<<<(unsigned)g, kLineWG, 0, s>>>(in, n, d_pat, plen, t, nhits,
+                                                        dev_count ? &t.ctr->nlist : nullptr, sorted);
 }
 
-void launch_grep_resolve_long(const uint8_t* in, uint64_t n, uint32_t plen, const Tables& t, uint64_t ndefer,
-                              uint64_t nhits, bool dev_count, bool sorted, hipStream_t s) {
+void launch_grep_resolve_long(const uint8_t* in, uint64_t n, const uint8_t* d_pat, uint32_t plen, const Tables& t,
+                              uint64_t ndefer, uint64_t nhits, bool dev_count, bool sorted, hipStream_t s) {
     if (!dev_count && ndefer == 0) return;
     const uint64_t g = dev_count ? 1024 : ndefer < 4096 ? ndefer : 4096;
-    grep_resolve_long_kernel<<<(unsigned)g, 256, 0, s>>>(in, n, plen, t, ndefer, nhits, sorted, dev_count);
+    grep_resolve_long_kernel<<<(unsigned)g, 256, 0, s>>>(in, n, d_pat, plen, t, ndefer, nhits, sorted, dev_count);
 }
 
 // The emitted records' counts: cnt held the claimed slot's index.

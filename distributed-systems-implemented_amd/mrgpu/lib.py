@@ -80,6 +80,7 @@ class Stats(ctypes.Structure):
         ("rccl_rank", ctypes.c_int64),
         ("device", ctypes.c_int64),
         ("spill_record_bytes", ctypes.c_uint64),
+        ("shuffle_recv_records", ctypes.c_uint64),
     ]
 
     def as_dict(self):

@@ -108,6 +108,8 @@ typedef struct {
     int64_t rccl_rank;        /* exchange: this context's rank per ncclCommUserRank (-1: none) */
     int64_t device;           /* the HIP device this context drives (ncclCommCuDevice when attached) */
     uint64_t spill_record_bytes; /* wc map: bytes of spill records written (8 per short key, 16 per 9-16-byte key) */
+    uint64_t shuffle_recv_records; /* exchange: wire records this rank received as owner, from every rank
+                                      (its own segment included), before re-aggregation */
 } mrg_stats;
 
 int mrg_open(int device, mrg_ctx** out);

@@ -116,6 +116,49 @@ def _seams(pat: bytes, nseams: int) -> bytes:
     return bytes(b)
 
 
+def grep_seam_lines(pat: bytes = b"distributed") -> bytes:
+    """Matching lines that cross 960-byte map-chunk seams with occurrences on
+    both sides (each chunk keeps its own first hit of the line), lines spanning
+    three or more chunks with a hit in every chunk, the same seam-crossing line
+    several times, lines over 4 KiB (the workgroup resolution path) with hits
+    in many chunks or only far apart, and an occurrence ending exactly at a
+    seam.  Every line occurrence must count once (dgrep.go:30-33)."""
+    rnd = random.Random(77)
+    out = bytearray()
+
+    def pad_to(off):  # filler lines up to input offset off
+        while len(out) < off:
+            k = min(off - len(out), rnd.randint(1, 50))
+            out.extend(b"x" * (k - 1) + b"\n" if k > 1 else b"\n")
+
+    for i in range(1, 60):
+        seam = 960 * (3 * i)
+        pad_to(seam - 200 + (i % 7))
+        kind = i % 6
+        if kind == 0:    # hits just before and just after the seam
+            line = b"a" * (190 - (i % 7) - len(pat)) + pat + b"b" * 5 + pat + b"c" * 20
+        elif kind == 1:  # hit before the seam, hit straddling it
+            line = b"a" * 20 + pat + b"a" * (176 - (i % 7) - 2 * len(pat)) + pat + b"z" * 30
+        elif kind == 2:  # a line over three chunks, a hit in each
+            line = pat + b"m" * 900 + pat + b"m" * 950 + pat + b"m" * 10
+        elif kind == 3:  # hit only after the seam (the line starts in the chunk before)
+            line = b"w" * 250 + pat + b"w" * 3
+        elif kind == 4:  # occurrence ending exactly at the seam, another after it
+            line = b"q" * (200 - (i % 7) - len(pat)) + pat + pat + b"r"
+        else:            # an occurrence straddling the seam only
+            line = b"s" * (200 - (i % 7) - 4) + pat + b"t" * 9
+        out.extend(line + b"\n")
+        if i % 5 == 0:  # the same line again at another seam offset
+            pad_to(960 * (3 * i + 1) - 100)
+            out.extend(line + b"\n")
+    # > 4 KiB lines: hits in many chunks; hits far apart (first near the start)
+    out.extend(b"y" * 37 + b"".join(pat + b"h" * 600 for _ in range(20)) + b"\n")
+    out.extend(pat + b"k" * 9000 + pat + b"k" * 7000 + pat + b"\n")
+    out.extend(b"k" * 6000 + pat + b"\n")
+    out.extend(b"y" * 37 + b"".join(pat + b"h" * 600 for _ in range(20)) + b"\n")  # a repeat
+    return bytes(out)
+
+
 def grep_edge_cases() -> dict[str, tuple[list[bytes], bytes]]:
     return {
         "basic": ([b"a distributed system\nnothing here\ndistributed\n\ndistributed distributed x\n"], b"distributed"),

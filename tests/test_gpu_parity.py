@@ -616,6 +616,59 @@ def test_export_matches_host_codec(ctx):
     assert all(int(pp) == O.c_ihash(k) % 7 for k, pp in zip(d["keys"], d["kpart"]))
 
 
+@pytest.fixture(scope="module")
+def ctx_sorted_hits():
+    """grep with option grep_sort_hits = 1 (hits sorted by position before the
+    line resolution: the round-4 path)."""
+    from mrgpu import Context
+    c = Context(0)
+    c.set_option("grep_sort_hits", 1)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("path", ["default", "sorted"])
+def test_grep_record_counts_one_per_line(ctx, ctx_sorted_hits, path):
+    """The map's grep records count every matching line occurrence exactly once
+    (dgrep.go:30-33 emits one KeyValue per line; mr-X-r holds that many JSON
+    lines): lines crossing chunk seams with hits on both sides, lines over
+    three chunks, > 4 KiB lines with hits in many chunks, every grep edge case.
+    The counts come from mrg_parts_export (mrgpu.intermediate)."""
+    import collections
+
+    import mr_oracle as M
+    from mrgpu import intermediate as I
+    c = ctx if path == "default" else ctx_sorted_hits
+    todo = [("seam_lines", [cases.grep_seam_lines()], b"distributed"),
+            ("seam_lines_e", [cases.grep_seam_lines(b"e")], b"e")]
+    todo += [(k, f, p) for k, (f, p) in cases.grep_edge_cases().items()]
+    for name, files, pat in todo:
+        for f in files:
+            parts = c.map(MRG_APP_GREP, f, pattern=pat, nreduce=5)
+            d = I.decode(c.export(parts))
+            parts.free()
+            got = collections.Counter()
+            for k, n in zip(d["keys"], d["count"]):
+                got[k] += int(n)
+            want = collections.Counter(M.grep_map(f, pat))
+            assert got == want, f"{name}: {sum(got.values())} records vs {sum(want.values())} matching lines"
+
+
+def test_export_json_grep_seam_lines(ctx):
+    """mr-X-r JSON lines of grep on the default path for seam-crossing lines
+    with hits on both sides: one line per matching line occurrence
+    (worker.go:80-92), as the reference map worker writes them."""
+    import mr_oracle as M
+    files = [cases.grep_seam_lines()]
+    R = 4
+    p = ctx.map(MRG_APP_GREP, files[0], pattern=b"distributed", nreduce=R)
+    for r in range(R):
+        got = ctx.export_json(p, r)
+        assert sorted(got.splitlines(keepends=True)) == sorted(
+            M.intermediate_json_lines("grep:distributed", files, R, r)), f"partition {r}"
+    p.free()
+
+
 JSON_GREP_LINES = (b'plain distributed line\n'
                    b'quote " and backslash \\ distributed <b>&amp;</b>\n'
                    b'ctrl \x01\x08\x0c\t\r distributed\n'
