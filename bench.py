@@ -917,6 +917,11 @@ def main():
     torch.cuda.empty_cache()
     scaling = None
     if world > 1 and args.scaling_workload not in ("", "none") and args.scaling_workload != args.workload:
+        if shared and args.scaling_files is None:
+            # a rehearsal: world ranks' C5 splits (2 x 25 GB each, plus their spill
+            # pools) do not fit one device's HBM; shrink them (not a measurement)
+            args.scaling_files = max(2, WORKLOADS[args.scaling_workload]["files"] * ndev // (4 * world))
+            log(f"rehearsal: the {args.scaling_workload} sub-run uses {args.scaling_files} files per split")
         tg = time.time()
         scaling = scaling_subrun(args.scaling_workload, args, rank, world, local, shared, ndev)
         wall.add("scaling_subrun", tg)

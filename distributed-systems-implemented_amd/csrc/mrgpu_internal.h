@@ -314,6 +314,7 @@ void reduce_ws_set_prefix32(ReduceWs*, bool on);
 void reduce_ws_set_own_sort(ReduceWs*, bool on);
 // grep's tied runs ranked per run (default) or all merge-sorted together.
 void reduce_ws_set_tie_rank(ReduceWs*, bool on);
+void reduce_ws_set_grep_bins(ReduceWs*, int v);
 // Sort recs (optionally only partition `only_part`), format "key value\n" lines.
 // Returns 0 or a hipError_t; output in device buffer *d_out (workspace-owned), sizes on host.
 // ascii_keys: every key byte is < 0x80 (the sort key then packs 7 bits per byte).

@@ -65,6 +65,9 @@ struct ReduceWs {
     // grep (16-byte passes): tied runs ordered by rank per run (waves / workgroups)
     // instead of one merge sort of every tied key
     bool tie_rank = true;
+    // grep (every partition): the bucketed sort fused with the output
+    // (grep_bin_reduce); off: the radix passes + tie ranking + line writer
+    int grep_bins = 1;  // 2: the sorting workgroups write the lines themselves
     RadixWs* rx = nullptr;
     ScanWs scan;                   // look-back state of the hand-written scans (mrgpu_scan.h)
 };
@@ -82,6 +85,7 @@ void reduce_ws_set_bin_sort(ReduceWs* w, bool on) { w->bin_sort = on; }
 void reduce_ws_set_prefix32(ReduceWs* w, bool on) { w->prefix32 = on; }
 void reduce_ws_set_own_sort(ReduceWs* w, bool on) { w->own_sort = on; }
 void reduce_ws_set_tie_rank(ReduceWs* w, bool on) { w->tie_rank = on; }
+void reduce_ws_set_grep_bins(ReduceWs* w, int v) { w->grep_bins = v; }
 
 ReduceWs* reduce_ws_new() {
     ReduceWs* w = new ReduceWs();
@@ -624,9 +628,13 @@ constexpr uint32_t kWlLines = 256;  // threads per workgroup
 // (slow into device memory, slower into pinned host memory)
 template <int kApp>
 constexpr uint32_t wl_lines() { return kApp == 1 ? 256u : 128u; }
+// skip (grep_bin_reduce): when *skip is set, a bin was too large for its sort,
+// so perm is incomplete and nothing is written (the caller redoes the reduce)
 template <int kApp>
 __global__ void __launch_bounds__(kWlLines) write_lines_staged_kernel(Recs r, const uint32_t* perm, uint64_t n,
-                                                                        const uint64_t* off, uint8_t* out) {
+                                                                        const uint64_t* off, uint8_t* out,
+                                                                        const unsigned long long* skip) {
+    if (skip && *skip) return;
     constexpr uint32_t kWlBytes = kApp == 1 ? 16384 : 49152;  // C2 lines ~14 B, C3 lines ~120 B
     __shared__ __attribute__((aligned(16))) uint8_t buf[kWlBytes];
     const uint32_t tid = threadIdx.x;
@@ -1383,6 +1391,465 @@ uint64_t reduce_out_bound(const Recs& r, int app) {
 // written there directly by the formatting kernel (its stores cross PCIe at the
 // copy engine's rate, measured 54.8 GB/s, so the write and the transfer overlap
 // and the separate device-to-host copy and its host round trip disappear).
+// ---- grep: bucketed sort fused with the output ---------------------------
+// C3's reduce ended with ~1.45 ms of PCIe: the 78 MB of "L L\n" lines written
+// into pinned host memory by write_lines_staged_kernel, after ~0.8 ms of sort
+// (17 radix passes, the tied runs ranked) in which the link was idle.  Here the
+// lines are cut into bins by rank (sampled splitters over (partition, first key
+// bits), as the wc sample sort: equal keys share a bin, bins are contiguous
+// ranges of the sorted order), each bin's byte offset comes from a scan of the
+// bins' line bytes, and one kernel then sorts each bin in LDS by full bytewise
+// order and writes its lines straight out: workgroups that finish sorting a bin
+// write while others still sort, so the sort runs under the link's time.
+//   gb_key_kernel      key64 = (partition, first 64 - pbits bits of the key)
+//   bin_sample_kernel  splitters (shared with the wc sample sort)
+//   gb_count_kernel    bin per key; per group: keys and line bytes per bin
+//   gb_offsets_kernel  per bin: prefix over the groups, totals (one wave a bin)
+//   gb_starts_kernel   exclusive scans of the bins' keys and bytes
+//   gb_scatter_kernel  record indices grouped by bin
+//   gb_sort_emit_kernel  per bin: LDS bitonic sort (partition, bytes 0-23 from
+//                      registers, then rec_cmp_ext), line offsets, lines out
+//   gb_part_offsets_kernel  partition offsets from the first line of each
+// A bin over kGbCap keys (more than kGbCap lines sharing partition and first
+// key bits, e.g. log lines behind one timestamp) flags flags[1]: the caller
+// redoes the reduce with the radix passes (its output overwrites everything).
+// bins of <= 2048 keys: 512 threads, 104 KB of LDS; of 2049-4096 keys: 1024
+// threads, 152 KB
+constexpr uint32_t kGbThreads = 512, kGbCap = 2048, kGbStage = 32768;
+constexpr uint32_t kGbBigThreads = 1024, kGbBigCap = 4096, kGbBigStage = 12288;
+constexpr uint32_t kGbBinMax = 4096;     // bins at most (count kernel LDS: 112 KB)
+constexpr uint32_t kGbGroups = 128;      // count / scatter workgroups at most
+
+struct GbEnt {
+    uint64_t a, b, c;  // key bytes 0-7, 8-15, 16-23 as big-endian words (zero-padded)
+    uint32_t part, idx;
+};
+
+// Key128 (hi, lo): (partition, the first 128 - pbits key bits), big-endian:
+// lines tie on it about as often as on their first 16 bytes (C3: runs of at
+// most ~1.4 K), where an 8-byte prefix put tens of thousands of lines behind
+// one Zipf-frequent first word into one bin.
+struct Key128 {
+    uint64_t hi, lo;
+};
+__device__ __forceinline__ bool k128_le(const Key128& a, const Key128& b) {
+    return a.hi < b.hi || (a.hi == b.hi && a.lo <= b.lo);
+}
+__device__ __forceinline__ bool k128_gt(const Key128& a, const Key128& b) {
+    return a.hi > b.hi || (a.hi == b.hi && a.lo > b.lo);
+}
+
+__global__ void gb_key_kernel(Recs r, uint32_t pbits, Key128* key) {
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < r.n; i += stride) {
+        const uint64_t A = __builtin_bswap64(r.k0[i]), B = __builtin_bswap64(r.k1[i]);
+        Key128 k;
+        if (pbits) {
+            k.hi = ((uint64_t)r.part[i] << (64 - pbits)) | (A >> pbits);
+            k.lo = (A << (64 - pbits)) | (B >> pbits);
+        } else {
+            k.hi = A;
+            k.lo = B;
+        }
+        key[i] = k;
+    }
+}
+
+// Splitters: one workgroup sorts an evenly spaced sample of S keys in LDS
+// (bitonic) and keeps every (S / nbins)-th.
+constexpr uint32_t kGbSample = 4096;
+__global__ void __launch_bounds__(1024) gb_sample_kernel(const Key128* keys, uint64_t n, uint32_t S, uint32_t nbins,
+                                                         Key128* spl) {
+    __shared__ Key128 K[kGbSample];
+    for (uint32_t i = threadIdx.x; i < S; i += 1024) K[i] = keys[(uint64_t)i * n / S];
+    for (uint32_t k = 2; k <= S; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            __syncthreads();
+            for (uint32_t i = threadIdx.x; i < S / 2; i += 1024) {
+                const uint32_t a = 2 * i - (i & (j - 1)), c = a + j;
+                const Key128 ka = K[a], kc = K[c];
+                if (k128_gt(ka, kc) == ((a & k) == 0)) {
+                    K[a] = kc;
+                    K[c] = ka;
+                }
+            }
+        }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j + 1 < nbins; j += 1024) spl[j] = K[(uint64_t)(j + 1) * S / nbins];
+}
+
+// the number of splitters <= k (nbins - 1 sorted splitters): equal keys share a bin
+__device__ __forceinline__ uint32_t gb_bin_of(const Key128* sp, uint32_t nbins, const Key128& k) {
+    uint32_t lo = 0, cnt = nbins - 1;
+    while (cnt) {
+        const uint32_t half = cnt >> 1;
+        if (k128_le(sp[lo + half], k)) {
+            lo += half + 1;
+            cnt -= half + 1;
+        } else {
+            cnt = half;
+        }
+    }
+    return lo;
+}
+
+__global__ void __launch_bounds__(1024) gb_count_kernel(Recs r, const Key128* key, const Key128* spl,
+                                                        uint32_t nbins, uint16_t* kbin, uint32_t* H,
+                                                        unsigned long long* HB) {
+    __shared__ Key128 sp[kGbBinMax];
+    __shared__ uint32_t h[kGbBinMax];
+    __shared__ unsigned long long hb[kGbBinMax];
+    for (uint32_t i = threadIdx.x; i < nbins; i += 1024) {
+        h[i] = 0;
+        hb[i] = 0;
+        if (i + 1 < nbins) sp[i] = spl[i];
+    }
+    __syncthreads();
+    const uint64_t n = r.n, per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b = (uint64_t)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 1024) {
+        const uint32_t bin = gb_bin_of(sp, nbins, key[i]);
+        kbin[i] = (uint16_t)bin;
+        atomicAdd(&h[bin], 1u);
+        atomicAdd(&hb[bin], 2ull * r.len[i] + 2ull);  // "L L\n" (dgrep.go:44-46, worker.go:144)
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nbins; i += 1024) {
+        H[(uint64_t)blockIdx.x * nbins + i] = h[i];
+        HB[(uint64_t)blockIdx.x * nbins + i] = hb[i];
+    }
+}
+
+// One wave per bin: the prefix over the G groups of its key and byte counts
+// (in place), the totals in tot / btot.
+__global__ void __launch_bounds__(256) gb_offsets_kernel(uint32_t* H, unsigned long long* HB, uint32_t G,
+                                                         uint32_t nbins, uint32_t* tot, unsigned long long* btot) {
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t bin = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    if (bin >= nbins) return;
+    uint32_t run = 0;
+    unsigned long long brun = 0;
+    for (uint32_t g0 = 0; g0 < G; g0 += 64) {
+        const uint32_t g = g0 + lane;
+        const uint64_t at = (uint64_t)g * nbins + bin;
+        const uint32_t v = g < G ? H[at] : 0u;
+        const unsigned long long bv = g < G ? HB[at] : 0ull;
+        const uint64_t iv = wave_incl_scan_u64(v), ib = wave_incl_scan_u64(bv);
+        if (g < G) {
+            H[at] = run + (uint32_t)(iv - v);
+            HB[at] = brun + (ib - bv);
+        }
+        run += (uint32_t)__shfl(iv, 63);
+        brun += __shfl(ib, 63);
+    }
+    if (lane == 0) {
+        tot[bin] = run;
+        btot[bin] = brun;
+    }
+}
+
+// start / bstart = exclusive scans of tot / btot (one workgroup); bstart[nbins]
+// = the output's total bytes
+__global__ void __launch_bounds__(1024) gb_starts_kernel(const uint32_t* tot, const unsigned long long* btot,
+                                                         uint32_t nbins, uint32_t* start,
+                                                         unsigned long long* bstart) {
+    __shared__ unsigned long long pa[1024], pb[1024];
+    const uint32_t per = (nbins + 1023) / 1024, t = threadIdx.x;
+    unsigned long long a = 0, bb = 0;
+    for (uint32_t q = 0; q < per; q++)
+        if (t * per + q < nbins) {
+            a += tot[t * per + q];
+            bb += btot[t * per + q];
+        }
+    pa[t] = a;
+    pb[t] = bb;
+    __syncthreads();
+    for (uint32_t d = 1; d < 1024; d <<= 1) {
+        const unsigned long long x = t >= d ? pa[t - d] : 0ull, y = t >= d ? pb[t - d] : 0ull;
+        __syncthreads();
+        pa[t] += x;
+        pb[t] += y;
+        __syncthreads();
+    }
+    unsigned long long run = pa[t] - a, brun = pb[t] - bb;
+    for (uint32_t q = 0; q < per; q++)
+        if (t * per + q < nbins) {
+            start[t * per + q] = (uint32_t)run;
+            bstart[t * per + q] = brun;
+            run += tot[t * per + q];
+            brun += btot[t * per + q];
+        }
+    if (t == 1023) bstart[nbins] = pb[1023];
+}
+
+__global__ void __launch_bounds__(1024) gb_scatter_kernel(uint64_t n, const uint16_t* kbin, uint32_t nbins,
+                                                          const uint32_t* H, const uint32_t* start, uint32_t* idx) {
+    __shared__ uint32_t cur[kGbBinMax];
+    for (uint32_t i = threadIdx.x; i < nbins; i += 1024) cur[i] = start[i] + H[(uint64_t)blockIdx.x * nbins + i];
+    __syncthreads();
+    const uint64_t per = (n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b = (uint64_t)blockIdx.x * per, e = b + per < n ? b + per : n;
+    for (uint64_t i = b + threadIdx.x; i < e; i += 1024) idx[atomicAdd(&cur[kbin[i]], 1u)] = (uint32_t)i;
+}
+
+// Bytewise order (worker.go:27 ByKey, partition first): bytes 0-23 from the
+// entries, then rec_cmp_ext.  Padding entries (idx ~0) sort last.
+__device__ __forceinline__ bool gb_less(const Recs& r, const uint64_t* ext, const GbEnt& x, const GbEnt& y) {
+    if (x.part != y.part) return x.part < y.part;
+    if (x.a != y.a) return x.a < y.a;
+    if (x.b != y.b) return x.b < y.b;
+    if (x.c != y.c) return x.c < y.c;
+    if (x.idx == ~0u || y.idx == ~0u) return x.idx != ~0u && y.idx == ~0u;
+    return rec_cmp_ext(r, ext, x.idx, y.idx) < 0;
+}
+
+// One output line "L L\n" (grep: the key twice) at o.
+template <class OutPtr>
+__device__ __forceinline__ void gb_emit_line(const Recs& r, uint32_t j, OutPtr o) {
+    const uint32_t len = r.len[j];
+    if (len > 16) {  // arena bytes by aligned 16-byte blocks
+        const uint8_t* kb = r.arena + r.koff[j];
+        for (int64_t q = 0; q < (int64_t)len;) {
+            const uintptr_t a = (uintptr_t)(kb + q), ab = a & ~(uintptr_t)15;
+            const int64_t bi = q - (int64_t)(a - ab);
+            const uint4 v4 = *(const uint4*)ab;
+            const uint32_t w4[4] = {v4.x, v4.y, v4.z, v4.w};
+#pragma unroll
+            for (int bb = 0; bb < 16; bb++) {
+                const int64_t k = bi + bb;
+                if (k < q || k >= (int64_t)len) continue;
+                const uint8_t c = (uint8_t)(w4[bb >> 2] >> (8 * (bb & 3)));
+                o[k] = c;
+                o[len + 1 + k] = c;
+            }
+            q = bi + 16;
+        }
+    } else {
+        const uint64_t k0 = r.k0[j], k1 = r.k1[j];
+        for (uint32_t k = 0; k < len; k++) {
+            const uint8_t c = (uint8_t)((k < 8 ? k0 : k1) >> (8 * (k & 7)));
+            o[k] = c;
+            o[len + 1 + k] = c;
+        }
+    }
+    o[len] = ' ';
+    o[2 * len + 1] = '\n';
+}
+
+// Bins of (lo, CAP] keys; a bin over the big variant's CAP flags flags[1].
+// EMIT: the bin's lines are written here (staged in LDS); else its sorted
+// record indices and global line offsets go to perm_out / off_out for
+// write_lines_staged_kernel.
+template <uint32_t CAP, uint32_t NT, uint32_t STAGE, bool EMIT>
+__global__ void __launch_bounds__(NT) gb_sort_emit_kernel(Recs r, const uint64_t* ext, const uint32_t* idx,
+                                                          const uint32_t* start, const uint32_t* tot,
+                                                          const unsigned long long* bstart, uint32_t nbins,
+                                                          uint32_t lo_keys, bool flag_over, uint8_t* out,
+                                                          uint32_t* perm_out, uint64_t* off_out,
+                                                          unsigned long long* poff, unsigned long long* flags) {
+    __shared__ GbEnt E[CAP];
+    __shared__ uint32_t loff[CAP + 1];  // line offsets inside the bin
+    __shared__ __attribute__((aligned(16))) uint8_t stage[STAGE];
+    __shared__ unsigned long long red[NT / 64];
+    constexpr uint32_t PER = CAP / NT, kGbStage = STAGE;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (uint32_t bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
+        const uint32_t m = tot[bin];
+        if (m <= lo_keys) continue;
+        if (m > CAP) {
+            if (flag_over && tid == 0) atomicOr(&flags[1], 1ull);
+            continue;
+        }
+        uint32_t P = 1;
+        while (P < m) P <<= 1;
+        const uint32_t s0 = start[bin];
+        for (uint32_t i = tid; i < P; i += NT) {
+            GbEnt x;
+            if (i < m) {
+                const uint32_t j = idx[s0 + i];
+                x.a = __builtin_bswap64(r.k0[j]);
+                x.b = __builtin_bswap64(r.k1[j]);
+                x.c = r.len[j] > 16 ? ext[(uint64_t)kExtWords * j] : 0ull;
+                x.part = r.part[j];
+                x.idx = j;
+            } else {
+                x.a = x.b = x.c = ~0ull;
+                x.part = ~0u;
+                x.idx = ~0u;
+            }
+            E[i] = x;
+        }
+        // bitonic network over P entries (swaps of whole entries)
+        for (uint32_t k = 2; k <= P; k <<= 1)
+            for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+                __syncthreads();
+                for (uint32_t i = tid; i < P / 2; i += NT) {
+                    const uint32_t a = 2 * i - (i & (jj - 1)), c = a + jj;
+                    const GbEnt xa = E[a], xc = E[c];
+                    const bool up = (a & k) == 0;
+                    if (gb_less(r, ext, xc, xa) == up) {
+                        E[a] = xc;
+                        E[c] = xa;
+                    }
+                }
+            }
+        __syncthreads();
+        // line offsets in the bin: thread t takes items [PER t, PER t + PER)
+        uint64_t l[PER], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t i = PER * tid + q;
+            l[q] = i < m ? 2ull * r.len[E[i].idx] + 2ull : 0ull;
+            sum += l[q];
+        }
+        const uint64_t incl = wave_incl_scan_u64(sum);
+        if (lane == 63) red[w] = incl;
+        __syncthreads();
+        uint64_t pre = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < NT / 64; q++) pre += q < w ? red[q] : 0ull;
+        uint64_t o = pre + incl - sum;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t i = PER * tid + q;
+            if (i < m) loff[i] = (uint32_t)o;
+            o += l[q];
+        }
+        if (tid == NT - 1) loff[m] = (uint32_t)(pre + incl);  // the bin's byte total
+        __syncthreads();
+        const uint64_t gbase = bstart[bin];
+        // the first line of each partition (partitions are contiguous in the sorted order)
+        for (uint32_t i = tid; i < m; i += NT)
+            if (i == 0 || E[i].part != E[i - 1].part) atomicMin(&poff[E[i].part], gbase + loff[i]);
+        if constexpr (!EMIT) {
+            for (uint32_t i = tid; i < m; i += NT) {
+                perm_out[s0 + i] = E[i].idx;
+                off_out[s0 + i] = gbase + loff[i];
+            }
+            __syncthreads();  // LDS reused by the workgroup's next bin
+            continue;
+        }
+        // lines out, in steps of as many lines as the staging buffer holds
+        for (uint32_t i0 = 0; i0 < m;) {
+            const uint64_t gs = gbase + loff[i0];
+            const uint64_t a0 = gs & ~15ull;
+            // lines [i0, i1): the most (<= NT) whose bytes fit the stage from a0
+            uint32_t lo = i0 + 1, hi = i0 + NT < m ? i0 + NT : m;  // i1 in [lo, hi]
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi + 1) >> 1;
+                if (gbase + loff[mid] - a0 <= kGbStage) lo = mid;
+                else hi = mid - 1;
+            }
+            const uint32_t i1 = lo;
+            const uint64_t ge = gbase + loff[i1];
+            const bool staged = ge - a0 <= kGbStage;  // (false: one line longer than the stage)
+            const uint32_t i = i0 + tid;
+            if (i < i1) {
+                const uint64_t go = gbase + loff[i];
+                if (staged) gb_emit_line(r, E[i].idx, stage + (go - a0));
+                else gb_emit_line(r, E[i].idx, out + go);
+            }
+            if (staged) {
+                __syncthreads();
+                const uint32_t nq = (uint32_t)((ge - a0 + 15) / 16);
+                for (uint32_t q = tid; q < nq; q += NT) {
+                    const uint64_t ga = a0 + 16ull * q;
+                    if (ga >= gs && ga + 16 <= ge) {
+                        *(uint4*)(out + ga) = *(const uint4*)(stage + 16 * q);
+                    } else {
+                        for (uint32_t bb = 0; bb < 16; bb++)
+                            if (ga + bb >= gs && ga + bb < ge) out[ga + bb] = stage[16 * q + bb];
+                    }
+                }
+            }
+            __syncthreads();
+            i0 = i1;
+        }
+    }
+}
+
+__global__ void gb_total_kernel(const unsigned long long* total, uint64_t* off_n) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *off_n = *total;
+}
+
+// offsets[p] = byte offset of partition p's first line (the next non-empty
+// partition's, or the total, when p has none); offsets[nparts] = the total.
+__global__ void gb_part_offsets_kernel(const unsigned long long* poff, const unsigned long long* total, uint32_t nparts,
+                                       uint64_t* offsets) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    uint64_t next = *total;
+    offsets[nparts] = next;
+    for (uint32_t p = nparts; p-- > 0;) {
+        if (poff[p] != ~0ull) next = poff[p];
+        offsets[p] = next;
+    }
+}
+
+// The fused grep reduce; returns 0, or a HIP error.  *over = a bin was too
+// large (nothing usable was written: the caller runs the radix path).
+static int grep_bin_reduce(ReduceWs* ws, const Recs& r, uint32_t nreduce, uint8_t* out, uint64_t* h_offsets,
+                           bool* over, bool emit, hipStream_t s) {
+    const uint64_t n = r.n;
+    uint32_t pbits = 0;
+    while (nreduce > 1 && (1ull << pbits) < nreduce) pbits++;
+    uint32_t nbins = 1;
+    while (nbins < kGbBinMax && (uint64_t)nbins * 256 < n) nbins <<= 1;
+    uint32_t S = 4 * nbins;
+    if (S > kGbSample) S = kGbSample;
+    while (S > n && S > 2) S >>= 1;
+    const uint32_t G = (uint32_t)std::min<uint64_t>(kGbGroups, (n + 4095) / 4096);
+    // scratch: key64 (key_b), idx (perm_a); bins: H, HB, tot, btot, start, bstart, spl, kbin, poff
+    const size_t hb = (size_t)G * nbins * 4, hbb = (size_t)G * nbins * 8;
+    const size_t need = hbb + hb + (size_t)nbins * (4 + 8 + 4 + 8 + 16) + 8 + n * 2 + 16 + (size_t)(nreduce + 1) * 8 + 256;
+    RCHK(ws->bins.ensure(need));
+    uint8_t* p8 = ws->bins.as<uint8_t>();
+    unsigned long long* HB = (unsigned long long*)p8;            p8 += hbb;
+    unsigned long long* btot = (unsigned long long*)p8;          p8 += (size_t)nbins * 8;
+    unsigned long long* bstart = (unsigned long long*)p8;        p8 += (size_t)nbins * 8 + 8;
+    Key128* spl = (Key128*)p8;                                    p8 += (size_t)nbins * 16;
+    unsigned long long* poff = (unsigned long long*)p8;          p8 += (size_t)(nreduce + 1) * 8;
+    uint32_t* H = (uint32_t*)p8;                                  p8 += hb;
+    uint32_t* tot = (uint32_t*)p8;                                p8 += (size_t)nbins * 4;
+    uint32_t* start = (uint32_t*)p8;                              p8 += (size_t)nbins * 4;
+    uint16_t* kbin = (uint16_t*)p8;
+    Key128* key = ws->ext.as<Key128>() + (size_t)n * kExtWords / 2;  // (ext holds n x kExtWords words, then these)
+    uint32_t* idx = ws->perm_a.as<uint32_t>();
+    unsigned long long* flags = ws->flags.as<unsigned long long>();
+    const uint32_t nparts = nreduce;
+    RCHK(hipMemsetAsync(poff, 0xFF, (size_t)nparts * 8, s));
+    gb_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pbits, key);
+    gb_sample_kernel<<<1, 1024, 0, s>>>(key, n, S, nbins, spl);
+    gb_count_kernel<<<G, 1024, 0, s>>>(r, key, spl, nbins, kbin, H, HB);
+    gb_offsets_kernel<<<(nbins + 3) / 4, 256, 0, s>>>(H, HB, G, nbins, tot, btot);
+    gb_starts_kernel<<<1, 1024, 0, s>>>(tot, btot, nbins, start, bstart);
+    gb_scatter_kernel<<<G, 1024, 0, s>>>(n, kbin, nbins, H, start, idx);
+    uint32_t* perm = ws->perm_b.as<uint32_t>();
+    uint64_t* off = ws->lineoff.as<uint64_t>();
+    const uint64_t* ext = ws->ext.as<uint64_t>();
+    if (emit) {  // (option grep_bins = 2: the lines written by the sorting workgroups)
+        gb_sort_emit_kernel<kGbCap, kGbThreads, kGbStage, true><<<nbins < 512 ? nbins : 512, kGbThreads, 0, s>>>(
+            r, ext, idx, start, tot, bstart, nbins, 0, false, out, perm, off, poff, flags);
+        gb_sort_emit_kernel<kGbBigCap, kGbBigThreads, kGbBigStage, true><<<nbins < 256 ? nbins : 256, kGbBigThreads, 0,
+                                                                          s>>>(
+            r, ext, idx, start, tot, bstart, nbins, kGbCap, true, out, perm, off, poff, flags);
+    } else {  // sorted order + line offsets, then the line writer over all of them
+        gb_sort_emit_kernel<kGbCap, kGbThreads, 16, false><<<nbins < 512 ? nbins : 512, kGbThreads, 0, s>>>(
+            r, ext, idx, start, tot, bstart, nbins, 0, false, out, perm, off, poff, flags);
+        gb_sort_emit_kernel<kGbBigCap, kGbBigThreads, 16, false><<<nbins < 256 ? nbins : 256, kGbBigThreads, 0, s>>>(
+            r, ext, idx, start, tot, bstart, nbins, kGbCap, true, out, perm, off, poff, flags);
+        gb_total_kernel<<<1, 64, 0, s>>>(bstart + nbins, off + n);
+        const unsigned g = (unsigned)std::min<uint64_t>((n + wl_lines<2>() - 1) / wl_lines<2>(), 8192);
+        write_lines_staged_kernel<2><<<g, kWlLines, 0, s>>>(r, perm, n, off, out, flags + 1);
+    }
+    gb_part_offsets_kernel<<<1, 64, 0, s>>>(poff, bstart + nbins, nparts, ws->offs.as<uint64_t>());
+    RCHK(hipGetLastError());
+    RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
+    RCHK(hipMemcpyAsync(ws->h_pinned + 1, flags + 1, 8, hipMemcpyDeviceToHost, s));
+    RCHK(hipStreamSynchronize(s));
+    *over = ws->h_pinned[1] != 0;
+    return 0;
+}
+
 int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32_t only_part, uint8_t** d_out,
                   uint64_t* out_n, uint64_t* h_offsets, hipStream_t s, bool ascii_keys, uint8_t* hout, uint64_t hout_cap) {
     const uint64_t n = r.n;
@@ -1422,9 +1889,22 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     radix_ws_set_digit_bits(ws->rx, ws->digit_bits);
     const uint64_t* ext = nullptr;
     if (grep) {
-        RCHK(ws->ext.ensure(n * 8 * kExtWords));
+        RCHK(ws->ext.ensure(n * 8 * kExtWords + n * 16 + 16));  // (+ grep_bin_reduce's 16-byte keys)
         ext_words_kernel<<<grid_for(n), 256, 0, s>>>(r, ws->ext.as<uint64_t>());
         ext = ws->ext.as<uint64_t>();
+    }
+    // grep, every partition: the bucketed sort fused with the output (above);
+    // the radix path below only when a bin was too large
+    if (grep && all && ws->grep_bins && n <= 0xFFFFFFFFull) {
+        bool over = false;
+        uint8_t* o = to_host ? hout : ws->out.as<uint8_t>();
+        if (int e = grep_bin_reduce(ws, r, nreduce, o, h_offsets, &over, ws->grep_bins == 2, s)) return e;
+        if (!over) {
+            *d_out = o;
+            *out_n = h_offsets[nparts];
+            return 0;
+        }
+        RCHK(hipMemsetAsync(flags, 0, 32, s));
     }
     auto pass32 = [&](int which, unsigned bits) -> int {
         gather_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pa, n, which, nullptr, ws->key_a.as<uint32_t>());
@@ -1546,10 +2026,10 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         else line_offsets_kernel<1><<<(unsigned)ntiles, kScanThreads, 0, s>>>(r, pa, n, off, st);
         if (app != 1) {
             const unsigned g = (unsigned)std::min<uint64_t>((n + wl_lines<2>() - 1) / wl_lines<2>(), 8192);
-            write_lines_staged_kernel<2><<<g, kWlLines, 0, s>>>(r, pa, n, off, out);
+            write_lines_staged_kernel<2><<<g, kWlLines, 0, s>>>(r, pa, n, off, out, nullptr);
         } else {
             const unsigned g = (unsigned)std::min<uint64_t>((n + wl_lines<1>() - 1) / wl_lines<1>(), 8192);
-            write_lines_staged_kernel<1><<<g, kWlLines, 0, s>>>(r, pa, n, off, out);
+            write_lines_staged_kernel<1><<<g, kWlLines, 0, s>>>(r, pa, n, off, out, nullptr);
         }
         part_offsets_kernel<<<(nparts + 1 + 255) / 256, 256, 0, s>>>(r, pa, n, off, nparts, !all, ws->offs.as<uint64_t>());
         RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));

@@ -236,7 +236,10 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        60/64 bits instead of the top 32), own_sort (kept
  *                                        for compatibility: every value runs the hand-written
  *                                        LSD passes), tie_rank (0: grep's tied runs
- *                                        merge-sorted together instead of ranked per run)
+ *                                        merge-sorted together instead of ranked per run),
+ *                                        grep_bins (0: grep's reduce by the radix passes +
+ *                                        tie ranking + line writer instead of the bucketed
+ *                                        sort fused with the output)
  *                                        reduce sort variants
  *   grep_literal (1: on)                 grep patterns with regexp metacharacters matched as
  *                                        literals (QuoteMeta) instead of refused with MRG_EINVAL
@@ -250,7 +253,9 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *   grep_sort_hits (1: on)               grep: the hits sorted by position before the line
  *                                        resolution (default: the map kernel's order, counts
  *                                        read on the device, sizes speculated from the
- *                                        previous split and checked once after the insert)
+ *                                        previous split and checked once after the insert;
+ *                                        either way a line occurrence is resolved once, so a
+ *                                        record's count = the line's occurrences)
  *   grep_emit (0: off)                   grep: each distinct line's record written by the
  *                                        LongTable insert that claims it (default) instead
  *                                        of a collect pass over the table */

@@ -627,6 +627,53 @@ def ctx_sorted_hits():
     c.close()
 
 
+@pytest.fixture(scope="module")
+def ctx_grep_radix():
+    """grep reduce by the radix passes + tie ranking + line writer (option
+    grep_bins = 0; the default is the bucketed sort fused with the output)."""
+    from mrgpu import Context
+    c = Context(0)
+    c.set_option("grep_bins", 0)
+    yield c
+    c.close()
+
+
+@pytest.mark.parametrize("name", ["basic", "tied_lines", "long_lines_many_hits", "chunk_seams", "overlapping",
+                                  "prefix5_utf8"])
+def test_grep_edge_cases_radix_reduce(ctx_grep_radix, name):
+    files, pat = cases.grep_edge_cases()[name]
+    check(ctx_grep_radix, "grep:" + pat.decode("utf-8", "surrogateescape"), files, nreduces=(1, 10))
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_grep_bins_many_lines(mode):
+    """The bucketed grep reduce over ~10^5 distinct matching lines (hundreds of
+    bins, partitions R = 1 / 10 / 64 / 1000, some empty), tied 16-byte prefixes,
+    lines of 1-3000 bytes, against the oracle; mode 1 (default): bins sorted,
+    then the line writer; mode 2: the sorting workgroups write the lines."""
+    import random
+    from mrgpu import Context
+    rnd = random.Random(5)
+    lines = []
+    for i in range(120_000):
+        k = rnd.random()
+        if k < 0.3:    # shared 24-byte prefix: ties past the entries' first 24 bytes
+            lines.append(b"distributed systems are h" + str(rnd.randrange(10**6)).encode())
+        elif k < 0.35:  # long lines
+            lines.append(b"x" * rnd.randrange(100, 3000) + b"distributed" + str(i).encode())
+        else:
+            lines.append(bytes(rnd.choice(b"abcdefgh ") for _ in range(rnd.randrange(0, 40))) + b"distributed"
+                         + bytes(rnd.choice(b"xyz") for _ in range(rnd.randrange(0, 8))))
+    data = b"\n".join(lines) + b"\n"
+    with Context(0) as c:
+        c.set_option("grep_bins", mode)
+        check(c, "grep:distributed", [data], nreduces=(1, 10, 64, 1000))
+        # a Zipf-frequent first word: > 4096 lines share their first 8 bytes
+        # (one bin per 128-bit key prefix, not per 8-byte one)
+        many = b"".join(b"fzlsGaIu distributed %07d\n" % rnd.randrange(10**7) for _ in range(20000))
+        check(c, "grep:distributed", [many], nreduces=(1, 10))
+
+
 @pytest.mark.parametrize("path", ["default", "sorted"])
 def test_grep_record_counts_one_per_line(ctx, ctx_sorted_hits, path):
     """The map's grep records count every matching line occurrence exactly once
