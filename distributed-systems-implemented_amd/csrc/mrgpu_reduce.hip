@@ -67,7 +67,7 @@ struct ReduceWs {
     bool tie_rank = true;
     // grep (every partition): the bucketed sort fused with the output
     // (grep_bin_reduce); off: the radix passes + tie ranking + line writer
-    int grep_bins = 1;  // 2: the sorting workgroups write the lines themselves
+    int grep_bins = 1;  // 1: the sorting workgroups write the lines; 2: sorted order, then the line writer
     RadixWs* rx = nullptr;
     ScanWs scan;                   // look-back state of the hand-written scans (mrgpu_scan.h)
 };
@@ -1413,9 +1413,9 @@ uint64_t reduce_out_bound(const Recs& r, int app) {
 // A bin over kGbCap keys (more than kGbCap lines sharing partition and first
 // key bits, e.g. log lines behind one timestamp) flags flags[1]: the caller
 // redoes the reduce with the radix passes (its output overwrites everything).
-// bins of <= 2048 keys: 512 threads, 104 KB of LDS; of 2049-4096 keys: 1024
-// threads, 152 KB
-constexpr uint32_t kGbThreads = 512, kGbCap = 2048, kGbStage = 32768;
+// bins of 2049-4096 keys (gbx_sort_emit_kernel takes the smaller ones): 1024
+// threads, 152 KB of LDS, tied keys compared through rec_cmp_ext
+constexpr uint32_t kGbCap = 2048;
 constexpr uint32_t kGbBigThreads = 1024, kGbBigCap = 4096, kGbBigStage = 12288;
 constexpr uint32_t kGbBinMax = 4096;     // bins at most (count kernel LDS: 112 KB)
 constexpr uint32_t kGbGroups = 128;      // count / scatter workgroups at most
@@ -1457,7 +1457,14 @@ __global__ void gb_key_kernel(Recs r, uint32_t pbits, Key128* key) {
 
 // Splitters: one workgroup sorts an evenly spaced sample of S keys in LDS
 // (bitonic) and keeps every (S / nbins)-th.
-constexpr uint32_t kGbSample = 4096;
+#ifndef MRG_GB_SAMPLE
+#define MRG_GB_SAMPLE 8192
+#endif
+#ifndef MRG_GB_PER_BIN
+#define MRG_GB_PER_BIN 256
+#endif
+constexpr uint32_t kGbSample = MRG_GB_SAMPLE;  // (A/B: 4096 cost 70 us, 8192 ~140 us)
+constexpr uint32_t kGbPerBin = MRG_GB_PER_BIN;  // mean keys a bin
 __global__ void __launch_bounds__(1024) gb_sample_kernel(const Key128* keys, uint64_t n, uint32_t S, uint32_t nbins,
                                                          Key128* spl) {
     __shared__ Key128 K[kGbSample];
@@ -1768,6 +1775,177 @@ __global__ void __launch_bounds__(NT) gb_sort_emit_kernel(Recs r, const uint64_t
     }
 }
 
+// Bins of at most kGbxCap keys (nearly all of them): gb_sort_emit_kernel with
+// every compared word in LDS.  An entry holds key bytes 0-23 and the bin-local
+// slot of its record; the slot's key bytes 24-63 (ext words 1-5), length and
+// record index sit in LDS beside the entries, so lines tied on their first 24
+// bytes (C3: lines behind a Zipf-frequent first word and the pattern) compare
+// without a global load; only keys equal in their first 64 bytes read the
+// arena.  (The first version compared ties through rec_cmp_ext in global
+// memory: its per-bin sorts took ~0.5 ms of C3's reduce in total.)
+constexpr uint32_t kGbxCap = 2048, kGbxThreads = 1024, kGbxStage = 16384;
+constexpr uint32_t kGbxWords = 3;  // ext words 1-3 (key bytes 24-47) in LDS; 4-5 read from ext when tied
+struct GbxEnt {
+    uint64_t a, b, c;  // key bytes 0-7, 8-15, 16-23, big-endian words (zero-padded)
+    uint32_t part, slot;
+};
+
+template <bool EMIT>
+__global__ void __launch_bounds__(kGbxThreads) gbx_sort_emit_kernel(Recs r, const uint64_t* ext, const uint32_t* idx,
+                                                                     const uint32_t* start, const uint32_t* tot,
+                                                                     const unsigned long long* bstart, uint32_t nbins,
+                                                                     uint8_t* out, uint32_t* perm_out,
+                                                                     uint64_t* off_out, unsigned long long* poff) {
+    constexpr uint32_t CAP = kGbxCap, NT = kGbxThreads, PER = CAP / NT, NX = kGbxWords;
+    __shared__ GbxEnt E[CAP];
+    __shared__ uint64_t X[CAP * NX];  // key bytes 24-63 of slot s at X[NX s, NX s + NX)
+    __shared__ uint32_t LEN[CAP], IDX[CAP];
+    __shared__ uint32_t loff[CAP + 1];
+    __shared__ __attribute__((aligned(16))) uint8_t stage[EMIT ? kGbxStage : 16];
+    __shared__ unsigned long long red[NT / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    // bytewise order (worker.go:27 ByKey, partition first), exactly rec_cmp_ext's
+    auto less = [&](const GbxEnt& x, const GbxEnt& y) -> bool {
+        if (x.part != y.part) return x.part < y.part;
+        if (x.a != y.a) return x.a < y.a;
+        if (x.b != y.b) return x.b < y.b;
+        if (x.c != y.c) return x.c < y.c;
+        if (x.slot == ~0u || y.slot == ~0u) return x.slot != ~0u && y.slot == ~0u;  // padding last
+#pragma unroll
+        for (uint32_t q = 0; q < NX; q++) {
+            const uint64_t ex = X[NX * x.slot + q], ey = X[NX * y.slot + q];
+            if (ex != ey) return ex < ey;
+        }
+        const uint32_t ia = IDX[x.slot], ib = IDX[y.slot];
+#pragma unroll
+        for (uint32_t q = 1 + NX; q < (uint32_t)kExtWords; q++) {  // (tied through byte 47: rare)
+            const uint64_t ex = ext[(uint64_t)kExtWords * ia + q], ey = ext[(uint64_t)kExtWords * ib + q];
+            if (ex != ey) return ex < ey;
+        }
+        constexpr uint32_t kCovered = 16 + 8 * kExtWords;
+        const uint32_t la = LEN[x.slot], lb = LEN[y.slot];
+        if (la > kCovered && lb > kCovered) {
+            const uint8_t* pa = r.arena + r.koff[ia];
+            const uint8_t* pb = r.arena + r.koff[ib];
+            const uint32_t mx = la > lb ? la : lb;
+            for (uint32_t pos = kCovered; pos < mx; pos += 8) {
+                const uint64_t wa = key_word_be(pa, pos, la), wb = key_word_be(pb, pos, lb);
+                if (wa != wb) return wa < wb;
+            }
+        }
+        return la < lb;
+    };
+    for (uint32_t bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
+        const uint32_t m = tot[bin];
+        if (m == 0 || m > CAP) continue;  // (larger bins: gb_sort_emit_kernel)
+        uint32_t P = 1;
+        while (P < m) P <<= 1;
+        const uint32_t s0 = start[bin];
+        for (uint32_t i = tid; i < P; i += NT) {
+            GbxEnt x;
+            if (i < m) {
+                const uint32_t j = idx[s0 + i];
+                const uint64_t* e = ext + (uint64_t)kExtWords * j;
+                x.a = __builtin_bswap64(r.k0[j]);
+                x.b = __builtin_bswap64(r.k1[j]);
+                x.c = e[0];  // (zero for keys of <= 16 bytes: ext_words_kernel)
+#pragma unroll
+                for (uint32_t q = 0; q < NX; q++) X[NX * i + q] = e[1 + q];
+                x.part = r.part[j];
+                x.slot = i;
+                LEN[i] = r.len[j];
+                IDX[i] = j;
+            } else {
+                x.a = x.b = x.c = ~0ull;
+                x.part = ~0u;
+                x.slot = ~0u;
+            }
+            E[i] = x;
+        }
+        for (uint32_t k = 2; k <= P; k <<= 1)
+            for (uint32_t jj = k >> 1; jj > 0; jj >>= 1) {
+                __syncthreads();
+                for (uint32_t i = tid; i < P / 2; i += NT) {
+                    const uint32_t a = 2 * i - (i & (jj - 1)), c = a + jj;
+                    const GbxEnt xa = E[a], xc = E[c];
+                    if (less(xc, xa) == ((a & k) == 0)) {
+                        E[a] = xc;
+                        E[c] = xa;
+                    }
+                }
+            }
+        __syncthreads();
+        uint64_t l[PER], sum = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t i = PER * tid + q;
+            l[q] = i < m ? 2ull * LEN[E[i].slot] + 2ull : 0ull;
+            sum += l[q];
+        }
+        const uint64_t incl = wave_incl_scan_u64(sum);
+        if (lane == 63) red[w] = incl;
+        __syncthreads();
+        uint64_t pre = 0;
+#pragma unroll
+        for (uint32_t q = 0; q < NT / 64; q++) pre += q < w ? red[q] : 0ull;
+        uint64_t o = pre + incl - sum;
+#pragma unroll
+        for (uint32_t q = 0; q < PER; q++) {
+            const uint32_t i = PER * tid + q;
+            if (i < m) loff[i] = (uint32_t)o;
+            o += l[q];
+        }
+        if (tid == NT - 1) loff[m] = (uint32_t)(pre + incl);
+        __syncthreads();
+        const uint64_t gbase = bstart[bin];
+        for (uint32_t i = tid; i < m; i += NT)
+            if (i == 0 || E[i].part != E[i - 1].part) atomicMin(&poff[E[i].part], gbase + loff[i]);
+        if constexpr (!EMIT) {
+            for (uint32_t i = tid; i < m; i += NT) {
+                perm_out[s0 + i] = IDX[E[i].slot];
+                off_out[s0 + i] = gbase + loff[i];
+            }
+        } else {
+            for (uint32_t i0 = 0; i0 < m;) {
+                const uint64_t gs = gbase + loff[i0];
+                const uint64_t a0 = gs & ~15ull;
+                uint32_t lo = i0 + 1, hi = i0 + NT < m ? i0 + NT : m;
+                while (lo < hi) {
+                    const uint32_t mid = (lo + hi + 1) >> 1;
+                    if (gbase + loff[mid] - a0 <= kGbxStage) lo = mid;
+                    else hi = mid - 1;
+                }
+                const uint32_t i1 = lo;
+                const uint64_t ge = gbase + loff[i1];
+                const bool staged = ge - a0 <= kGbxStage;
+                const uint32_t i = i0 + tid;
+                if (i < i1) {
+                    const uint64_t go = gbase + loff[i];
+                    const uint32_t j = IDX[E[i].slot];
+                    if (staged) gb_emit_line(r, j, stage + (go - a0));
+                    else gb_emit_line(r, j, out + go);
+                }
+                if (staged) {
+                    __syncthreads();
+                    const uint32_t nq = (uint32_t)((ge - a0 + 15) / 16);
+                    for (uint32_t q = tid; q < nq; q += NT) {
+                        const uint64_t ga = a0 + 16ull * q;
+                        if (ga >= gs && ga + 16 <= ge) {
+                            *(uint4*)(out + ga) = *(const uint4*)(stage + 16 * q);
+                        } else {
+                            for (uint32_t bb = 0; bb < 16; bb++)
+                                if (ga + bb >= gs && ga + bb < ge) out[ga + bb] = stage[16 * q + bb];
+                        }
+                    }
+                }
+                __syncthreads();
+                i0 = i1;
+            }
+        }
+        __syncthreads();  // LDS reused by the workgroup's next bin
+    }
+}
+
 __global__ void gb_total_kernel(const unsigned long long* total, uint64_t* off_n) {
     if (blockIdx.x == 0 && threadIdx.x == 0) *off_n = *total;
 }
@@ -1792,9 +1970,11 @@ static int grep_bin_reduce(ReduceWs* ws, const Recs& r, uint32_t nreduce, uint8_
     const uint64_t n = r.n;
     uint32_t pbits = 0;
     while (nreduce > 1 && (1ull << pbits) < nreduce) pbits++;
+    // ~512 keys a bin on average and >= 4 samples a bin (bins cut by sampled
+    // rank: fewer samples a bin spread the sizes past kGbxCap)
     uint32_t nbins = 1;
-    while (nbins < kGbBinMax && (uint64_t)nbins * 256 < n) nbins <<= 1;
-    uint32_t S = 4 * nbins;
+    while (nbins < kGbBinMax && (uint64_t)nbins * kGbPerBin < n) nbins <<= 1;
+    uint32_t S = 8 * nbins;
     if (S > kGbSample) S = kGbSample;
     while (S > n && S > 2) S >>= 1;
     const uint32_t G = (uint32_t)std::min<uint64_t>(kGbGroups, (n + 4095) / 4096);
@@ -1826,15 +2006,15 @@ static int grep_bin_reduce(ReduceWs* ws, const Recs& r, uint32_t nreduce, uint8_
     uint32_t* perm = ws->perm_b.as<uint32_t>();
     uint64_t* off = ws->lineoff.as<uint64_t>();
     const uint64_t* ext = ws->ext.as<uint64_t>();
-    if (emit) {  // (option grep_bins = 2: the lines written by the sorting workgroups)
-        gb_sort_emit_kernel<kGbCap, kGbThreads, kGbStage, true><<<nbins < 512 ? nbins : 512, kGbThreads, 0, s>>>(
-            r, ext, idx, start, tot, bstart, nbins, 0, false, out, perm, off, poff, flags);
+    if (emit) {  // the lines written by the sorting workgroups
+        gbx_sort_emit_kernel<true><<<nbins < 256 ? nbins : 256, kGbxThreads, 0, s>>>(r, ext, idx, start, tot, bstart,
+                                                                                   nbins, out, perm, off, poff);
         gb_sort_emit_kernel<kGbBigCap, kGbBigThreads, kGbBigStage, true><<<nbins < 256 ? nbins : 256, kGbBigThreads, 0,
                                                                           s>>>(
             r, ext, idx, start, tot, bstart, nbins, kGbCap, true, out, perm, off, poff, flags);
     } else {  // sorted order + line offsets, then the line writer over all of them
-        gb_sort_emit_kernel<kGbCap, kGbThreads, 16, false><<<nbins < 512 ? nbins : 512, kGbThreads, 0, s>>>(
-            r, ext, idx, start, tot, bstart, nbins, 0, false, out, perm, off, poff, flags);
+        gbx_sort_emit_kernel<false><<<nbins < 256 ? nbins : 256, kGbxThreads, 0, s>>>(r, ext, idx, start, tot, bstart,
+                                                                                    nbins, out, perm, off, poff);
         gb_sort_emit_kernel<kGbBigCap, kGbBigThreads, 16, false><<<nbins < 256 ? nbins : 256, kGbBigThreads, 0, s>>>(
             r, ext, idx, start, tot, bstart, nbins, kGbCap, true, out, perm, off, poff, flags);
         gb_total_kernel<<<1, 64, 0, s>>>(bstart + nbins, off + n);
@@ -1898,7 +2078,7 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
     if (grep && all && ws->grep_bins && n <= 0xFFFFFFFFull) {
         bool over = false;
         uint8_t* o = to_host ? hout : ws->out.as<uint8_t>();
-        if (int e = grep_bin_reduce(ws, r, nreduce, o, h_offsets, &over, ws->grep_bins == 2, s)) return e;
+        if (int e = grep_bin_reduce(ws, r, nreduce, o, h_offsets, &over, ws->grep_bins != 2, s)) return e;
         if (!over) {
             *d_out = o;
             *out_n = h_offsets[nparts];
