@@ -333,11 +333,6 @@ constexpr uint32_t kLongReserve = 256;
 #define MRG_STAGE2_DRAIN 1
 #endif
 constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
-// dictionary lookups: both sets read at once (0) or the second only on a
-// first-set miss (1: A/B variant)
-#ifndef MRG_DICT_LAZY
-#define MRG_DICT_LAZY 0
-#endif
 // UTF-8 chunks: leads decoded wave-compacted (utf8_mask16_wave) or by the
 // per-lane loop (utf8_mask16)
 #ifndef MRG_UTF8_WAVE
@@ -790,28 +785,6 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     if (use_dict) {
                         u32x4 A[kBatch], B[kBatch];
                         uint32_t a1[kBatch], a2[kBatch];  // byte offsets of the two sets
-#if MRG_DICT_LAZY
-                        // (A/B variant) the second set read only by lanes whose key is not
-                        // in its first set: fewer LDS lanes, one more round trip
-        #pragma unroll
-                        for (int u = 0; u < kBatch; u++) {
-                            dict_set_addrs<Geo>(hh[u], __builtin_amdgcn_inverse_ballot_w64(mMid[u]), a1[u], a2[u]);
-                            A[u] = *(const lds_uint4*)((const lds_u8*)dset + a1[u]);
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-        #pragma unroll
-                        for (int u = 0; u < kBatch; u++) {
-                            const bool mid = __builtin_amdgcn_inverse_ballot_w64(mMid[u]);
-                            const uint64_t kk = mid ? k1[u] : k0[u];
-                            const uint64_t alo = ((uint64_t)A[u].y << 32) | A[u].x, ahi = ((uint64_t)A[u].w << 32) | A[u].z;
-                            const uint64_t mA0 = __ballot(alo == k0[u]), mA1 = __ballot(ahi == kk);
-                            const uint64_t mHa = (mA0 & mA1) | (~mMid[u] & (mA0 | mA1));
-                            u32x4 b = {0u, 0u, 0u, 0u};  // (zero never equals a key: letters are nonzero)
-                            if (__builtin_amdgcn_inverse_ballot_w64(mOk[u] & ~mHa)) b = *(const lds_uint4*)((const lds_u8*)dset + a2[u]);
-                            B[u] = b;
-                        }
-                        __builtin_amdgcn_sched_barrier(0);
-#else
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
                             dict_set_addrs<Geo>(hh[u], __builtin_amdgcn_inverse_ballot_w64(mMid[u]), a1[u], a2[u]);
@@ -819,7 +792,6 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             B[u] = *(const lds_uint4*)((const lds_u8*)dset + a2[u]);
                         }
                         __builtin_amdgcn_sched_barrier(0);  // all 2 * kBatch set reads in flight before the compares
-#endif
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
                             // short key: any of the 4 ways of its two sets; mid key: the single
