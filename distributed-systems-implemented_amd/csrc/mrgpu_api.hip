@@ -1502,7 +1502,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
         c->lrec_cap = v > 0 ? (uint32_t)std::min<int64_t>(v, 1 << 22) : 1024u;
     } else if (!strcmp(name, "grep_literal")) {  // grep: metacharacters quoted (1) instead of refused (0)
         c->grep_literal = v > 0;
-    } else if (!strcmp(name, "grep_bins")) {  // grep reduce: bucketed sort fused with the output (1, default) or radix passes (0)
+    } else if (!strcmp(name, "grep_bins")) {  // grep reduce path (include/mrgpu.h)
         reduce_ws_set_grep_bins(c->rws, (int)v);
     } else if (!strcmp(name, "tie_rank")) {  // grep reduce: tied runs ranked per run (1, default) or merge-sorted (0)
         reduce_ws_set_tie_rank(c->rws, v != 0);

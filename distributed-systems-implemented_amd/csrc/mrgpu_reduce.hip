@@ -67,7 +67,7 @@ struct ReduceWs {
     bool tie_rank = true;
     // grep (every partition): the bucketed sort fused with the output
     // (grep_bin_reduce); off: the radix passes + tie ranking + line writer
-    int grep_bins = 1;  // 1: the sorting workgroups write the lines; 2: sorted order, then the line writer
+    int grep_bins = 1;  // see reduce_format
     RadixWs* rx = nullptr;
     ScanWs scan;                   // look-back state of the hand-written scans (mrgpu_scan.h)
 };
@@ -2073,9 +2073,16 @@ int reduce_format(ReduceWs* ws, const Recs& r, int app, uint32_t nreduce, uint32
         ext_words_kernel<<<grid_for(n), 256, 0, s>>>(r, ws->ext.as<uint64_t>());
         ext = ws->ext.as<uint64_t>();
     }
-    // grep, every partition: the bucketed sort fused with the output (above);
-    // the radix path below only when a bin was too large
-    if (grep && all && ws->grep_bins && n <= 0xFFFFFFFFull) {
+    // grep, every partition, lines written into pinned host memory: the
+    // bucketed sort fused with the output (above), whose sorting runs under the
+    // PCIe time; the radix path below when a bin was too large, and for a device
+    // output buffer (mrg_run_job_async: the transfer overlaps the next job on
+    // another stream, and with nothing to hide under, the bin sorts measured
+    // slower than the radix passes: C3 pipelined 2557 vs 2664 GB/s)
+    // (grep_bins: 0 radix path; 1 bins fused with the output into host memory
+    // (default), radix for a device buffer; 2 / 3 bins for any output: sorted
+    // order then the line writer / fused, for tests and A/B)
+    if (grep && all && (ws->grep_bins >= 2 || (to_host && ws->grep_bins == 1)) && n <= 0xFFFFFFFFull) {
         bool over = false;
         uint8_t* o = to_host ? hout : ws->out.as<uint8_t>();
         if (int e = grep_bin_reduce(ws, r, nreduce, o, h_offsets, &over, ws->grep_bins != 2, s)) return e;

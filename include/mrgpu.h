@@ -237,9 +237,12 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        for compatibility: every value runs the hand-written
  *                                        LSD passes), tie_rank (0: grep's tied runs
  *                                        merge-sorted together instead of ranked per run),
- *                                        grep_bins (0: grep's reduce by the radix passes +
- *                                        tie ranking + line writer instead of the bucketed
- *                                        sort fused with the output)
+ *                                        grep_bins (grep reduce: 1 = default, bins sorted in
+ *                                        LDS and written out by the same workgroups when the
+ *                                        lines go to pinned host memory, else the radix
+ *                                        passes; 0 = radix passes + tie ranking + line
+ *                                        writer always; 2 / 3 = bins for any output, sorted
+ *                                        order then the line writer / fused)
  *                                        reduce sort variants
  *   grep_literal (1: on)                 grep patterns with regexp metacharacters matched as
  *                                        literals (QuoteMeta) instead of refused with MRG_EINVAL

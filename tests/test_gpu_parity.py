@@ -59,10 +59,39 @@ def test_wc_edge_cases(wctx, name):
     check(wctx, "wc", cases.edge_cases()[name])
 
 
+@pytest.fixture(scope="module")
+def ctx_grep_bins():
+    """grep reduce by the bins for a device output too (option grep_bins = 3;
+    by default the bins serve mrg_run_job's output into pinned host memory and
+    mrg_reduce_all keeps the radix path)."""
+    from mrgpu import Context
+    c = Context(0)
+    c.set_option("grep_bins", 3)
+    yield c
+    c.close()
+
+
 @pytest.mark.parametrize("name", sorted(cases.grep_edge_cases()))
 def test_grep_edge_cases(ctx, name):
     files, pat = cases.grep_edge_cases()[name]
     check(ctx, "grep:" + pat.decode("utf-8", "surrogateescape"), files, nreduces=(1, 10))
+
+
+@pytest.mark.parametrize("name", sorted(cases.grep_edge_cases()))
+def test_grep_edge_cases_bins(ctx_grep_bins, name):
+    files, pat = cases.grep_edge_cases()[name]
+    check(ctx_grep_bins, "grep:" + pat.decode("utf-8", "surrogateescape"), files, nreduces=(1, 10))
+
+
+@pytest.mark.parametrize("name", ["basic", "tied_lines", "chunk_seams", "long_lines_many_hits", "shared_prefix_70"])
+def test_grep_run_job_host_output(ctx, name):
+    """mrg_run_job's default path (lines into pinned host memory: the bins fused
+    with the output) against the oracle."""
+    files, pat = cases.grep_edge_cases()[name]
+    for R in (1, 10):
+        got = ctx.run_job(MRG_APP_GREP, b"\n".join(files), pattern=pat, nreduce=R)
+        want = O.c_partitioned("grep:" + pat.decode("utf-8", "surrogateescape"), [b"\n".join(files)], R)
+        assert got == want, f"{name} R={R}"
 
 
 @pytest.mark.parametrize("pat", [b"a.b", b"x+y", b"(q)", b"[z]", b"^s", b"e$", b"w*", b"u?", b"{2}", b"p|q", "ά\\d".encode()])
@@ -645,12 +674,13 @@ def test_grep_edge_cases_radix_reduce(ctx_grep_radix, name):
     check(ctx_grep_radix, "grep:" + pat.decode("utf-8", "surrogateescape"), files, nreduces=(1, 10))
 
 
-@pytest.mark.parametrize("mode", [1, 2])
+@pytest.mark.parametrize("mode", [3, 2])
 def test_grep_bins_many_lines(mode):
     """The bucketed grep reduce over ~10^5 distinct matching lines (hundreds of
     bins, partitions R = 1 / 10 / 64 / 1000, some empty), tied 16-byte prefixes,
-    lines of 1-3000 bytes, against the oracle; mode 1 (default): bins sorted,
-    then the line writer; mode 2: the sorting workgroups write the lines."""
+    lines of 1-3000 bytes, against the oracle; mode 3: the sorting workgroups
+    write the lines (the default for host output); mode 2: bins sorted, then
+    the line writer."""
     import random
     from mrgpu import Context
     rnd = random.Random(5)
