@@ -13,6 +13,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <functional>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -662,9 +663,13 @@ static void print_stamps(mrg_ctx* c, const char* what, uint32_t nblocks, uint32_
 // spills, evenly over the buckets; its dictionary hits and aggregated tail
 // become the records the final dictionary is built from.  Only speed depends
 // on the dictionary: every key it misses is counted exactly through the spill.
+// keep_if (warm start): the map's counters are read first and *kept set when
+// keep_if(hit fraction) holds; the sample's aggregation, only needed to build a
+// new dictionary, is then skipped (~45 us per split).
 static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win, uint32_t nwin, LetterTables lt,
                        bool with_dict, uint64_t* nrec_out, double* spill_rate = nullptr, const uint8_t* host = nullptr,
-                       double* hit_frac = nullptr) {
+                       double* hit_frac = nullptr, const std::function<bool(double)>* keep_if = nullptr,
+                       bool* kept = nullptr) {
     const uint64_t stride = ((len - win) / nwin) & ~15ull;
     const uint64_t sn = (uint64_t)nwin * (win + 16);
     HCHK(c, c->sample.ensure(sn + 64));
@@ -695,6 +700,19 @@ static int sample_pass(mrg_ctx* c, const uint8_t* in, uint64_t len, uint64_t win
     // the spill layout was sized for the split's workgroup count (ensure_spill): never launch more
     const uint32_t g = wc_map_grid(sn, (int)c->spill_nwg);
     if (!launch_wc_map((const uint8_t*)c->sample.p, sn, t, lt, (int)g, 0, c->s)) return fail(c, MRG_EINVAL, "sample too large");
+    if (keep_if) {  // the map's counters decide whether the aggregation is needed at all
+        HCHK(c, hipGetLastError());
+        if ((rc = read_counters(c))) return rc;
+        const double words = (double)(c->h_ctr->dict_hits + c->h_ctr->spilled + c->h_ctr->spill_ovf);
+        const double frac = words > 0 ? (double)c->h_ctr->dict_hits / words : 0.0;
+        if (spill_rate) *spill_rate = (double)(c->h_ctr->spilled + c->h_ctr->spill_ovf) / (double)sn;
+        if (hit_frac) *hit_frac = frac;
+        *kept = (*keep_if)(frac);
+        if (*kept) {
+            *nrec_out = 0;
+            return MRG_OK;
+        }
+    }
     launch_wc_agg(t, c->map_mode & 512, 2, false, c->s);
     if (with_dict) launch_dict_emit(t, g, c->s);
     HCHK(c, hipGetLastError());
@@ -759,15 +777,19 @@ static int build_dict(mrg_ctx* c, const uint8_t* in, uint64_t len, LetterTables 
     c->dict_fresh = true;
     if (target > small) {
         double rate = 0, frac = 0;
-        if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, target / win), lt, true, &nrec, &rate,
-                              host, &frac)))
-            return rc;
         // a warm dictionary that still hits this split's sample about as well as it
-        // hit its own split is kept: the candidate sort and placement are skipped
-        // (or within half a point of it: the mini dictionary hits ~13 % of C5's
-        // words, where 3 % relative is sample noise and a rebuild costs ~1 ms)
-        const bool keep = warm && c->dict_keep > 0 && c->dict_frac_built > 0 &&
-                          (frac >= c->dict_keep * c->dict_frac_built || frac >= c->dict_frac_built - 0.005);
+        // hit its own split is kept: the sample's aggregation, the candidate sort
+        // and the placement are skipped (or within half a point of it: the mini
+        // dictionary hits ~13 % of C5's words, where 3 % relative is sample noise
+        // and a rebuild costs ~1 ms)
+        const bool may_keep = warm && c->dict_keep > 0 && c->dict_frac_built > 0;
+        const std::function<bool(double)> keep_if = [&](double f) {
+            return f >= c->dict_keep * c->dict_frac_built || f >= c->dict_frac_built - 0.005;
+        };
+        bool keep = false;
+        if ((rc = sample_pass(c, in, len, win, (uint32_t)std::max<uint64_t>(1, target / win), lt, true, &nrec, &rate,
+                              host, &frac, may_keep ? &keep_if : nullptr, &keep)))
+            return rc;
         c->dict_fresh = !keep;
         if (!keep && nrec && (rc = dict_from_recs(c, nrec, mini))) return rc;
         // Spill streams hold 0.094 8-byte records per input byte at scale 1 (C2
