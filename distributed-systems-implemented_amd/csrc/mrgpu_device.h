@@ -363,9 +363,6 @@ __device__ __forceinline__ uint32_t utf8_mask16(const lds_u8* slot, uint32_t q0,
 // of LDS free during the call (leads as u16 at [0, 768), the 64 masks at
 // [768, 1024)); more than 384 leads: the serial loop.  Wave-uniform call.
 constexpr uint32_t kWaveLeads = 384;
-#ifndef MRG_UTF8_PAIRS
-#define MRG_UTF8_PAIRS 0
-#endif
 __device__ __forceinline__ uint32_t utf8_mask16_wave(const lds_u8* slot, uint32_t lane, lds_u8* scratch, LdsLetters L) {
     const uint32_t q0 = 16 * lane;
     const lds_u32* s4 = (const lds_u32*)(slot + q0);
@@ -398,19 +395,6 @@ __device__ __forceinline__ uint32_t utf8_mask16_wave(const lds_u8* slot, uint32_
                 __hip_atomic_fetch_or(&M[ow + 1], bits >> 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
     };
-#if MRG_UTF8_PAIRS
-    // two leads per lane per pass, both chains (list entry -> rune bytes ->
-    // table word) in flight together: half the passes' dependent round trips
-    for (uint32_t p = 0; p < total; p += 128) {
-        const bool h1 = p + lane < total, h2 = p + 64 + lane < total;
-        const uint32_t e1 = h1 ? lst[p + lane] : 0u, e2 = h2 ? lst[p + 64 + lane] : 0u;
-        const uint32_t w1 = *(const lds_u32_unaligned*)(slot + e1), w2 = *(const lds_u32_unaligned*)(slot + e2);
-        const LeadRune r1 = lead_decode(w1), r2 = lead_decode(w2);
-        const uint32_t t1 = lead_word(r1, L), t2 = lead_word(r2, L);
-        if (h1) mark(e1, r1, t1);
-        if (h2) mark(e2, r2, t2);
-    }
-#else
     for (uint32_t p = 0; p < total; p += 64) {
         if (p + lane < total) {
             const uint32_t e = lst[p + lane];
@@ -418,7 +402,6 @@ __device__ __forceinline__ uint32_t utf8_mask16_wave(const lds_u8* slot, uint32_
             mark(e, r, lead_word(r, L));
         }
     }
-#endif
     wave_sync();
     return m | M[lane];
 }
