@@ -676,7 +676,7 @@ def test_grep_edge_cases_radix_reduce(ctx_grep_radix, name):
 
 @pytest.mark.parametrize("mode", [3, 2])
 def test_grep_bins_many_lines(mode):
-    """The bucketed grep reduce over ~10^5 distinct matching lines (hundreds of
+    """The bucketed grep reduce over ~3 x 10^5 distinct matching lines (hundreds of
     bins, partitions R = 1 / 10 / 64 / 1000, some empty), tied 16-byte prefixes,
     lines of 1-3000 bytes, against the oracle; mode 3: the sorting workgroups
     write the lines (the default for host output); mode 2: bins sorted, then
@@ -685,7 +685,7 @@ def test_grep_bins_many_lines(mode):
     from mrgpu import Context
     rnd = random.Random(5)
     lines = []
-    for i in range(120_000):
+    for i in range(300_000):  # > 262 144 distinct lines: 8192 splitter samples (the register-blocked sort)
         k = rnd.random()
         if k < 0.3:    # shared 24-byte prefix: ties past the entries' first 24 bytes
             lines.append(b"distributed systems are h" + str(rnd.randrange(10**6)).encode())
