@@ -68,6 +68,13 @@ struct ReduceWs {
     // grep (every partition): the bucketed sort fused with the output
     // (grep_bin_reduce); off: the radix passes + tie ranking + line writer
     int grep_bins = 1;  // see reduce_format
+    // grep bins: the previous reduce's splitters, reused for a reduce of similar
+    // size whose bins all fit the LDS sort (a worker's map tasks are alike; the
+    // 8192-key sample sort is the bin path's largest serial step, ~146 us)
+    DBuf gb_spl;
+    uint32_t gb_nbins = 0, gb_pbits = 0;
+    uint64_t gb_n = 0;
+    bool gb_ok = false, gb_warm = true;
     RadixWs* rx = nullptr;
     ScanWs scan;                   // look-back state of the hand-written scans (mrgpu_scan.h)
 };
@@ -85,7 +92,15 @@ void reduce_ws_set_bin_sort(ReduceWs* w, bool on) { w->bin_sort = on; }
 void reduce_ws_set_prefix32(ReduceWs* w, bool on) { w->prefix32 = on; }
 void reduce_ws_set_own_sort(ReduceWs* w, bool on) { w->own_sort = on; }
 void reduce_ws_set_tie_rank(ReduceWs* w, bool on) { w->tie_rank = on; }
-void reduce_ws_set_grep_bins(ReduceWs* w, int v) { w->grep_bins = v; }
+void reduce_ws_set_grep_bins(ReduceWs* w, int v) {
+    if (v < 0) {  // -1: bins with fresh splitters every reduce (no warm start)
+        w->grep_bins = 1;
+        w->gb_warm = false;
+        return;
+    }
+    w->grep_bins = v;
+    w->gb_warm = true;
+}
 
 ReduceWs* reduce_ws_new() {
     ReduceWs* w = new ReduceWs();
@@ -96,7 +111,7 @@ ReduceWs* reduce_ws_new() {
 
 void reduce_ws_free(ReduceWs* w) {
     if (!w) return;
-    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek, &w->bins, &w->runs};
+    DBuf* bs[] = {&w->perm_a, &w->perm_b, &w->key_a, &w->key_b, &w->lineoff, &w->out, &w->flags, &w->sel, &w->offs, &w->ext, &w->tiek, &w->bins, &w->runs, &w->gb_spl};
     for (DBuf* b : bs) b->release();
     if (w->h_pinned) hipHostFree(w->h_pinned);
     radix_ws_free(w->rx);
@@ -1667,6 +1682,7 @@ __global__ void __launch_bounds__(NT) gb_sort_emit_kernel(Recs r, const uint64_t
             if (flag_over && tid == 0) atomicOr(&flags[1], 1ull);
             continue;
         }
+        if (flag_over && tid == 0) atomicOr(&flags[0], 1ull);  // a bin past the LDS sort's size: resample next time
         uint32_t P = 1;
         while (P < m) P <<= 1;
         const uint32_t s0 = start[bin];
@@ -1980,13 +1996,12 @@ static int grep_bin_reduce(ReduceWs* ws, const Recs& r, uint32_t nreduce, uint8_
     const uint32_t G = (uint32_t)std::min<uint64_t>(kGbGroups, (n + 4095) / 4096);
     // scratch: key64 (key_b), idx (perm_a); bins: H, HB, tot, btot, start, bstart, spl, kbin, poff
     const size_t hb = (size_t)G * nbins * 4, hbb = (size_t)G * nbins * 8;
-    const size_t need = hbb + hb + (size_t)nbins * (4 + 8 + 4 + 8 + 16) + 8 + n * 2 + 16 + (size_t)(nreduce + 1) * 8 + 256;
+    const size_t need = hbb + hb + (size_t)nbins * (4 + 8 + 4 + 8) + 8 + n * 2 + 16 + (size_t)(nreduce + 1) * 8 + 256;
     RCHK(ws->bins.ensure(need));
     uint8_t* p8 = ws->bins.as<uint8_t>();
     unsigned long long* HB = (unsigned long long*)p8;            p8 += hbb;
     unsigned long long* btot = (unsigned long long*)p8;          p8 += (size_t)nbins * 8;
     unsigned long long* bstart = (unsigned long long*)p8;        p8 += (size_t)nbins * 8 + 8;
-    Key128* spl = (Key128*)p8;                                    p8 += (size_t)nbins * 16;
     unsigned long long* poff = (unsigned long long*)p8;          p8 += (size_t)(nreduce + 1) * 8;
     uint32_t* H = (uint32_t*)p8;                                  p8 += hb;
     uint32_t* tot = (uint32_t*)p8;                                p8 += (size_t)nbins * 4;
@@ -1998,7 +2013,11 @@ static int grep_bin_reduce(ReduceWs* ws, const Recs& r, uint32_t nreduce, uint8_
     const uint32_t nparts = nreduce;
     RCHK(hipMemsetAsync(poff, 0xFF, (size_t)nparts * 8, s));
     gb_key_kernel<<<grid_for(n), 256, 0, s>>>(r, pbits, key);
-    gb_sample_kernel<<<1, 1024, 0, s>>>(key, n, S, nbins, spl);
+    RCHK(ws->gb_spl.ensure((size_t)kGbBinMax * sizeof(Key128)));
+    Key128* spl = ws->gb_spl.as<Key128>();
+    const bool reuse = ws->gb_warm && ws->gb_ok && nbins == ws->gb_nbins && pbits == ws->gb_pbits &&
+                       n >= ws->gb_n / 2 && n <= 2 * ws->gb_n;
+    if (!reuse) gb_sample_kernel<<<1, 1024, 0, s>>>(key, n, S, nbins, spl);
     gb_count_kernel<<<G, 1024, 0, s>>>(r, key, spl, nbins, kbin, H, HB);
     gb_offsets_kernel<<<(nbins + 3) / 4, 256, 0, s>>>(H, HB, G, nbins, tot, btot);
     gb_starts_kernel<<<1, 1024, 0, s>>>(tot, btot, nbins, start, bstart);
@@ -2024,9 +2043,13 @@ static int grep_bin_reduce(ReduceWs* ws, const Recs& r, uint32_t nreduce, uint8_
     gb_part_offsets_kernel<<<1, 64, 0, s>>>(poff, bstart + nbins, nparts, ws->offs.as<uint64_t>());
     RCHK(hipGetLastError());
     RCHK(hipMemcpyAsync(h_offsets, ws->offs.p, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, s));
-    RCHK(hipMemcpyAsync(ws->h_pinned + 1, flags + 1, 8, hipMemcpyDeviceToHost, s));
+    RCHK(hipMemcpyAsync(ws->h_pinned + 8, flags, 16, hipMemcpyDeviceToHost, s));  // flags 0 (big bins), 1 (over)
     RCHK(hipStreamSynchronize(s));
-    *over = ws->h_pinned[1] != 0;
+    *over = ws->h_pinned[9] != 0;
+    ws->gb_ok = ws->h_pinned[8] == 0 && ws->h_pinned[9] == 0;
+    ws->gb_nbins = nbins;
+    ws->gb_pbits = pbits;
+    ws->gb_n = n;
     return 0;
 }
 

@@ -333,10 +333,6 @@ constexpr uint32_t kLongReserve = 256;
 #define MRG_STAGE2_DRAIN 1
 #endif
 constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
-// the bucket aggregator's round-0 8-byte streams: two blocks in flight (1) or one (0)
-#ifndef MRG_AGG_DEEP
-#define MRG_AGG_DEEP 0
-#endif
 // UTF-8 chunks: leads decoded wave-compacted (utf8_mask16_wave) or by the
 // per-lane loop (utf8_mask16)
 #ifndef MRG_UTF8_WAVE
@@ -1638,34 +1634,16 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                 }
             }
         };
-        // the block after next in flight too (MRG_AGG_DEEP, round 0's 8-byte
-        // streams: the stream reads, not the table, set the round's time)
-        constexpr bool kDeep = MRG_AGG_DEEP && !kMid && kRound0;
-        uint4 nx2[kDeep ? kAggUnroll : 1];
-        auto advance = [&](uint32_t& jj, uint32_t& oo, uint32_t& cc) {
-            while (jj < js && oo >= cc) {
-                jj++;
-                oo = 0;
-                cc = jj < js ? __builtin_amdgcn_readlane(vcnt, jj) : 0u;
-            }
-        };
         load(j, off, cnt, cur);
-        // (j1, off1, cnt1): the block after cur's (kDeep: its loads already in nxt)
-        uint32_t j1 = j, off1 = off + kAggBlock, cnt1 = cnt;
-        advance(j1, off1, cnt1);
-        if constexpr (kDeep) load(j1, off1, cnt1, nxt);
         while (j < js) {
-            uint32_t j2 = j1, off2 = off1, cnt2 = cnt1;  // where cur moves next
-            if constexpr (kDeep) {
-                uint32_t j3 = j1, off3 = off1 + kAggBlock, cnt3 = cnt1;
-                advance(j3, off3, cnt3);
-                load(j3, off3, cnt3, nx2);
-                j1 = j3;
-                off1 = off3;
-                cnt1 = cnt3;
-            } else {
-                load(j2, off2, cnt2, nxt);
+            // next block's position and loads
+            uint32_t j2 = j, off2 = off + kAggBlock, cnt2 = cnt;
+            while (j2 < js && off2 >= cnt2) {
+                j2++;
+                off2 = 0;
+                cnt2 = j2 < js ? __builtin_amdgcn_readlane(vcnt, j2) : 0u;
             }
+            load(j2, off2, cnt2, nxt);
             uint32_t h[kAggUnroll];
 #pragma unroll
             for (uint32_t u = 0; u < kAggUnroll; u++) h[u] = fold32(cur[u].x, cur[u].y, cur[u].z, cur[u].w);
@@ -1818,19 +1796,9 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
             }
 #pragma unroll
             for (uint32_t u = 0; u < kAggUnroll; u++) cur[u] = nxt[u];
-            if constexpr (kDeep) {
-#pragma unroll
-                for (uint32_t u = 0; u < kAggUnroll; u++) nxt[u] = nx2[u];
-            }
             j = j2;
             off = off2;
             cnt = cnt2;
-            if constexpr (!kDeep) {
-                j1 = j;
-                off1 = off + kAggBlock;
-                cnt1 = cnt;
-                advance(j1, off1, cnt1);
-            }
         }
     }
 }

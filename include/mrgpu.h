@@ -242,7 +242,9 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *                                        lines go to pinned host memory, else the radix
  *                                        passes; 0 = radix passes + tie ranking + line
  *                                        writer always; 2 / 3 = bins for any output, sorted
- *                                        order then the line writer / fused)
+ *                                        order then the line writer / fused; -1 = the
+ *                                        default without reusing the previous reduce's
+ *                                        splitters)
  *                                        reduce sort variants
  *   grep_literal (1: on)                 grep patterns with regexp metacharacters matched as
  *                                        literals (QuoteMeta) instead of refused with MRG_EINVAL

@@ -704,6 +704,27 @@ def test_grep_bins_many_lines(mode):
         check(c, "grep:distributed", [many], nreduces=(1, 10))
 
 
+def test_grep_bins_splitter_reuse():
+    """A context reuses its last grep reduce's splitters for a reduce of similar
+    size: a split whose lines sort nothing like the previous one's (every line
+    beyond the old splitters: one bin far past the LDS sort) is still exact (the
+    bin is flagged and the radix path redoes the reduce), and the context then
+    samples afresh."""
+    import random
+    from mrgpu import Context
+    rnd = random.Random(9)
+
+    def corpus(first: bytes):
+        return b"".join(first + bytes(rnd.choice(b"abcdefghij") for _ in range(rnd.randrange(5, 30)))
+                        + b" distributed " + str(i).encode() + b"\n" for i in range(60_000))
+    a, z = corpus(b"a"), corpus(b"zz")
+    with Context(0) as c:
+        for R in (1, 7):
+            for data in (a, z, z, a):
+                got = c.run_job(MRG_APP_GREP, data, pattern=b"distributed", nreduce=R)
+                assert got == O.c_partitioned("grep:distributed", [data], R)
+
+
 @pytest.mark.parametrize("path", ["default", "sorted"])
 def test_grep_record_counts_one_per_line(ctx, ctx_sorted_hits, path):
     """The map's grep records count every matching line occurrence exactly once
