@@ -218,6 +218,15 @@ __device__ __forceinline__ void wait_vmem_extra(uint32_t xv) {
 
 // The staged (kS) loop: the flush's 4 stores and the DMA follow the awaited DMA
 __device__ __forceinline__ void wait_vmem_iter_staged() { asm volatile("s_waitcnt vmcnt(5)" ::: "memory"); }
+// kS: a write-combining round every kFlushEvery chunk trips (a round is two
+// workgroup barriers, which cost more than its stores: 2.2 of 11.4 ms per 10 GB
+// of C5, profiles/mapprobe_r06_c5_staged_modes.txt); between rounds a group past
+// its 4 records stores the rest directly.  2 measured 4 % faster than 1, 3 the
+// same as 2.
+#ifndef MRG_FLUSH_EVERY
+#define MRG_FLUSH_EVERY 2
+#endif
+constexpr uint32_t kFlushEvery = MRG_FLUSH_EVERY;
 
 // kS: an 8-byte record bound for stream position pos of bucket b (o8: its store
 // offset, kOutOfRange if the lane has none) joins the stream's LDS group when
@@ -362,7 +371,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     // 32 = spill cursors but no stores, 8 = dictionary counters not updated,
     // 64 = non-ASCII chunks classified by the ASCII rule (no rune decoding);
     // 0x100 / 0x4000 / 0x8000 (exact) = input loads with the default policy /
-    // sc1 / sc0 sc1 instead of nt.  (Measured and removed, DESIGN.md §6: the 4
+    // sc1 / sc0 sc1 instead of nt; staged kernel only: 0x10000 = the write-combining
+    // round without its stores, 0x20000 = no round.  (Measured and removed, DESIGN.md §6: the 4
     // hottest keys counted by ballots into SGPRs; key bytes by three aligned
     // 8-byte reads; a single-choice dictionary lookup.)
     __shared__ MapLdsT<NW, NB, kS> L;
@@ -458,8 +468,8 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     for (uint32_t c = c0; kS ? trip < ktrips : c < cend;
          c += stride, cs += cstep, kf = k, k = k == kRing - 1 ? 0 : k + 1, trip++) {
         // chunk c's DMA (issued two iterations ago) has landed
-        if constexpr (kS) wait_vmem_extra<5>(xv);
-        else wait_vmem_extra<kVmemPerIter>(xv);
+        if constexpr (kS && (mode & 0x20000) == 0 && kFlushEvery == 1) wait_vmem_extra<5>(xv);
+        else wait_vmem_extra<kVmemPerIter>(xv);  // (kFlushEvery > 1: a round adds its stores to xv)
         xv = 0;
         lds_u8* buf = (lds_u8*)L.ring[wv][k];
         const uint32_t bufa = ring0 + k * kSlotStride;  // = lds_addr(buf)
@@ -1020,7 +1030,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 }
             }
         }
-        if constexpr (kS) {
+        if constexpr (kS && (mode & 0x20000) == 0) if (kFlushEvery == 1 || trip % kFlushEvery == kFlushEvery - 1) {
             // Write-combining round: after a barrier every stream whose LDS group
             // holds 4 records writes them as one 32-byte store (a full sector; the
             // 2048-bucket layout's 4096 streams per workgroup otherwise leave the
@@ -1037,10 +1047,11 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                 const uint32_t f = cc - ((cc - (uint32_t)L.fl[b]) & 0xFFFFu);
                 const bool grp = cc - f >= 4u;
                 const bool whole = grp && f + 4u <= sub8;
+                const bool put = whole && (mode & 0x10000) == 0;  // (ablation 0x10000: the round without its stores)
                 const u32x4 lo = *(const lds_uint4*)&L.stage8[b][0], hi = *(const lds_uint4*)&L.stage8[b][2];
                 const uint32_t o = (__umul24(b, sub8) + f) * 8u;
-                __builtin_amdgcn_raw_buffer_store_b128(lo, rs8, whole ? o : kOutOfRange, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b128(hi, rs8, whole ? o + 16u : kOutOfRange, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(lo, rs8, put ? o : kOutOfRange, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b128(hi, rs8, put ? o + 16u : kOutOfRange, 0, 0);
                 if (grp && !whole) {  // the group reaches past the stream's capacity: its records below it
                     for (uint32_t j = 0; j < 4u; j++)
                         if (f + j < sub8) t.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
@@ -1050,6 +1061,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             }
             if (__ballot(rare)) wait_vmem_all();  // (other VMEM operations: the counted wait no longer holds)
             __syncthreads();  // the groups and fl are reused by the next round's appends
+            if constexpr (kFlushEvery > 1) xv += 2;  // (the next wait: vmcnt(5), as with a round every trip)
         }
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
@@ -1070,7 +1082,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
         for (uint32_t b = tid; b < (uint32_t)NB; b += kT) {
             const uint32_t cc = curs[b];
             const uint32_t f = cc - ((cc - (uint32_t)L.fl[b]) & 0xFFFFu);
-            for (uint32_t j = 0; f + j < cc; j++)
+            for (uint32_t j = 0; f + j < cc && j < 4u; j++)  // (kFlushEvery > 1: a full group, the rest stored directly)
                 if (f + j < sub8) t.sp.pool8[((uint64_t)blockIdx.x * NB + b) * sub8 + f + j] = L.stage8[b][j];
         }
     }
@@ -2207,9 +2219,22 @@ bool launch_wc_map(const uint8_t* in, uint64_t n, const Tables& t, LetterTables 
     return true;
 #endif
     if (t.sp.nb == kSpillBucketsHi) {  // high-cardinality layout (ablation modes apply to the default one only)
-        if (t.hi_staged)  // the mini dictionary: its LDS write-combines the 8-byte spill streams
-            wc_map_kernel<0, kWavesPerWG, kSpillBucketsHi, true><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
-        else
+        if (t.hi_staged) {  // the mini dictionary: its LDS write-combines the 8-byte spill streams
+            switch (mode) {  // ablation modes of the staged kernel (mapprobe --opt spill_buckets=2048)
+#ifndef MRG_NO_STAGED_MODES
+#define MRG_MAP_MODE(M)                                                                                           \
+    case M:                                                                                                       \
+        wc_map_kernel<M, kWavesPerWG, kSpillBucketsHi, true><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt); \
+        break;
+                // 0x10000: the write-combining round without its stores; 0x20000:
+                // no round (no barriers; the 8-byte records stored one by one)
+                MRG_MAP_MODE(2) MRG_MAP_MODE(16) MRG_MAP_MODE(32) MRG_MAP_MODE(32 | 0x10000) MRG_MAP_MODE(32 | 0x20000)
+                MRG_MAP_MODE(0x10000) MRG_MAP_MODE(0x20000)
+#undef MRG_MAP_MODE
+#endif
+                default: wc_map_kernel<0, kWavesPerWG, kSpillBucketsHi, true><<<(unsigned)g, kThreads, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
+            }
+        } else
             wc_map_kernel<0, 12, kSpillBucketsHi><<<(unsigned)g, 12 * kWave, 0, s>>>(in, n, cb, ce, ctail, rs, t, lt);
         return true;
     }
