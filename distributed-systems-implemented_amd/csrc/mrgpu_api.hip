@@ -293,6 +293,10 @@ struct mrg_ctx {
     // same-process T(1) for the weak-scaling efficiency: the rank's own split,
     // every partition reduced locally)
     bool skip_exchange = false;
+    // (tests) mrg_exchange runs its RCCL collectives on a one-rank communicator
+    // too, instead of keeping every key locally: the calls, the count and
+    // displacement arrays and the unpack, on one GPU (RCCL refuses two ranks on one)
+    bool exch_force_rccl = false;
     // Host-input splits of at least ingest_min bytes are copied in pieces of
     // ~ingest_piece bytes on a second stream, each piece mapped as soon as it and
     // the next one (look-ahead) are resident.
@@ -1541,6 +1545,7 @@ int mrg_set_option(mrg_ctx* c, const char* name, int64_t v) {
     else if (!strcmp(name, "dict_sample_bytes")) c->dict_sample_bytes = v > 0 ? (uint64_t)v : (16ull << 20);
     else if (!strcmp(name, "rec_cap")) c->rec_cap = v > 0 ? (uint64_t)v : (1u << 21);
     else if (!strcmp(name, "skip_exchange")) c->skip_exchange = v > 0;
+    else if (!strcmp(name, "exch_force_rccl")) c->exch_force_rccl = v > 0;
     else if (!strcmp(name, "exchange_timeout_ms")) c->exch_timeout_ms = v > 0 ? v : 120000;
     else if (!strcmp(name, "ingest_piece")) c->ingest_piece = v > 0 ? (uint64_t)v : (256ull << 20);
     else if (!strcmp(name, "ingest_min")) c->ingest_min = v > 0 ? (uint64_t)v : (64ull << 20);
@@ -2339,7 +2344,7 @@ int mrg_exchange(mrg_ctx* c, const mrg_parts* local, mrg_parts** owned) {
     int rc;
     if ((rc = bind(c))) return rc;
     const int P = c->nranks;
-    if (!c->comm || P == 1) {  // single rank: everything is owned; copy through aggregate for a fresh object
+    if (!c->comm || (P == 1 && !c->exch_force_rccl)) {  // single rank: everything is owned; copy through aggregate
         return aggregate(c, {local->r}, local->app, local->nreduce, owned);
     }
     HCHK(c, hipEventRecord(c->ev[6], c->s));

@@ -226,6 +226,9 @@ int mrg_get_stats(const mrg_ctx* ctx, mrg_stats* out);
  *   skip_exchange                        CHANGES RESULTS: mrg_run_job with nranks > 1 skips
  *                                        the shuffle and reduces only this rank's own split
  *                                        (bench.py's same-process T(1); never for real jobs)
+ *   exch_force_rccl (1: on)              mrg_exchange runs its RCCL collectives on a
+ *                                        one-rank communicator too (tests: the collective
+ *                                        calls on one GPU); same results
  *   exchange_timeout_ms                  deadline of a collective phase (mrg_exchange;
  *                                        mrg_comm_init gets 4x; default 120000): past it the
  *                                        process prints the phase and exits with status 124

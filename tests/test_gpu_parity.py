@@ -597,6 +597,37 @@ def test_exchange_rccl_one_rank():
         assert c2.run_job(MRG_APP_WC, files[0], nreduce=6) == O.c_partitioned("wc", files, 6)
 
 
+@pytest.mark.parametrize("app,R", [("wc", 6), ("wc", 64), ("grep:distributed", 10)])
+def test_exchange_rccl_collectives_one_rank(app, R):
+    """The RCCL collectives of mrg_exchange themselves (ncclAllToAll of the
+    P x 2 counts, then one group of two ncclAllToAllv: records and long-key
+    bytes) on a one-rank communicator (option exch_force_rccl): every key comes
+    back through RCCL, unpacked and re-aggregated, exact against the oracle.
+    Long UTF-8 keys put bytes in the arena stream too."""
+    from mrgpu import Context
+    name, pat = (app.split(":") + [None])[:2]
+    files = cases.synthetic(C.KIND_UTF8, 20000, [700_000], 29, 0.001)
+    if pat:  # matching lines, some tied on their first bytes
+        lines = files[0].split(b"\n")
+        for i in range(0, len(lines), 37):
+            lines[i] += b" distributed"
+        files = [b"\n".join(lines)]
+    want = O.c_partitioned(app, files, R)
+    assert sum(len(w) for w in want) > 0
+    with Context(0) as c2:
+        c2.comm_init(Context.unique_id(), 1, 0)
+        c2.set_option("exch_force_rccl", 1)
+        kind = MRG_APP_WC if name == "wc" else MRG_APP_GREP
+        p = c2.map(kind, files[0], nreduce=R, **({"pattern": pat.encode()} if pat else {}))
+        q = c2.exchange(p)
+        st = c2.stats()
+        assert st["rccl_nranks"] == 1 and st["rccl_rank"] == 0
+        assert st["exchange_a2a_ms"] > 0 and st["shuffle_recv_records"] > 0
+        assert c2.reduce_all(q) == want
+        p.free()
+        q.free()
+
+
 @pytest.mark.parametrize("P,app,R", [(2, "wc", 10), (3, "wc", 64), (4, "grep:distributed", 10), (8, "wc", 64)])
 def test_exchange_group_multi_rank(P, app, R):
     """The P > 1 shuffle (owner counts, pack per owner, all-to-all, unpack with the
