@@ -735,6 +735,40 @@ def test_grep_bins_many_lines(mode):
         check(c, "grep:distributed", [many], nreduces=(1, 10))
 
 
+@pytest.mark.parametrize("bins", [1, -1])
+def test_grep_bins_host_output_many_lines(bins):
+    """mrg_run_job's default grep output, lines written into pinned host memory
+    by the workgroups that sort the bins, over ~10^5 distinct matching lines
+    (~400 bins), with the previous reduce's splitters reused (1) or sampled
+    afresh (-1): tied prefixes, long lines, R = 1 / 10 / 64, and a split whose
+    one tied prefix overflows the bins (the radix path redoes it), then the
+    first split again."""
+    import random
+    from mrgpu import Context
+    rnd = random.Random(11)
+    lines = []
+    for i in range(100_000):
+        k = rnd.random()
+        if k < 0.3:
+            lines.append(b"distributed systems are h" + str(rnd.randrange(10**6)).encode())
+        elif k < 0.33:
+            lines.append(b"y" * rnd.randrange(100, 2000) + b"distributed" + str(i).encode())
+        else:
+            lines.append(bytes(rnd.choice(b"abcdefgh ") for _ in range(rnd.randrange(0, 40))) + b"distributed"
+                         + bytes(rnd.choice(b"xyz") for _ in range(rnd.randrange(0, 8))))
+    data = b"\n".join(lines) + b"\n"
+    many = b"".join(b"distributed tied prefix, one bin %07d\n" % rnd.randrange(10**7) for _ in range(9000))
+    with Context(0) as c:
+        c.set_option("grep_bins", bins)
+        try:
+            for d in (data, many, data):
+                for R in (1, 10, 64):
+                    assert c.run_job(MRG_APP_GREP, d, pattern=b"distributed", nreduce=R) == \
+                        O.c_partitioned("grep:distributed", [d], R), (bins, R, len(d))
+        finally:
+            c.set_option("grep_bins", 1)
+
+
 def test_grep_bins_splitter_reuse():
     """A context reuses its last grep reduce's splitters for a reduce of similar
     size: a split whose lines sort nothing like the previous one's (every line
