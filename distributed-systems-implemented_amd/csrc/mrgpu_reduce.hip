@@ -1806,18 +1806,12 @@ struct GbxEnt {
     uint32_t part, slot;
 };
 
-// MRG_GB_DYN (A/B): workgroups take the next bin from a counter (grab) instead
-// of every gridDim-th bin
-#ifndef MRG_GB_DYN
-#define MRG_GB_DYN 0
-#endif
 template <bool EMIT>
 __global__ void __launch_bounds__(kGbxThreads) gbx_sort_emit_kernel(Recs r, const uint64_t* ext, const uint32_t* idx,
                                                                      const uint32_t* start, const uint32_t* tot,
                                                                      const unsigned long long* bstart, uint32_t nbins,
                                                                      uint8_t* out, uint32_t* perm_out,
-                                                                     uint64_t* off_out, unsigned long long* poff,
-                                                                     unsigned long long* grab) {
+                                                                     uint64_t* off_out, unsigned long long* poff) {
     constexpr uint32_t CAP = kGbxCap, NT = kGbxThreads, PER = CAP / NT, NX = kGbxWords;
     __shared__ GbxEnt E[CAP];
     __shared__ uint64_t X[CAP * NX];  // key bytes 24-63 of slot s at X[NX s, NX s + NX)
@@ -1857,17 +1851,7 @@ __global__ void __launch_bounds__(kGbxThreads) gbx_sort_emit_kernel(Recs r, cons
         }
         return la < lb;
     };
-    __shared__ uint32_t sbin;
-    auto next_bin = [&](uint32_t cur) -> uint32_t {
-        if constexpr (MRG_GB_DYN != 0) {
-            __syncthreads();  // every thread has read the previous bin
-            if (tid == 0) sbin = (uint32_t)atomicAdd(grab, 1ull);
-            __syncthreads();
-            return sbin;
-        }
-        return cur;
-    };
-    for (uint32_t bin = next_bin(blockIdx.x); bin < nbins; bin = next_bin(bin + gridDim.x)) {
+    for (uint32_t bin = blockIdx.x; bin < nbins; bin += gridDim.x) {
         const uint32_t m = tot[bin];
         if (m == 0 || m > CAP) continue;  // (larger bins: gb_sort_emit_kernel)
         uint32_t P = 1;
@@ -2043,13 +2027,13 @@ static int grep_bin_reduce(ReduceWs* ws, const Recs& r, uint32_t nreduce, uint8_
     const uint64_t* ext = ws->ext.as<uint64_t>();
     if (emit) {  // the lines written by the sorting workgroups
         gbx_sort_emit_kernel<true><<<nbins < 256 ? nbins : 256, kGbxThreads, 0, s>>>(r, ext, idx, start, tot, bstart,
-                                                                                   nbins, out, perm, off, poff, flags + 2);
+                                                                                   nbins, out, perm, off, poff);
         gb_sort_emit_kernel<kGbBigCap, kGbBigThreads, kGbBigStage, true><<<nbins < 256 ? nbins : 256, kGbBigThreads, 0,
                                                                           s>>>(
             r, ext, idx, start, tot, bstart, nbins, kGbCap, true, out, perm, off, poff, flags);
     } else {  // sorted order + line offsets, then the line writer over all of them
         gbx_sort_emit_kernel<false><<<nbins < 256 ? nbins : 256, kGbxThreads, 0, s>>>(r, ext, idx, start, tot, bstart,
-                                                                                    nbins, out, perm, off, poff, flags + 2);
+                                                                                    nbins, out, perm, off, poff);
         gb_sort_emit_kernel<kGbBigCap, kGbBigThreads, 16, false><<<nbins < 256 ? nbins : 256, kGbBigThreads, 0, s>>>(
             r, ext, idx, start, tot, bstart, nbins, kGbCap, true, out, perm, off, poff, flags);
         gb_total_kernel<<<1, 64, 0, s>>>(bstart + nbins, off + n);
