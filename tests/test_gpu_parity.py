@@ -597,7 +597,7 @@ def test_exchange_rccl_one_rank():
         assert c2.run_job(MRG_APP_WC, files[0], nreduce=6) == O.c_partitioned("wc", files, 6)
 
 
-@pytest.mark.parametrize("app,R", [("wc", 6), ("wc", 64), ("grep:distributed", 10)])
+@pytest.mark.parametrize("app,R", [("wc", 6), ("wc", 64), ("grep:distributed", 10), ("wc-hi", 64)])
 def test_exchange_rccl_collectives_one_rank(app, R):
     """The RCCL collectives of mrg_exchange themselves (ncclAllToAll of the
     P x 2 counts, then one group of two ncclAllToAllv: records and long-key
@@ -606,7 +606,13 @@ def test_exchange_rccl_collectives_one_rank(app, R):
     Long UTF-8 keys put bytes in the arena stream too."""
     from mrgpu import Context
     name, pat = (app.split(":") + [None])[:2]
-    files = cases.synthetic(C.KIND_UTF8, 20000, [700_000], 29, 0.001)
+    hi = name == "wc-hi"  # C5's shape: the staged 2048-bucket map, ~10^6 distinct keys
+    if hi:
+        name, app = "wc", "wc"
+        voc = C.Vocab(C.KIND_ASCII, 0.8, 2_000_000, 31)
+        files = [bytes(voc.fill_files([12_000_000], [31], C.wc_params(vocab_lo=0, vocab_hi=2_000_000))[0])]
+    else:
+        files = cases.synthetic(C.KIND_UTF8, 20000, [700_000], 29, 0.001)
     if pat:  # matching lines, some tied on their first bytes
         lines = files[0].split(b"\n")
         for i in range(0, len(lines), 37):
@@ -617,8 +623,13 @@ def test_exchange_rccl_collectives_one_rank(app, R):
     with Context(0) as c2:
         c2.comm_init(Context.unique_id(), 1, 0)
         c2.set_option("exch_force_rccl", 1)
+        if hi:
+            c2.set_option("spill_buckets", 2048)
+            c2.set_option("hi_stage", 1)
         kind = MRG_APP_WC if name == "wc" else MRG_APP_GREP
         p = c2.map(kind, files[0], nreduce=R, **({"pattern": pat.encode()} if pat else {}))
+        if hi:
+            assert c2.stats()["spill_buckets"] == 2048
         q = c2.exchange(p)
         st = c2.stats()
         assert st["rccl_nranks"] == 1 and st["rccl_rank"] == 0
