@@ -351,6 +351,14 @@ constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
 #ifndef MRG_LIST_PAIRS
 #define MRG_LIST_PAIRS 0
 #endif
+// Wave priority MRG_PRIO while a batch issues its list, key-byte and
+// dictionary-set reads, 0 after: the SIMD's arbiter then issues a wave's
+// dependent LDS round trips ahead of the other waves' compute, so more of them
+// are in flight (C2 map 6.64-6.71 -> 6.54-6.57 ms, C5 -0.1 ms per 10 GB;
+// profiles/ab_r06_prio.txt; priority 3 no better)
+#ifndef MRG_PRIO
+#define MRG_PRIO 1
+#endif
 __device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint32_t lleft, uint32_t lane) {
     for (uint32_t g = 0; g < lleft; g += kWave)
         if (g + lane < lleft && lbase + g + lane < t.list_cap) t.list[lbase + g + lane] = kListHole;
@@ -582,6 +590,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     // on per-lane outcomes: misses add to a per-lane dummy counter and
                     // hits bump a per-lane dummy cursor.
                     uint32_t e[kBatch];
+                    if constexpr (MRG_PRIO != 0) __builtin_amdgcn_s_setprio(MRG_PRIO);  // (A/B)
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         const uint32_t w = base + lane + 64u * u;
@@ -802,6 +811,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             B[u] = *(const lds_uint4*)((const lds_u8*)dset + a2[u]);
                         }
                         __builtin_amdgcn_sched_barrier(0);  // all 2 * kBatch set reads in flight before the compares
+                        if constexpr (MRG_PRIO != 0) __builtin_amdgcn_s_setprio(0);
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
                             // short key: any of the 4 ways of its two sets; mid key: the single
@@ -836,6 +846,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                                 __hip_atomic_fetch_add((lds_u32*)((lds_u8*)dcnt + cofs), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
                     } else {
+                        if constexpr (MRG_PRIO != 0) __builtin_amdgcn_s_setprio(0);
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
                             hit[u] = false;
