@@ -359,6 +359,12 @@ constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
 #ifndef MRG_PRIO
 #define MRG_PRIO 1
 #endif
+// (A/B) where: 0 the batch's reads (default), 1 through the dictionary count
+// adds, 2 static (odd waves 1, even 0, no toggling), 3 the reads and the fast
+// path's staging + cursor adds, 4 from the batch's reads to the chunk's end
+#ifndef MRG_PRIO_MODE
+#define MRG_PRIO_MODE 1
+#endif
 __device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint32_t lleft, uint32_t lane) {
     for (uint32_t g = 0; g < lleft; g += kWave)
         if (g + lane < lleft && lbase + g + lane < t.list_cap) t.list[lbase + g + lane] = kListHole;
@@ -388,6 +394,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
     const uint32_t tid = threadIdx.x;
     const uint32_t lane = tid & 63;
     const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform (SGPR) for the DMA operands
+    if constexpr (MRG_PRIO != 0 && MRG_PRIO_MODE == 2) {
+        if (wv & 1u) __builtin_amdgcn_s_setprio(1);
+    }
     lds_uint4* dset = (lds_uint4*)L.dset;
     lds_u32* dcnt = (lds_u32*)L.dcnt;
     lds_u32* curs = (lds_u32*)L.curs;
@@ -590,7 +599,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     // on per-lane outcomes: misses add to a per-lane dummy counter and
                     // hits bump a per-lane dummy cursor.
                     uint32_t e[kBatch];
-                    if constexpr (MRG_PRIO != 0) __builtin_amdgcn_s_setprio(MRG_PRIO);  // (A/B)
+                    if constexpr (MRG_PRIO != 0 && MRG_PRIO_MODE != 2) __builtin_amdgcn_s_setprio(MRG_PRIO);
         #pragma unroll
                     for (int u = 0; u < kBatch; u++) {
                         const uint32_t w = base + lane + 64u * u;
@@ -811,7 +820,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             B[u] = *(const lds_uint4*)((const lds_u8*)dset + a2[u]);
                         }
                         __builtin_amdgcn_sched_barrier(0);  // all 2 * kBatch set reads in flight before the compares
-                        if constexpr (MRG_PRIO != 0) __builtin_amdgcn_s_setprio(0);
+                        if constexpr (MRG_PRIO != 0 && (MRG_PRIO_MODE == 0 || MRG_PRIO_MODE == 3)) __builtin_amdgcn_s_setprio(0);
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
                             // short key: any of the 4 ways of its two sets; mid key: the single
@@ -845,8 +854,9 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                             if (cnt_lds)
                                 __hip_atomic_fetch_add((lds_u32*)((lds_u8*)dcnt + cofs), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         }
+                        if constexpr (MRG_PRIO != 0 && MRG_PRIO_MODE == 1) __builtin_amdgcn_s_setprio(0);
                     } else {
-                        if constexpr (MRG_PRIO != 0) __builtin_amdgcn_s_setprio(0);
+                        if constexpr (MRG_PRIO != 0 && MRG_PRIO_MODE != 2 && MRG_PRIO_MODE != 4) __builtin_amdgcn_s_setprio(0);
         #pragma unroll
                         for (int u = 0; u < kBatch; u++) {
                             hit[u] = false;
@@ -877,6 +887,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                     }
                     const uint32_t nm = nmu[kBatch];
                     if (passes == 1 && nm <= (uint32_t)kWave) {
+                        if constexpr (MRG_PRIO != 0 && MRG_PRIO_MODE == 3) __builtin_amdgcn_s_setprio(MRG_PRIO);
                         lds_uint4* stage = (lds_uint4*)buf;
         #pragma unroll
                         for (int u = 0; u < kBatch; u++)
@@ -889,6 +900,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
                         const bool big = (r.z | r.w) != 0;
                         const uint32_t ci = valid ? b + (big ? (uint32_t)NB : 0u) : 2u * NB + lane;
                         const uint32_t pos = __hip_atomic_fetch_add(&curs[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if constexpr (MRG_PRIO != 0 && MRG_PRIO_MODE == 3) __builtin_amdgcn_s_setprio(0);
                         if constexpr ((mode & 32) != 0) {
                             acc += pos;
                             continue;
@@ -1074,6 +1086,7 @@ __global__ void __launch_bounds__(kThreads) wc_map_kernel(const uint8_t* __restr
             __syncthreads();  // the groups and fl are reused by the next round's appends
             if constexpr (kFlushEvery > 1) xv += 2;  // (the next wait: vmcnt(5), as with a round every trip)
         }
+        if constexpr (MRG_PRIO != 0 && MRG_PRIO_MODE == 4) __builtin_amdgcn_s_setprio(0);
         wave_sync();
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // every LDS read of slot kf (the list) has returned
         ds.issue<dma_policy(mode)>(lane, ring0 + kf * kSlotStride);
