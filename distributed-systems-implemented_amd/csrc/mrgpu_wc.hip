@@ -359,6 +359,10 @@ constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
 #ifndef MRG_PRIO
 #define MRG_PRIO 1
 #endif
+// (A/B) the bucket aggregator's first-set lookups and count adds at this priority
+#ifndef MRG_AGG_PRIO
+#define MRG_AGG_PRIO 0
+#endif
 // (A/B) where: 0 the batch's reads (default), 1 through the dictionary count
 // adds, 2 static (odd waves 1, even 0, no toggling), 3 the reads and the fast
 // path's staging + cursor adds, 4 from the batch's reads to the chunk's end
@@ -1471,6 +1475,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
             } else if constexpr (!kMid && (amode & 64) != 0) {
                 // first-set lookups only, each miss its own slow path (sparse tables)
                 uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
+                if constexpr (MRG_AGG_PRIO != 0) __builtin_amdgcn_s_setprio(MRG_AGG_PRIO);
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     base[u] = sbase<AL>(h[u]);
@@ -1486,6 +1491,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
                     else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+                if constexpr (MRG_AGG_PRIO != 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     if (slow[u]) {
@@ -1689,6 +1695,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
             } else if constexpr (!kMid && (amode & 64) != 0) {
                 // first-set lookups only, each miss its own slow path (sparse tables)
                 uint32_t m[kAggUnroll], z[kAggUnroll], base[kAggUnroll];
+                if constexpr (MRG_AGG_PRIO != 0) __builtin_amdgcn_s_setprio(MRG_AGG_PRIO);
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     base[u] = sbase<AL>(h[u]);
@@ -1704,6 +1711,7 @@ __device__ __forceinline__ void agg_pool(AL& A, const Tables& t, const void* poo
                     if constexpr ((amode & 1024) != 0) miss += ci;  // ablation: no count adds
                     else __hip_atomic_fetch_add(&A.sc[ci], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 }
+                if constexpr (MRG_AGG_PRIO != 0) __builtin_amdgcn_s_setprio(0);
 #pragma unroll
                 for (uint32_t u = 0; u < kAggUnroll; u++) {
                     if (slow[u]) {
