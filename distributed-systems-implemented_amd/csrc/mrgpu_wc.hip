@@ -367,7 +367,7 @@ constexpr bool kStage2Drain = MRG_STAGE2_DRAIN != 0;
 // adds, 2 static (odd waves 1, even 0, no toggling), 3 the reads and the fast
 // path's staging + cursor adds, 4 from the batch's reads to the chunk's end
 #ifndef MRG_PRIO_MODE
-#define MRG_PRIO_MODE 1
+#define MRG_PRIO_MODE 4
 #endif
 __device__ __forceinline__ void list_close(const Tables& t, uint64_t lbase, uint32_t lleft, uint32_t lane) {
     for (uint32_t g = 0; g < lleft; g += kWave)
